@@ -1,0 +1,351 @@
+// gsd_capi.hip -- the extern "C" boundary (include/gsd_raster.h).
+//
+// Orchestration of Rasterizer::forward / ::backward (rasterizer_impl.cu:198-434)
+// over caller-owned state buffers.  No device allocation, no hipFree, and one
+// host synchronisation per forward (the num_rendered read the reference also
+// does, rasterizer_impl.cu:281); everything else is stream-ordered on the
+// caller's stream, so one process per GPU can run views back to back.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gsd_raster.h"
+#include "gsd_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+thread_local uint32_t* g_pinned = nullptr;  // 16 B of pinned host memory for the counter read-back
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define GSD_HIP(expr)                                                                                    \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) return fail(GSD_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// CHECK_CUDA(..., debug) equivalent (auxiliary.h:166-173)
+#define GSD_CHECK(debug, stream)                                                                      \
+    do {                                                                                              \
+        hipError_t e_ = hipGetLastError();                                                            \
+        if (e_ == hipSuccess && (debug)) e_ = hipStreamSynchronize(stream);                           \
+        if (e_ != hipSuccess) return fail(GSD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr size_t kAlign = 256;
+size_t up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+char* align_ptr(void* p) { return reinterpret_cast<char*>(up(reinterpret_cast<uintptr_t>(p))); }
+
+struct Geom {
+    float2* means2D;
+    float4* conic_opacity;
+    float4* rgb;
+    float* depths;
+    int* radii;
+    uint8_t* clamped;
+};
+// GeometryState (rasterizer_impl.h:29-41), re-laid out: what render gathers per
+// instance (xy, conic/opacity, rgb) is 16-B aligned; cov3D is recomputed in
+// the backward instead of stored; no P-wide scan space is needed.
+size_t carve_geom(void* base, size_t P, Geom* g) {
+    char* p = base ? align_ptr(base) : nullptr;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* r = p ? p + off : nullptr;
+        off += up(bytes);
+        return r;
+    };
+    Geom v;
+    v.means2D = reinterpret_cast<float2*>(take(P * sizeof(float2)));
+    v.conic_opacity = reinterpret_cast<float4*>(take(P * sizeof(float4)));
+    v.rgb = reinterpret_cast<float4*>(take(P * sizeof(float4)));
+    v.depths = reinterpret_cast<float*>(take(P * sizeof(float)));
+    v.radii = reinterpret_cast<int*>(take(P * sizeof(int)));
+    v.clamped = reinterpret_cast<uint8_t*>(take(P));
+    if (g) *g = v;
+    return off + kAlign;
+}
+
+struct Img {
+    float* final_T;
+    uint32_t* n_contrib;
+    uint2* ranges;
+    uint32_t* tile_count;
+    uint32_t* tile_cursor;
+    uint32_t* counters;
+};
+size_t carve_img(void* base, size_t npix, size_t T, Img* g) {
+    char* p = base ? align_ptr(base) : nullptr;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* r = p ? p + off : nullptr;
+        off += up(bytes);
+        return r;
+    };
+    Img v;
+    v.final_T = reinterpret_cast<float*>(take(npix * sizeof(float)));
+    v.n_contrib = reinterpret_cast<uint32_t*>(take(npix * sizeof(uint32_t)));
+    v.ranges = reinterpret_cast<uint2*>(take(T * sizeof(uint2)));
+    v.tile_count = reinterpret_cast<uint32_t*>(take(T * sizeof(uint32_t)));
+    v.tile_cursor = reinterpret_cast<uint32_t*>(take(T * sizeof(uint32_t)));
+    v.counters = reinterpret_cast<uint32_t*>(take(4 * sizeof(uint32_t)));
+    if (g) *g = v;
+    return off + kAlign;
+}
+
+struct Bin {
+    unsigned long long* keys;
+    unsigned long long* scratch;
+    uint32_t* point_list;
+};
+size_t carve_bin(void* base, size_t K, Bin* g) {
+    char* p = base ? align_ptr(base) : nullptr;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* r = p ? p + off : nullptr;
+        off += up(bytes);
+        return r;
+    };
+    Bin v;
+    v.keys = reinterpret_cast<unsigned long long*>(take(K * 8));
+    v.scratch = reinterpret_cast<unsigned long long*>(take(K * 8));
+    v.point_list = reinterpret_cast<uint32_t*>(take(K * 4));
+    if (g) *g = v;
+    return off + kAlign;
+}
+
+int grid_x(const gsd_raster_args* a) { return (a->width + gsd::kTileX - 1) / gsd::kTileX; }
+int grid_y(const gsd_raster_args* a) { return (a->height + gsd::kTileY - 1) / gsd::kTileY; }
+
+int validate(const gsd_raster_args* a, bool forward) {
+    if (!a) return fail(GSD_ERR_ARG, "null gsd_raster_args");
+    if (a->P < 0) return fail(GSD_ERR_ARG, "means3D must have dimensions (num_points, 3)");
+    if (a->width <= 0 || a->height <= 0) return fail(GSD_ERR_ARG, "image_width and image_height must be positive");
+    if (a->P == 0) return GSD_OK;
+    if (!a->means3D || (forward && !a->opacities) || !a->viewmatrix || !a->projmatrix || !a->background)
+        return fail(GSD_ERR_ARG, "means3D, opacities, viewmatrix, projmatrix and bg are required");
+    if ((a->shs == nullptr) == (a->colors_precomp == nullptr))
+        return fail(GSD_ERR_ARG, "Please provide excatly one of either SHs or precomputed colors!");
+    const bool have_sr = a->scales && a->rotations;
+    if (have_sr == (a->cov3D_precomp != nullptr) || ((a->scales == nullptr) != (a->rotations == nullptr)))
+        return fail(GSD_ERR_ARG,
+                    "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (a->shs) {
+        if (!a->campos) return fail(GSD_ERR_ARG, "campos is required with SHs");
+        const int d = a->D < 0 ? 0 : (a->D > 3 ? 3 : a->D);
+        if (a->D < 0) return fail(GSD_ERR_ARG, "sh_degree must be >= 0");
+        if (a->M < (d + 1) * (d + 1))
+            return fail(GSD_ERR_ARG, "sh has fewer coefficients than (sh_degree+1)^2");
+    }
+    return GSD_OK;
+}
+
+hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+int gsd_abi_version(void) { return GSD_ABI_VERSION; }
+const char* gsd_last_error(void) { return g_err.c_str(); }
+
+size_t gsd_geom_buffer_bytes(int32_t P) { return carve_geom(nullptr, (size_t)(P < 0 ? 0 : P), nullptr); }
+size_t gsd_image_buffer_bytes(int32_t width, int32_t height) {
+    const size_t gx = (size_t)(width + gsd::kTileX - 1) / gsd::kTileX, gy = (size_t)(height + gsd::kTileY - 1) / gsd::kTileY;
+    return carve_img(nullptr, (size_t)width * (size_t)height, gx * gy, nullptr);
+}
+size_t gsd_binning_buffer_bytes(int64_t K) { return carve_bin(nullptr, (size_t)(K < 0 ? 0 : K), nullptr); }
+
+void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t K, size_t* go, size_t* io, size_t* bo) {
+    // carve from a fake, 256-aligned base so the returned pointers are the offsets
+    char* const base = reinterpret_cast<char*>(uintptr_t(1) << 20);
+    auto off = [&](const void* p) { return (size_t)(reinterpret_cast<const char*>(p) - base); };
+    const size_t gx = (size_t)(width + gsd::kTileX - 1) / gsd::kTileX, gy = (size_t)(height + gsd::kTileY - 1) / gsd::kTileY;
+    Geom g;
+    Img im;
+    Bin b;
+    carve_geom(base, (size_t)(P < 0 ? 0 : P), &g);
+    carve_img(base, (size_t)width * (size_t)height, gx * gy, &im);
+    carve_bin(base, (size_t)(K < 0 ? 0 : K), &b);
+    if (go) {
+        go[0] = off(g.means2D); go[1] = off(g.conic_opacity); go[2] = off(g.rgb);
+        go[3] = off(g.depths); go[4] = off(g.radii); go[5] = off(g.clamped);
+    }
+    if (io) {
+        io[0] = off(im.final_T); io[1] = off(im.n_contrib); io[2] = off(im.ranges);
+        io[3] = off(im.tile_count); io[4] = off(im.tile_cursor); io[5] = off(im.counters);
+    }
+    if (bo) {
+        bo[0] = off(b.keys); bo[1] = off(b.scratch); bo[2] = off(b.point_list);
+    }
+}
+
+int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, int32_t* radii,
+                              int64_t* num_rendered, void* stream) {
+    int rc = validate(a, true);
+    if (rc) return rc;
+    if (!num_rendered) return fail(GSD_ERR_ARG, "num_rendered must not be null");
+    *num_rendered = 0;
+    if (a->P == 0) return GSD_OK;
+    if (!geom_buffer || !image_buffer) return fail(GSD_ERR_STATE, "state buffers must be allocated");
+    hipStream_t s = as_stream(stream);
+    Geom g;
+    Img im;
+    carve_geom(geom_buffer, a->P, &g);
+    const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
+    GSD_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
+    GSD_HIP(hipMemsetAsync(im.counters, 0, 16, s));
+
+    gsd::PreprocessParams p{};
+    p.P = a->P; p.D = a->D; p.M = a->M; p.W = a->width; p.H = a->height; p.grid_x = gx; p.grid_y = gy;
+    p.prefiltered = a->prefiltered;
+    p.scale_modifier = a->scale_modifier; p.tan_fovx = a->tan_fovx; p.tan_fovy = a->tan_fovy;
+    p.focal_y = a->height / (2.0f * a->tan_fovy);  // rasterizer_impl.cu:222-223
+    p.focal_x = a->width / (2.0f * a->tan_fovx);
+    p.means3D = a->means3D; p.scales = a->scales; p.rotations = a->rotations; p.opacities = a->opacities;
+    p.shs = a->shs; p.cov3D_precomp = a->cov3D_precomp; p.colors_precomp = a->colors_precomp;
+    p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
+    p.radii = radii ? radii : g.radii;
+    p.means2D = g.means2D; p.depths = g.depths; p.conic_opacity = g.conic_opacity; p.rgb = g.rgb;
+    p.clamped = g.clamped; p.tile_count = im.tile_count; p.err_flags = im.counters + 1;
+    gsd::launch_preprocess_fwd(p, s);
+    GSD_CHECK(a->debug, s);
+    gsd::launch_tile_scan(T, im.tile_count, im.ranges, im.tile_cursor, im.counters, s);
+    GSD_CHECK(a->debug, s);
+    if (!g_pinned) GSD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_pinned), 16, hipHostMallocDefault));
+    GSD_HIP(hipMemcpyAsync(g_pinned, im.counters, 8, hipMemcpyDeviceToHost, s));
+    GSD_HIP(hipStreamSynchronize(s));
+    if (g_pinned[1] & gsd::kErrPrefiltered)
+        return fail(GSD_ERR_ARG, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    *num_rendered = (int64_t)g_pinned[0];
+    return GSD_OK;
+}
+
+int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, void* image_buffer,
+                                 void* binning_buffer, int64_t K, const int32_t* radii, float* out_color,
+                                 void* stream) {
+    int rc = validate(a, true);
+    if (rc) return rc;
+    if (a->P == 0) return GSD_OK;
+    if (!geom_buffer || !image_buffer || (K > 0 && !binning_buffer) || !out_color)
+        return fail(GSD_ERR_STATE, "state buffers / out_color must be allocated");
+    hipStream_t s = as_stream(stream);
+    Geom g;
+    Img im;
+    Bin b;
+    carve_geom(geom_buffer, a->P, &g);
+    const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
+    carve_bin(binning_buffer, (size_t)K, &b);
+    if (K > 0) {
+        gsd::BinParams bp{};
+        bp.P = a->P; bp.grid_x = gx; bp.grid_y = gy; bp.num_tiles = T;
+        bp.radii = radii ? radii : g.radii;
+        bp.means2D = g.means2D; bp.depths = g.depths; bp.tile_cursor = im.tile_cursor; bp.bucket_keys = b.keys;
+        gsd::launch_scatter_keys(bp, s);
+        GSD_CHECK(a->debug, s);
+        gsd::launch_tile_sort(T, im.ranges, b.keys, b.scratch, b.point_list, s);
+        GSD_CHECK(a->debug, s);
+    }
+    gsd::RenderParams rp{};
+    rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
+    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
+    rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
+    rp.out_color = out_color;
+    gsd::launch_render_fwd(rp, s);
+    GSD_CHECK(a->debug, s);
+    return GSD_OK;
+}
+
+int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const void* geom_buffer,
+                           const void* binning_buffer, const void* image_buffer, int64_t K,
+                           const float* dL_dout_color, float* dL_dmeans2D, float* dL_dconic, float* dL_dopacity,
+                           float* dL_dcolors, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                           float* dL_dscales, float* dL_drotations, void* stream) {
+    int rc = validate(a, false);
+    if (rc) return rc;
+    if (a->P == 0) return GSD_OK;
+    if (!geom_buffer || !image_buffer || (K > 0 && !binning_buffer))
+        return fail(GSD_ERR_STATE, "state buffers from the matching forward are required");
+    if (!dL_dout_color || !dL_dmeans2D || !dL_dconic || !dL_dopacity || !dL_dcolors || !dL_dmeans3D || !dL_dcov3D)
+        return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
+    if ((a->shs && !dL_dsh) || (a->scales && (!dL_dscales || !dL_drotations)))
+        return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
+    hipStream_t s = as_stream(stream);
+    Geom g;
+    Img im;
+    Bin b;
+    carve_geom(const_cast<void*>(geom_buffer), a->P, &g);
+    const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_img(const_cast<void*>(image_buffer), (size_t)a->width * a->height, T, &im);
+    carve_bin(const_cast<void*>(binning_buffer), (size_t)K, &b);
+
+    gsd::RenderBwdParams rp{};
+    rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
+    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
+    rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
+    rp.dL_dpix = dL_dout_color; rp.dL_dmean2D = dL_dmeans2D; rp.dL_dconic = dL_dconic;
+    rp.dL_dopacity = dL_dopacity; rp.dL_dcolors = dL_dcolors;
+    if (K > 0) {
+        gsd::launch_render_bwd(rp, s);
+        GSD_CHECK(a->debug, s);
+    }
+    gsd::PreprocessBwdParams p{};
+    p.P = a->P; p.D = a->D; p.M = a->M;
+    p.scale_modifier = a->scale_modifier; p.tan_fovx = a->tan_fovx; p.tan_fovy = a->tan_fovy;
+    p.focal_y = a->height / (2.0f * a->tan_fovy);
+    p.focal_x = a->width / (2.0f * a->tan_fovx);
+    p.means3D = a->means3D; p.radii = radii ? radii : g.radii; p.shs = a->shs; p.clamped = g.clamped;
+    p.scales = a->scales; p.rotations = a->rotations; p.cov3D_precomp = a->cov3D_precomp;
+    p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
+    p.dL_dmean2D = dL_dmeans2D; p.dL_dconic = dL_dconic; p.dL_dcolor = dL_dcolors;
+    p.dL_dmeans3D = dL_dmeans3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = dL_dsh; p.dL_dscales = dL_dscales;
+    p.dL_drotations = dL_drotations;
+    gsd::launch_preprocess_bwd(p, s);
+    GSD_CHECK(a->debug, s);
+    return GSD_OK;
+}
+
+int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream) {
+    (void)projmatrix;  // in_frustum computes the projection but only tests the view-space depth
+    if (P < 0) return fail(GSD_ERR_ARG, "means3D must have dimensions (num_points, 3)");
+    if (P == 0) return GSD_OK;
+    if (!means3D || !viewmatrix || !present) return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::launch_mark_visible(P, means3D, viewmatrix, present, as_stream(stream));
+    GSD_CHECK(false, as_stream(stream));
+    return GSD_OK;
+}
+
+int gsd_se3_deform_forward(int32_t P, const float* twist, const float* means_in, const float* rot_in,
+                           float* means_out, float* rot_out, void* stream) {
+    if (P < 0) return fail(GSD_ERR_ARG, "twist must have dimensions (num_points, 6)");
+    if (P == 0) return GSD_OK;
+    if (!twist || !means_in || !means_out || (rot_in && !rot_out)) return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::launch_se3_fwd(P, twist, means_in, rot_in, means_out, rot_out, as_stream(stream));
+    GSD_CHECK(false, as_stream(stream));
+    return GSD_OK;
+}
+
+int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in, const float* rot_in,
+                            const float* dL_dmeans_out, const float* dL_drot_out, float* dL_dtwist,
+                            float* dL_dmeans_in, float* dL_drot_in, void* stream) {
+    if (P < 0) return fail(GSD_ERR_ARG, "twist must have dimensions (num_points, 6)");
+    if (P == 0) return GSD_OK;
+    if (!twist || !means_in || !dL_dmeans_out || !dL_dtwist || !dL_dmeans_in ||
+        (rot_in && (!dL_drot_out || !dL_drot_in)))
+        return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::launch_se3_bwd(P, twist, means_in, rot_in, dL_dmeans_out, dL_drot_out, dL_dtwist, dL_dmeans_in, dL_drot_in,
+                        as_stream(stream));
+    GSD_CHECK(false, as_stream(stream));
+    return GSD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+// gsd_device.h -- device-side building blocks shared by the gfx950 kernels.
+//
+// Numerics contract: the library is compiled with -ffp-contract=off and every
+// expression below keeps the evaluation order of the reference's glm/CUDA
+// code (cited per function), so preprocess outputs are bit-identical to the
+// un-contracted float32 arithmetic of the reference (DESIGN.md "Numerics").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsd {
+
+constexpr int kTileX = 16;  // config.h:16 -- part of the bit-exact key contract
+constexpr int kTileY = 16;  // config.h:17
+constexpr int kTilePix = kTileX * kTileY;
+
+// auxiliary.h:22-39
+constexpr float kSH0 = 0.28209479177387814f;
+constexpr float kSH1 = 0.4886025119029199f;
+constexpr float kSH2_0 = 1.0925484305920792f, kSH2_1 = -1.0925484305920792f, kSH2_2 = 0.31539156525252005f,
+                kSH2_3 = -1.0925484305920792f, kSH2_4 = 0.5462742152960396f;
+constexpr float kSH3_0 = -0.5900435899266435f, kSH3_1 = 2.890611442640554f, kSH3_2 = -0.4570457994644658f,
+                kSH3_3 = 0.3731763325901154f, kSH3_4 = -0.4570457994644658f, kSH3_5 = 1.445305721320277f,
+                kSH3_6 = -0.5900435899266435f;
+
+// The 4x4 camera matrices, read once per block into SGPR-resident registers.
+struct Mat4 {
+    float m[16];
+};
+
+__device__ __forceinline__ Mat4 load_mat4(const float* __restrict__ p) {
+    Mat4 r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r.m[i] = p[i];
+    return r;
+}
+
+// auxiliary.h:58-66 transformPoint4x3
+__device__ __forceinline__ float3 xform_point3(const float3 p, const Mat4& m) {
+    return make_float3(m.m[0] * p.x + m.m[4] * p.y + m.m[8] * p.z + m.m[12],
+                       m.m[1] * p.x + m.m[5] * p.y + m.m[9] * p.z + m.m[13],
+                       m.m[2] * p.x + m.m[6] * p.y + m.m[10] * p.z + m.m[14]);
+}
+// auxiliary.h:68-77 transformPoint4x4
+__device__ __forceinline__ float4 xform_point4(const float3 p, const Mat4& m) {
+    return make_float4(m.m[0] * p.x + m.m[4] * p.y + m.m[8] * p.z + m.m[12],
+                       m.m[1] * p.x + m.m[5] * p.y + m.m[9] * p.z + m.m[13],
+                       m.m[2] * p.x + m.m[6] * p.y + m.m[10] * p.z + m.m[14],
+                       m.m[3] * p.x + m.m[7] * p.y + m.m[11] * p.z + m.m[15]);
+}
+// auxiliary.h:89-97 transformVec4x3Transpose
+__device__ __forceinline__ float3 xform_vec3_T(const float3 p, const Mat4& m) {
+    return make_float3(m.m[0] * p.x + m.m[1] * p.y + m.m[2] * p.z, m.m[4] * p.x + m.m[5] * p.y + m.m[6] * p.z,
+                       m.m[8] * p.x + m.m[9] * p.y + m.m[10] * p.z);
+}
+
+// auxiliary.h:41-44 ndc2Pix (a double expression upstream: literals 1.0 / 0.5)
+__device__ __forceinline__ float ndc_to_pix(float v, int S) {
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+// auxiliary.h:46-56 getRect, clamped to the tile grid
+struct Rect {
+    int x0, y0, x1, y1;
+};
+__device__ __forceinline__ Rect tile_rect(float px, float py, int radius, int gx, int gy) {
+    const float r = (float)radius;
+    Rect o;
+    o.x0 = min(gx, max(0, (int)((px - r) / (float)kTileX)));
+    o.y0 = min(gy, max(0, (int)((py - r) / (float)kTileY)));
+    o.x1 = min(gx, max(0, (int)((px + r + (float)kTileX - 1.0f) / (float)kTileX)));
+    o.y1 = min(gy, max(0, (int)((py + r + (float)kTileY - 1.0f) / (float)kTileY)));
+    return o;
+}
+
+// Column-major 3x3 (glm convention): c[k] is column k.
+struct M3 {
+    float3 c[3];
+};
+// glm operator*(mat3,mat3) (type_mat3x3.inl:486-520): R[c][r] = (A0r*Bc0 + A1r*Bc1) + A2r*Bc2
+__device__ __forceinline__ float3 m3_col(const M3& A, const float3 b) {
+    return make_float3(A.c[0].x * b.x + A.c[1].x * b.y + A.c[2].x * b.z,
+                       A.c[0].y * b.x + A.c[1].y * b.y + A.c[2].y * b.z,
+                       A.c[0].z * b.x + A.c[1].z * b.y + A.c[2].z * b.z);
+}
+__device__ __forceinline__ M3 m3_mul(const M3& A, const M3& B) {
+    M3 R;
+    R.c[0] = m3_col(A, B.c[0]);
+    R.c[1] = m3_col(A, B.c[1]);
+    R.c[2] = m3_col(A, B.c[2]);
+    return R;
+}
+__device__ __forceinline__ M3 m3_T(const M3& A) {
+    M3 R;
+    R.c[0] = make_float3(A.c[0].x, A.c[1].x, A.c[2].x);
+    R.c[1] = make_float3(A.c[0].y, A.c[1].y, A.c[2].y);
+    R.c[2] = make_float3(A.c[0].z, A.c[1].z, A.c[2].z);
+    return R;
+}
+__device__ __forceinline__ M3 m3_cols(float a, float b, float c, float d, float e, float f, float g, float h,
+                                      float i) {
+    M3 R;
+    R.c[0] = make_float3(a, b, c);
+    R.c[1] = make_float3(d, e, f);
+    R.c[2] = make_float3(g, h, i);
+    return R;
+}
+__device__ __forceinline__ float dot3(const float3 a, const float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// Quaternion (r,x,y,z) -> glm rotation matrix of forward.cu:134-138 / backward.cu:287-291
+__device__ __forceinline__ M3 quat_to_R(const float4 q) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    return m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                   2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                   2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+}
+
+// forward.cu:118-152 computeCov3D (no quaternion normalisation, :127)
+struct Cov6 {
+    float v[6];
+};
+__device__ __forceinline__ Cov6 cov3d_from_scale_rot(const float3 s, float mod, const float4 q) {
+    M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    S.c[0].x = mod * s.x;
+    S.c[1].y = mod * s.y;
+    S.c[2].z = mod * s.z;
+    const M3 R = quat_to_R(q);
+    const M3 M = m3_mul(S, R);
+    const M3 Sig = m3_mul(m3_T(M), M);
+    Cov6 o;
+    o.v[0] = Sig.c[0].x; o.v[1] = Sig.c[0].y; o.v[2] = Sig.c[0].z;
+    o.v[3] = Sig.c[1].y; o.v[4] = Sig.c[1].z; o.v[5] = Sig.c[2].z;
+    return o;
+}
+
+// ---- wave64 reductions (DPP; full sum lands in lane 63, returned wave-uniform) ----
+template <int CTRL, int ROWMASK, int BANKMASK>
+__device__ __forceinline__ float dpp_step(float v) {
+    const int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, BANKMASK, false);
+    return v + __int_as_float(t);
+}
+// quad_perm[1,0,3,2] -> quad_perm[2,3,0,1] -> row_shr:4 -> row_shr:8 -> row_bcast:15 -> row_bcast:31
+__device__ __forceinline__ float wave_sum(float v) {
+    v = dpp_step<0xb1, 0xf, 0xf>(v);
+    v = dpp_step<0x4e, 0xf, 0xf>(v);
+    v = dpp_step<0x114, 0xf, 0xe>(v);
+    v = dpp_step<0x118, 0xf, 0xc>(v);
+    v = dpp_step<0x142, 0xa, 0xf>(v);
+    v = dpp_step<0x143, 0xc, 0xf>(v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// XCD-aware remap of a 1-D block index: blocks b and b+8 are dealt to the same
+// XCD (MI355X_MICROARCH.md "Workgroup dispatch"), so give each XCD a
+// contiguous run of tiles -- neighbouring tiles gather the same Gaussians and
+// then share that XCD's L2.  Speed only; any placement is correct.
+__device__ __forceinline__ int xcd_swizzle(int b, int n) {
+    const int full = n & ~7;
+    if (b >= full) return b;
+    const int per = full >> 3;
+    return (b & 7) * per + (b >> 3);
+}
+
+}  // namespace gsd

@@ -1,0 +1,123 @@
+// gsd_kernels.h -- kernel parameter blocks and launch declarations.
+//
+// State layout in HBM (one view; all arrays SoA, 256-B aligned; see
+// gsd_capi.hip "carve" functions and DESIGN.md "Data layout"):
+//   geometry (per Gaussian):  means2D float2 | conic_opacity float4 | rgb float4 (a=0) |
+//                             depth f32 | clamped u8 (bit c = channel c clamped) | radii i32
+//   image (per pixel / tile): final_T f32 [Npix] | n_contrib u32 [Npix] |
+//                             ranges uint2 [T] | tile_count u32 [T] | tile_cursor u32 [T] |
+//                             counters u32 [4] (num_rendered, error flags)
+//   binning (per instance):   bucket_keys u64 [K] ((depth bits << 32) | gaussian id, grouped by
+//                             tile) | merge scratch u64 [K] | point_list u32 [K]
+#pragma once
+#include "gsd_device.h"
+
+namespace gsd {
+
+enum : uint32_t { kErrPrefiltered = 1u };
+
+struct PreprocessParams {
+    int P, D, M, W, H, grid_x, grid_y, prefiltered;
+    float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
+    const float* means3D;
+    const float* scales;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* cov3D_precomp;
+    const float* colors_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    int* radii;
+    float2* means2D;
+    float* depths;
+    float4* conic_opacity;
+    float4* rgb;
+    uint8_t* clamped;
+    uint32_t* tile_count;
+    uint32_t* err_flags;
+};
+
+struct PreprocessBwdParams {
+    int P, D, M;
+    float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
+    const float* means3D;
+    const int* radii;
+    const float* shs;
+    const uint8_t* clamped;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    const float* dL_dmean2D;  // (P,3)
+    const float* dL_dconic;   // (P,4)
+    const float* dL_dcolor;   // (P,3)
+    float* dL_dmeans3D;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dscales;
+    float* dL_drotations;
+};
+
+struct BinParams {
+    int P, grid_x, grid_y, num_tiles;
+    const int* radii;
+    const float2* means2D;
+    const float* depths;
+    uint32_t* tile_cursor;
+    unsigned long long* bucket_keys;
+};
+
+struct RenderParams {
+    int W, H, grid_x, num_tiles;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float4* rgb;
+    const float* bg;
+    float* final_T;
+    uint32_t* n_contrib;
+    float* out_color;
+};
+
+struct RenderBwdParams {
+    int W, H, grid_x, num_tiles;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float4* rgb;
+    const float* bg;
+    const float* final_T;
+    const uint32_t* n_contrib;
+    const float* dL_dpix;
+    float* dL_dmean2D;  // (P,3)
+    float* dL_dconic;   // (P,4)
+    float* dL_dopacity; // (P)
+    float* dL_dcolors;  // (P,3)
+};
+
+// Host-side launchers (one per kernel; each lives in the .hip file that defines the kernel).
+void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s);
+void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s);
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
+void launch_tile_scan(int num_tiles, const uint32_t* tile_count, uint2* ranges, uint32_t* tile_cursor,
+                      uint32_t* counters, hipStream_t s);
+void launch_scatter_keys(const BinParams& p, hipStream_t s);
+void launch_tile_sort(int num_tiles, const uint2* ranges, unsigned long long* keys, unsigned long long* scratch,
+                      uint32_t* point_list, hipStream_t s);
+void launch_render_fwd(const RenderParams& p, hipStream_t s);
+void launch_render_bwd(const RenderBwdParams& p, hipStream_t s);
+void launch_se3_fwd(int P, const float* twist, const float* means_in, const float* rot_in, float* means_out,
+                    float* rot_out, hipStream_t s);
+void launch_se3_bwd(int P, const float* twist, const float* means_in, const float* rot_in, const float* dmeans_out,
+                    const float* drot_out, float* dtwist, float* dmeans_in, float* drot_in, hipStream_t s);
+
+constexpr int kScanThreads = 1024;
+constexpr int kSortCap = 4096;  // instances sorted in one LDS pass (32 KiB of u64 keys)
+
+}  // namespace gsd

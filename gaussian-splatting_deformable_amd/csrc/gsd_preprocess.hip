@@ -1,0 +1,402 @@
+// gsd_preprocess.hip -- per-Gaussian kernels of the hot path (forward and backward).
+//
+// One lane per Gaussian, 256-lane workgroups (4 waves).  These kernels are
+// HBM-bound (DESIGN.md roofline table): ~60 B of position/shape/opacity +
+// 12*(D+1)^2 B of SH read per Gaussian, ~50 B written.  VALU 3x3 chains are
+// cheaper than packing single 3x3 products into MFMA tiles (a 16x16x4 f32 MFMA
+// wastes >90% of its lanes on one Gaussian's 3x3), so there is no MFMA here.
+#include "gsd_kernels.h"
+
+namespace gsd {
+
+// ---------------------------------------------------------------------------
+// SH -> RGB, forward.cu:20-71 (per channel, identical expression tree)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sh_channel(int deg, const float* __restrict__ s, float x, float y, float z) {
+    // s[3*k] is coefficient k of this channel
+    float res = kSH0 * s[0];
+    if (deg > 0) {
+        res = res - kSH1 * y * s[3] + kSH1 * z * s[6] - kSH1 * x * s[9];
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            res = res + kSH2_0 * xy * s[12] + kSH2_1 * yz * s[15] + kSH2_2 * (2.0f * zz - xx - yy) * s[18] +
+                  kSH2_3 * xz * s[21] + kSH2_4 * (xx - yy) * s[24];
+            if (deg > 2) {
+                res = res + kSH3_0 * y * (3.0f * xx - yy) * s[27] + kSH3_1 * xy * z * s[30] +
+                      kSH3_2 * y * (4.0f * zz - xx - yy) * s[33] +
+                      kSH3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s[36] +
+                      kSH3_4 * x * (4.0f * zz - xx - yy) * s[39] + kSH3_5 * z * (xx - yy) * s[42] +
+                      kSH3_6 * x * (xx - 3.0f * yy) * s[45];
+            }
+        }
+    }
+    return res + 0.5f;
+}
+
+// Stage one Gaussian's active SH coefficients (3*(D+1)^2 floats, <= 48) into
+// registers with the widest aligned loads the (P,M,3) row allows.
+template <int NC>
+__device__ __forceinline__ void load_sh(const float* __restrict__ row, float (&s)[48]) {
+#pragma unroll
+    for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
+}
+
+__device__ __forceinline__ float3 sh_to_rgb(int deg, const float* __restrict__ row, float3 pos, float3 cam,
+                                            uint8_t& clamp_bits) {
+    float3 d = make_float3(pos.x - cam.x, pos.y - cam.y, pos.z - cam.z);
+    const float len = sqrtf(dot3(d, d));
+    d = make_float3(d.x / len, d.y / len, d.z / len);
+    float s[48];
+    if (deg >= 3) load_sh<16>(row, s);
+    else if (deg == 2) load_sh<9>(row, s);
+    else if (deg == 1) load_sh<4>(row, s);
+    else load_sh<1>(row, s);
+    float3 rgb;
+    rgb.x = sh_channel(deg, s + 0, d.x, d.y, d.z);
+    rgb.y = sh_channel(deg, s + 1, d.x, d.y, d.z);
+    rgb.z = sh_channel(deg, s + 2, d.x, d.y, d.z);
+    clamp_bits = (uint8_t)((rgb.x < 0) | ((rgb.y < 0) << 1) | ((rgb.z < 0) << 2));
+    rgb.x = rgb.x < 0.0f ? 0.0f : rgb.x;
+    rgb.y = rgb.y < 0.0f ? 0.0f : rgb.y;
+    rgb.z = rgb.z < 0.0f ? 0.0f : rgb.z;
+    return rgb;
+}
+
+// forward.cu:74-113 computeCov2D -> (a, b, c) of the low-pass-filtered 2D covariance
+__device__ __forceinline__ float3 cov2d_fwd(const float3 mean, float fx, float fy, float tanx, float tany,
+                                            const Cov6& c3, const Mat4& V) {
+    float3 t = xform_point3(mean, V);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const M3 J = m3_cols(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z, -(fy * t.y) / (t.z * t.z), 0,
+                         0, 0);
+    const M3 W = m3_cols(V.m[0], V.m[4], V.m[8], V.m[1], V.m[5], V.m[9], V.m[2], V.m[6], V.m[10]);
+    const M3 T = m3_mul(W, J);
+    const M3 Vk = m3_cols(c3.v[0], c3.v[1], c3.v[2], c3.v[1], c3.v[3], c3.v[4], c3.v[2], c3.v[4], c3.v[5]);
+    const M3 A = m3_mul(m3_T(T), m3_T(Vk));
+    const M3 cov = m3_mul(A, T);
+    return make_float3(cov.c[0].x + 0.3f, cov.c[0].y, cov.c[1].y + 0.3f);
+}
+
+// ---------------------------------------------------------------------------
+// Forward preprocess: forward.cu:155-256 (+ the per-tile instance count of
+// the binning stage, folded in so the rect is computed once).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= p.P) return;
+    const Mat4 V = load_mat4(p.view);
+    const Mat4 Pm = load_mat4(p.proj);
+    p.radii[idx] = 0;
+    const float3 mean = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+    // auxiliary.h:139-164 in_frustum (near plane only)
+    const float3 pv = xform_point3(mean, V);
+    if (pv.z <= 0.2f) {
+        if (p.prefiltered) atomicOr(p.err_flags, kErrPrefiltered);
+        return;
+    }
+    const float4 ph = xform_point4(mean, Pm);
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float ppx = ph.x * pw, ppy = ph.y * pw;
+
+    Cov6 c3;
+    if (p.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3.v[k] = p.cov3D_precomp[6 * idx + k];
+    } else {
+        const float3 s = make_float3(p.scales[3 * idx], p.scales[3 * idx + 1], p.scales[3 * idx + 2]);
+        const float4 q = reinterpret_cast<const float4*>(p.rotations)[idx];
+        c3 = cov3d_from_scale_rot(s, p.scale_modifier, q);
+    }
+    const float3 cov = cov2d_fwd(mean, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, c3, V);
+    const float det = (cov.x * cov.z - cov.y * cov.y);
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+    const float mid = 0.5f * (cov.x + cov.z);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float2 pix = make_float2(ndc_to_pix(ppx, p.W), ndc_to_pix(ppy, p.H));
+    const Rect r = tile_rect(pix.x, pix.y, (int)my_radius, p.grid_x, p.grid_y);
+    if ((r.x1 - r.x0) * (r.y1 - r.y0) == 0) return;
+
+    float4 col;
+    uint8_t cl = 0;
+    if (p.colors_precomp) {
+        col = make_float4(p.colors_precomp[3 * idx], p.colors_precomp[3 * idx + 1], p.colors_precomp[3 * idx + 2], 0.f);
+    } else {
+        const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+        const float3 rgb = sh_to_rgb(p.D, p.shs + (size_t)idx * p.M * 3, mean, cam, cl);
+        col = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+    }
+    p.clamped[idx] = cl;
+    p.rgb[idx] = col;
+    p.depths[idx] = pv.z;
+    p.radii[idx] = (int)my_radius;
+    p.means2D[idx] = pix;
+    p.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, p.opacities[idx]);
+    // per-tile instance counts (the binning histogram)
+    for (int y = r.y0; y < r.y1; ++y)
+        for (int x = r.x0; x < r.x1; ++x)
+            __hip_atomic_fetch_add(p.tile_count + (y * p.grid_x + x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// auxiliary.h:139-164 via rasterizer_impl.cu:54-66 checkFrustum
+__global__ __launch_bounds__(256) void k_mark_visible(int P, const float* __restrict__ means3D,
+                                                      const float* __restrict__ view, uint8_t* __restrict__ present) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= P) return;
+    const Mat4 V = load_mat4(view);
+    const float3 mean = make_float3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+    present[idx] = (uint8_t)!(xform_point3(mean, V).z <= 0.2f);
+}
+
+// ---------------------------------------------------------------------------
+// Backward: computeCov2DCUDA (backward.cu:144-274) + preprocessCUDA
+// (backward.cu:346-396: projective mean term, SH backward :20-139, cov3D
+// backward :278-341) fused into one pass over the Gaussians.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cov2d_bwd(const float3 mean, const Cov6& c3, float hx, float hy, float tanx,
+                                          float tany, const Mat4& Vm, const float3 dc, float3& dmean, Cov6& dcov) {
+    float3 t = xform_point3(mean, Vm);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float xgm = txtz < -limx || txtz > limx ? 0 : 1;
+    const float ygm = tytz < -limy || tytz > limy ? 0 : 1;
+    const M3 J = m3_cols(hx / t.z, 0.0f, -(hx * t.x) / (t.z * t.z), 0.0f, hy / t.z, -(hy * t.y) / (t.z * t.z), 0,
+                         0, 0);
+    const M3 W = m3_cols(Vm.m[0], Vm.m[4], Vm.m[8], Vm.m[1], Vm.m[5], Vm.m[9], Vm.m[2], Vm.m[6], Vm.m[10]);
+    const M3 V = m3_cols(c3.v[0], c3.v[1], c3.v[2], c3.v[1], c3.v[3], c3.v[4], c3.v[2], c3.v[4], c3.v[5]);
+    const M3 T = m3_mul(W, J);
+    const M3 cov2 = m3_mul(m3_mul(m3_T(T), m3_T(V)), T);
+    const float a = cov2.c[0].x + 0.3f;
+    const float b = cov2.c[0].y;
+    const float c = cov2.c[1].y + 0.3f;
+    const float denom = a * c - b * b;
+    float dL_da = 0, dL_db = 0, dL_dc = 0;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    // T[col][row] accessors
+    const float T00 = T.c[0].x, T01 = T.c[0].y, T02 = T.c[0].z, T10 = T.c[1].x, T11 = T.c[1].y, T12 = T.c[1].z;
+    if (denom2inv != 0) {
+        dL_da = denom2inv * (-c * c * dc.x + 2 * b * c * dc.y + (denom - a * c) * dc.z);
+        dL_dc = denom2inv * (-a * a * dc.z + 2 * a * b * dc.y + (denom - a * c) * dc.x);
+        dL_db = denom2inv * 2 * (b * c * dc.x - (denom + 2 * b * b) * dc.y + a * b * dc.z);
+        dcov.v[0] = (T00 * T00 * dL_da + T00 * T10 * dL_db + T10 * T10 * dL_dc);
+        dcov.v[3] = (T01 * T01 * dL_da + T01 * T11 * dL_db + T11 * T11 * dL_dc);
+        dcov.v[5] = (T02 * T02 * dL_da + T02 * T12 * dL_db + T12 * T12 * dL_dc);
+        dcov.v[1] = 2 * T00 * T01 * dL_da + (T00 * T11 + T01 * T10) * dL_db + 2 * T10 * T11 * dL_dc;
+        dcov.v[2] = 2 * T00 * T02 * dL_da + (T00 * T12 + T02 * T10) * dL_db + 2 * T10 * T12 * dL_dc;
+        dcov.v[4] = 2 * T02 * T01 * dL_da + (T01 * T12 + T02 * T11) * dL_db + 2 * T11 * T12 * dL_dc;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dcov.v[i] = 0;
+    }
+    // Vrk[col][row]
+    const float V00 = V.c[0].x, V01 = V.c[0].y, V02 = V.c[0].z, V10 = V.c[1].x, V11 = V.c[1].y, V12 = V.c[1].z,
+                V20 = V.c[2].x, V21 = V.c[2].y, V22 = V.c[2].z;
+    const float dT00 = 2 * (T00 * V00 + T01 * V01 + T02 * V02) * dL_da + (T10 * V00 + T11 * V01 + T12 * V02) * dL_db;
+    const float dT01 = 2 * (T00 * V10 + T01 * V11 + T02 * V12) * dL_da + (T10 * V10 + T11 * V11 + T12 * V12) * dL_db;
+    const float dT02 = 2 * (T00 * V20 + T01 * V21 + T02 * V22) * dL_da + (T10 * V20 + T11 * V21 + T12 * V22) * dL_db;
+    const float dT10 = 2 * (T10 * V00 + T11 * V01 + T12 * V02) * dL_dc + (T00 * V00 + T01 * V01 + T02 * V02) * dL_db;
+    const float dT11 = 2 * (T10 * V10 + T11 * V11 + T12 * V12) * dL_dc + (T00 * V10 + T01 * V11 + T02 * V12) * dL_db;
+    const float dT12 = 2 * (T10 * V20 + T11 * V21 + T12 * V22) * dL_dc + (T00 * V20 + T01 * V21 + T02 * V22) * dL_db;
+    // W[col][row]
+    const float W00 = W.c[0].x, W01 = W.c[0].y, W02 = W.c[0].z, W10 = W.c[1].x, W11 = W.c[1].y, W12 = W.c[1].z,
+                W20 = W.c[2].x, W21 = W.c[2].y, W22 = W.c[2].z;
+    const float dJ00 = W00 * dT00 + W01 * dT01 + W02 * dT02;
+    const float dJ02 = W20 * dT00 + W21 * dT01 + W22 * dT02;
+    const float dJ11 = W10 * dT10 + W11 * dT11 + W12 * dT12;
+    const float dJ12 = W20 * dT10 + W21 * dT11 + W22 * dT12;
+    const float tz = 1.f / t.z;
+    const float tz2 = tz * tz;
+    const float tz3 = tz2 * tz;
+    const float dtx = xgm * -hx * tz2 * dJ02;
+    const float dty = ygm * -hy * tz2 * dJ12;
+    const float dtz = -hx * tz2 * dJ00 - hy * tz2 * dJ11 + (2 * hx * t.x) * tz3 * dJ02 + (2 * hy * t.y) * tz3 * dJ12;
+    dmean = xform_vec3_T(make_float3(dtx, dty, dtz), Vm);
+}
+
+// auxiliary.h:107-117 dnormvdv(float3)
+__device__ __forceinline__ float3 dnormvdv(const float3 v, const float3 dv) {
+    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    return make_float3(((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32,
+                       (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32,
+                       (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
+}
+
+// backward.cu:20-139 for one channel: writes the channel's dL/dsh, returns its (dRGB/dx, dRGB/dy, dRGB/dz)
+__device__ __forceinline__ float3 sh_channel_bwd(int deg, const float* __restrict__ s, float dRGB, float x, float y,
+                                                 float z, float* __restrict__ dsh) {
+    float dx = 0, dy = 0, dz = 0;
+    dsh[0] = kSH0 * dRGB;
+    if (deg > 0) {
+        dsh[3] = (-kSH1 * y) * dRGB;
+        dsh[6] = (kSH1 * z) * dRGB;
+        dsh[9] = (-kSH1 * x) * dRGB;
+        dx = -kSH1 * s[9];
+        dy = -kSH1 * s[3];
+        dz = kSH1 * s[6];
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            dsh[12] = (kSH2_0 * xy) * dRGB;
+            dsh[15] = (kSH2_1 * yz) * dRGB;
+            dsh[18] = (kSH2_2 * (2.f * zz - xx - yy)) * dRGB;
+            dsh[21] = (kSH2_3 * xz) * dRGB;
+            dsh[24] = (kSH2_4 * (xx - yy)) * dRGB;
+            dx += kSH2_0 * y * s[12] + kSH2_2 * 2.f * -x * s[18] + kSH2_3 * z * s[21] + kSH2_4 * 2.f * x * s[24];
+            dy += kSH2_0 * x * s[12] + kSH2_1 * z * s[15] + kSH2_2 * 2.f * -y * s[18] + kSH2_4 * 2.f * -y * s[24];
+            dz += kSH2_1 * y * s[15] + kSH2_2 * 2.f * 2.f * z * s[18] + kSH2_3 * x * s[21];
+            if (deg > 2) {
+                dsh[27] = (kSH3_0 * y * (3.f * xx - yy)) * dRGB;
+                dsh[30] = (kSH3_1 * xy * z) * dRGB;
+                dsh[33] = (kSH3_2 * y * (4.f * zz - xx - yy)) * dRGB;
+                dsh[36] = (kSH3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy)) * dRGB;
+                dsh[39] = (kSH3_4 * x * (4.f * zz - xx - yy)) * dRGB;
+                dsh[42] = (kSH3_5 * z * (xx - yy)) * dRGB;
+                dsh[45] = (kSH3_6 * x * (xx - 3.f * yy)) * dRGB;
+                dx += (kSH3_0 * s[27] * 3.f * 2.f * xy + kSH3_1 * s[30] * yz + kSH3_2 * s[33] * -2.f * xy +
+                       kSH3_3 * s[36] * -3.f * 2.f * xz + kSH3_4 * s[39] * (-3.f * xx + 4.f * zz - yy) +
+                       kSH3_5 * s[42] * 2.f * xz + kSH3_6 * s[45] * 3.f * (xx - yy));
+                dy += (kSH3_0 * s[27] * 3.f * (xx - yy) + kSH3_1 * s[30] * xz +
+                       kSH3_2 * s[33] * (-3.f * yy + 4.f * zz - xx) + kSH3_3 * s[36] * -3.f * 2.f * yz +
+                       kSH3_4 * s[39] * -2.f * xy + kSH3_5 * s[42] * -2.f * yz + kSH3_6 * s[45] * -3.f * 2.f * xy);
+                dz += (kSH3_1 * s[30] * xy + kSH3_2 * s[33] * 4.f * 2.f * yz +
+                       kSH3_3 * s[36] * 3.f * (2.f * zz - xx - yy) + kSH3_4 * s[39] * 4.f * 2.f * xz +
+                       kSH3_5 * s[42] * (xx - yy));
+            }
+        }
+    }
+    return make_float3(dx, dy, dz);
+}
+
+__device__ __forceinline__ void cov3d_bwd(const float3 scale, float mod, const float4 q, const Cov6& dc,
+                                          float3& dscale, float4& drot) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    const M3 R = quat_to_R(q);
+    M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    const float3 s = make_float3(mod * scale.x, mod * scale.y, mod * scale.z);
+    S.c[0].x = s.x;
+    S.c[1].y = s.y;
+    S.c[2].z = s.z;
+    const M3 M = m3_mul(S, R);
+    const M3 dSig = m3_cols(dc.v[0], 0.5f * dc.v[1], 0.5f * dc.v[2], 0.5f * dc.v[1], dc.v[3], 0.5f * dc.v[4],
+                            0.5f * dc.v[2], 0.5f * dc.v[4], dc.v[5]);
+    M3 M2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) M2.c[k] = make_float3(2.0f * M.c[k].x, 2.0f * M.c[k].y, 2.0f * M.c[k].z);
+    const M3 dM = m3_mul(M2, dSig);
+    const M3 Rt = m3_T(R);
+    M3 dMt = m3_T(dM);
+    dscale = make_float3(dot3(Rt.c[0], dMt.c[0]), dot3(Rt.c[1], dMt.c[1]), dot3(Rt.c[2], dMt.c[2]));
+    dMt.c[0] = make_float3(dMt.c[0].x * s.x, dMt.c[0].y * s.x, dMt.c[0].z * s.x);
+    dMt.c[1] = make_float3(dMt.c[1].x * s.y, dMt.c[1].y * s.y, dMt.c[1].z * s.y);
+    dMt.c[2] = make_float3(dMt.c[2].x * s.z, dMt.c[2].y * s.z, dMt.c[2].z * s.z);
+    const float D00 = dMt.c[0].x, D01 = dMt.c[0].y, D02 = dMt.c[0].z, D10 = dMt.c[1].x, D11 = dMt.c[1].y,
+                D12 = dMt.c[1].z, D20 = dMt.c[2].x, D21 = dMt.c[2].y, D22 = dMt.c[2].z;
+    drot.x = 2 * z * (D01 - D10) + 2 * y * (D20 - D02) + 2 * x * (D12 - D21);
+    drot.y = 2 * y * (D10 + D01) + 2 * z * (D20 + D02) + 2 * r * (D12 - D21) - 4 * x * (D22 + D11);
+    drot.z = 2 * x * (D10 + D01) + 2 * r * (D20 - D02) + 2 * z * (D12 + D21) - 4 * y * (D22 + D00);
+    drot.w = 2 * r * (D01 - D10) + 2 * x * (D20 + D02) + 2 * y * (D12 + D21) - 4 * z * (D11 + D00);
+}
+
+__global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= p.P || !(p.radii[idx] > 0)) return;
+    const Mat4 Vm = load_mat4(p.view);
+    const Mat4 Pm = load_mat4(p.proj);
+    const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+
+    // the 3D covariance the forward used (recomputed: cheaper than storing 24 B/G)
+    Cov6 c3;
+    float3 scale = make_float3(0, 0, 0);
+    float4 q = make_float4(0, 0, 0, 0);
+    if (p.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3.v[k] = p.cov3D_precomp[6 * idx + k];
+    } else {
+        scale = make_float3(p.scales[3 * idx], p.scales[3 * idx + 1], p.scales[3 * idx + 2]);
+        q = reinterpret_cast<const float4*>(p.rotations)[idx];
+        c3 = cov3d_from_scale_rot(scale, p.scale_modifier, q);
+    }
+    const float4 dcon4 = reinterpret_cast<const float4*>(p.dL_dconic)[idx];
+    float3 dmean;
+    Cov6 dcov;
+    cov2d_bwd(m, c3, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, Vm, make_float3(dcon4.x, dcon4.y, dcon4.w), dmean,
+              dcov);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = dcov.v[k];
+
+    // backward.cu:373-387 projective term from dL/dmean2D
+    const float4 mh = xform_point4(m, Pm);
+    const float mw = 1.0f / (mh.w + 0.0000001f);
+    const float* P = Pm.m;
+    const float mul1 = (P[0] * m.x + P[4] * m.y + P[8] * m.z + P[12]) * mw * mw;
+    const float mul2 = (P[1] * m.x + P[5] * m.y + P[9] * m.z + P[13]) * mw * mw;
+    const float d2x = p.dL_dmean2D[3 * idx], d2y = p.dL_dmean2D[3 * idx + 1];
+    float3 dm2;
+    dm2.x = (P[0] * mw - P[3] * mul1) * d2x + (P[1] * mw - P[3] * mul2) * d2y;
+    dm2.y = (P[4] * mw - P[7] * mul1) * d2x + (P[5] * mw - P[7] * mul2) * d2y;
+    dm2.z = (P[8] * mw - P[11] * mul1) * d2x + (P[9] * mw - P[11] * mul2) * d2y;
+    dmean = make_float3(dmean.x + dm2.x, dmean.y + dm2.y, dmean.z + dm2.z);
+
+    if (p.shs) {
+        const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+        const float3 dir_orig = make_float3(m.x - cam.x, m.y - cam.y, m.z - cam.z);
+        const float len = sqrtf(dot3(dir_orig, dir_orig));
+        const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+        const uint8_t cl = p.clamped[idx];
+        const float3 dc = make_float3(p.dL_dcolor[3 * idx] * ((cl & 1) ? 0 : 1),
+                                      p.dL_dcolor[3 * idx + 1] * ((cl & 2) ? 0 : 1),
+                                      p.dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0 : 1));
+        const float* row = p.shs + (size_t)idx * p.M * 3;
+        float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
+        float s[48];
+        const int nc = p.D >= 3 ? 16 : (p.D + 1) * (p.D + 1);
+        for (int k = 0; k < nc * 3; ++k) s[k] = row[k];
+        float ds[48];
+        const float3 gx = sh_channel_bwd(p.D, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
+        const float3 gy = sh_channel_bwd(p.D, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
+        const float3 gz = sh_channel_bwd(p.D, s + 2, dc.z, dir.x, dir.y, dir.z, ds + 2);
+        for (int k = 0; k < nc * 3; ++k) drow[k] = ds[k];
+        // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
+        const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
+                                        gx.z * dc.x + gy.z * dc.y + gz.z * dc.z);
+        const float3 dmn = dnormvdv(dir_orig, ddir);
+        dmean = make_float3(dmean.x + dmn.x, dmean.y + dmn.y, dmean.z + dmn.z);
+    }
+    p.dL_dmeans3D[3 * idx] = dmean.x;
+    p.dL_dmeans3D[3 * idx + 1] = dmean.y;
+    p.dL_dmeans3D[3 * idx + 2] = dmean.z;
+
+    if (p.scales) {
+        float3 dscale;
+        float4 drot;
+        cov3d_bwd(scale, p.scale_modifier, q, dcov, dscale, drot);
+        p.dL_dscales[3 * idx] = dscale.x;
+        p.dL_dscales[3 * idx + 1] = dscale.y;
+        p.dL_dscales[3 * idx + 2] = dscale.z;
+        reinterpret_cast<float4*>(p.dL_drotations)[idx] = drot;
+    }
+}
+
+}  // namespace gsd
+
+namespace gsd {
+void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
+    if (p.P > 0) hipLaunchKernelGGL(k_preprocess_fwd, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+}
+void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s) {
+    if (p.P > 0) hipLaunchKernelGGL(k_preprocess_bwd, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+}
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s) {
+    if (P > 0) hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);
+}
+}  // namespace gsd

@@ -1,0 +1,188 @@
+"""Torch-facing mirror of the reference's pybind module ``_C``.
+
+Same three functions, argument order, return tuples and error messages as
+``submodules/diff-gaussian-rasterization/ext.cpp:15-19`` /
+``rasterize_points.cu:35-217``; each call unwraps torch tensors into device
+pointers and goes through the C-ABI of ``include/gsd_raster.h`` on the
+tensors' device and torch's current HIP stream (the reference used the
+legacy default stream and the *current* device -- rasterize_points.cu:71).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+
+_i64 = ctypes.c_int64
+
+
+def _stream(dev: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _absent(t) -> bool:
+    """The reference's placeholders are empty tensors (``torch.Tensor([])``) -> nullptr."""
+    return t is None or t.numel() == 0
+
+
+def _dev_f32(t: torch.Tensor, name: str, dev: torch.device) -> torch.Tensor:
+    if t.device != dev:
+        raise RuntimeError(f"{name} must be on {dev} (got {t.device}); the rasterizer has no CPU path")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+class _Args:
+    """Holds the contiguous device tensors alive for the duration of one native call."""
+
+    def __init__(self, background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                 viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                 prefiltered, debug):
+        dev = means3D.device
+        if dev.type != "cuda":
+            raise RuntimeError("means3D must be a HIP device tensor: this rasterizer has no CPU implementation")
+        self.dev = dev
+        self.P = int(means3D.size(0))
+        self.means3D = _dev_f32(means3D, "means3D", dev)
+        self.bg = _dev_f32(background, "bg", dev)
+        self.opacity = None if (opacity is None or not self.P) else _dev_f32(opacity, "opacities", dev)
+        self.sh = None if _absent(sh) else _dev_f32(sh, "sh", dev)
+        self.colors = None if _absent(colors) else _dev_f32(colors, "colors_precomp", dev)
+        self.scales = None if _absent(scales) else _dev_f32(scales, "scales", dev)
+        self.rotations = None if _absent(rotations) else _dev_f32(rotations, "rotations", dev)
+        self.cov3D = None if _absent(cov3D_precomp) else _dev_f32(cov3D_precomp, "cov3D_precomp", dev)
+        self.view = _dev_f32(viewmatrix, "viewmatrix", dev)
+        self.proj = _dev_f32(projmatrix, "projmatrix", dev)
+        self.campos = _dev_f32(campos, "campos", dev)
+        self.M = 0 if self.sh is None else int(self.sh.size(1))  # rasterize_points.cu:83-87
+        self.H, self.W = int(image_height), int(image_width)
+        self.c = _native.RasterArgs(
+            P=self.P, D=int(degree), M=self.M, width=self.W, height=self.H,
+            scale_modifier=float(scale_modifier), tan_fovx=float(tan_fovx), tan_fovy=float(tan_fovy),
+            prefiltered=int(bool(prefiltered)), debug=int(bool(debug)),
+            background=_ptr(self.bg).value, means3D=_ptr(self.means3D).value, shs=_ptr(self.sh).value,
+            colors_precomp=_ptr(self.colors).value, opacities=_ptr(self.opacity).value,
+            scales=_ptr(self.scales).value, rotations=_ptr(self.rotations).value,
+            cov3D_precomp=_ptr(self.cov3D).value, viewmatrix=_ptr(self.view).value,
+            projmatrix=_ptr(self.proj).value, campos=_ptr(self.campos).value)
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered, debug):
+    """RasterizeGaussiansCUDA (rasterize_points.cu:35-115):
+    -> (num_rendered, color (3,H,W), radii (P,) int32, geomBuffer, binningBuffer, imgBuffer)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    lib = _native.load()
+    a = _Args(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+              projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug)
+    dev, P, H, W = a.dev, a.P, a.H, a.W
+    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    byte = dict(dtype=torch.uint8, device=dev)
+    if P == 0:
+        empty = torch.empty(0, **byte)
+        return 0, torch.zeros(3, H, W, dtype=torch.float32, device=dev), radii, empty, empty.clone(), empty.clone()
+    with torch.cuda.device(dev):
+        stream = _stream(dev)
+        geom = torch.empty(lib.gsd_geom_buffer_bytes(P), **byte)
+        img = torch.empty(lib.gsd_image_buffer_bytes(W, H), **byte)
+        K = _i64(0)
+        _native.check(lib.gsd_rasterize_forward_bin(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(radii),
+                                                    ctypes.byref(K), stream))
+        num_rendered = int(K.value)
+        binning = torch.empty(lib.gsd_binning_buffer_bytes(num_rendered), **byte)
+        color = torch.empty(3, H, W, dtype=torch.float32, device=dev)
+        _native.check(lib.gsd_rasterize_forward_render(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(binning),
+                                                       num_rendered, _ptr(radii), _ptr(color), stream))
+    return num_rendered, color, radii, geom, binning, img
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer, debug):
+    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196):
+    -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)."""
+    lib = _native.load()
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))  # rasterize_points.cu:142-143
+    a = _Args(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+              projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
+    dev, P, M = a.dev, a.P, a.M
+    # one zero-filled slab for every gradient (a single memset instead of nine);
+    # the float4-accessed arrays (conic, rotation) first so they stay 16-B aligned
+    widths = [4, 4, 3, 3, 1, 3, 6, M * 3, 3]
+    slab = torch.zeros(P * sum(widths), dtype=torch.float32, device=dev)
+    views, off = [], 0
+    for w in widths:
+        views.append(slab[off:off + P * w].view(P, w))
+        off += P * w
+    dconic, drot, dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales = views
+    dsh = dsh.view(P, M, 3)
+    if P != 0:
+        dout = _dev_f32(dL_dout_color, "dL_dout_color", dev)
+        radii_c = radii.contiguous()
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_rasterize_backward(
+                ctypes.byref(a.c), _ptr(radii_c), _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer), int(R),
+                _ptr(dout), _ptr(dmeans2D), _ptr(dconic), _ptr(dopacity), _ptr(dcolors), _ptr(dmeans3D),
+                _ptr(dcov3D), _ptr(dsh if M else None), _ptr(dscales), _ptr(drot), _stream(dev)))
+    return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (rasterize_points.cu:198-217) -> bool (P,)."""
+    lib = _native.load()
+    P = int(means3D.size(0))
+    dev = means3D.device
+    present = torch.zeros(P, dtype=torch.bool, device=dev)
+    if P != 0:
+        if dev.type != "cuda":
+            raise RuntimeError("means3D must be a HIP device tensor: this rasterizer has no CPU implementation")
+        m = _dev_f32(means3D, "means3D", dev)
+        v = _dev_f32(viewmatrix, "viewmatrix", dev)
+        p = _dev_f32(projmatrix, "projmatrix", dev)
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(dev)))
+    return present
+
+
+def se3_deform_forward(twist, means, rotations=None):
+    """Fused per-Gaussian SE(3) deform (gsd_se3_deform_forward) -> (means', rotations' or None)."""
+    lib = _native.load()
+    dev = means.device
+    P = int(means.size(0))
+    tw = _dev_f32(twist, "twist", dev)
+    m = _dev_f32(means, "means3D", dev)
+    q = None if rotations is None else _dev_f32(rotations, "rotations", dev)
+    mo = torch.empty_like(m)
+    qo = None if q is None else torch.empty_like(q)
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_se3_deform_forward(P, _ptr(tw), _ptr(m), _ptr(q), _ptr(mo), _ptr(qo), _stream(dev)))
+    return mo, qo
+
+
+def se3_deform_backward(twist, means, rotations, dL_dmeans_out, dL_drot_out):
+    lib = _native.load()
+    dev = means.device
+    P = int(means.size(0))
+    tw = _dev_f32(twist, "twist", dev)
+    m = _dev_f32(means, "means3D", dev)
+    q = None if rotations is None else _dev_f32(rotations, "rotations", dev)
+    gm = _dev_f32(dL_dmeans_out, "dL_dmeans", dev)
+    gq = None
+    if q is not None:
+        gq = torch.zeros_like(q) if dL_drot_out is None else _dev_f32(dL_drot_out, "dL_drot", dev)
+    dtw = torch.empty_like(tw)
+    dm = torch.empty_like(m)
+    dq = None if q is None else torch.empty_like(q)
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_se3_deform_backward(P, _ptr(tw), _ptr(m), _ptr(q), _ptr(gm), _ptr(gq), _ptr(dtw),
+                                                  _ptr(dm), _ptr(dq), _stream(dev)))
+    return dtw, dm, dq

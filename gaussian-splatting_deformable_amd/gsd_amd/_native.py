@@ -1,0 +1,84 @@
+"""Loader for libgsd_hip.so -- the C-ABI of include/gsd_raster.h.
+
+There is no fallback: if the HIP library is missing or stale the import of the
+product path fails loudly (the parity claims rest on the HIP kernels being the
+code that runs).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
+ABI_VERSION = 1
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_sz = ctypes.c_size_t
+
+
+class RasterArgs(ctypes.Structure):
+    """Mirror of ``gsd_raster_args`` (include/gsd_raster.h)."""
+
+    _fields_ = [
+        ("P", _i32), ("D", _i32), ("M", _i32), ("width", _i32), ("height", _i32),
+        ("scale_modifier", _f32), ("tan_fovx", _f32), ("tan_fovy", _f32),
+        ("prefiltered", _i32), ("debug", _i32),
+        ("background", _vp), ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp),
+        ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp), ("projmatrix", _vp),
+        ("campos", _vp),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/gsd_raster.h declares
+SIGNATURES = {
+    "gsd_abi_version": (_i32, []),
+    "gsd_last_error": (ctypes.c_char_p, []),
+    "gsd_geom_buffer_bytes": (_sz, [_i32]),
+    "gsd_image_buffer_bytes": (_sz, [_i32, _i32]),
+    "gsd_binning_buffer_bytes": (_sz, [_i64]),
+    "gsd_state_layout": (None, [_i32, _i32, _i32, _i64, ctypes.POINTER(_sz), ctypes.POINTER(_sz),
+                                ctypes.POINTER(_sz)]),
+    "gsd_rasterize_forward_bin": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, ctypes.POINTER(_i64), _vp]),
+    "gsd_rasterize_forward_render": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "gsd_rasterize_backward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                                      _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_se3_deform_forward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_se3_deform_backward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and type the library once; raises if it is absent or ABI-mismatched."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"gsd: HIP library not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (make -C gaussian-splatting_deformable_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gsd_abi_version() != ABI_VERSION:
+        raise ImportError(f"gsd: {LIB_PATH} has ABI {lib.gsd_abi_version()}, expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = _lib.gsd_last_error().decode("utf-8", "replace")
+        raise NativeError(msg)

@@ -1,0 +1,219 @@
+"""Drop-in ``render()`` (L2) and the minimal Gaussian container it reads.
+
+``render`` mirrors ``gaussian_renderer/__init__.py:20-195``: same signature,
+same camera/model attributes read, same returned dict.  The deform preamble
+(``:79-140``) supports the reference's live additive mode
+(``xyz + dx``, ``exp(s + ds)``, ``normalize(q + dq)``, ``features + dSH``) and
+the SE(3) mode the north star asks for (twist -> fused HIP exp-map on means
+and rotations, ``gsd_amd.deform``).  The deformation network that produces
+offsets/twists is outside the hot path: any callable
+``offset_model(pts, time, iteration)`` can be plugged in.
+"""
+from __future__ import annotations
+
+import math
+from types import SimpleNamespace
+
+import torch
+import torch.nn.functional as F
+
+from .deform import se3_deform
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+from .sh import eval_sh
+
+
+def inverse_sigmoid(x):
+    return torch.log(x / (1 - x))
+
+
+def build_rotation(r):
+    """utils/general_utils.py:78-99 (device taken from the input)."""
+    norm = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1] + r[:, 2] * r[:, 2] + r[:, 3] * r[:, 3])
+    q = r / norm[:, None]
+    R = torch.zeros((q.size(0), 3, 3), device=r.device, dtype=r.dtype)
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R[:, 0, 0] = 1 - 2 * (y * y + z * z)
+    R[:, 0, 1] = 2 * (x * y - r * z)
+    R[:, 0, 2] = 2 * (x * z + r * y)
+    R[:, 1, 0] = 2 * (x * y + r * z)
+    R[:, 1, 1] = 1 - 2 * (x * x + z * z)
+    R[:, 1, 2] = 2 * (y * z - r * x)
+    R[:, 2, 0] = 2 * (x * z - r * y)
+    R[:, 2, 1] = 2 * (y * z + r * x)
+    R[:, 2, 2] = 1 - 2 * (x * x + y * y)
+    return R
+
+
+def build_scaling_rotation(s, r):
+    """utils/general_utils.py:101-110."""
+    L = torch.zeros((s.shape[0], 3, 3), dtype=s.dtype, device=s.device)
+    R = build_rotation(r)
+    L[:, 0, 0], L[:, 1, 1], L[:, 2, 2] = s[:, 0], s[:, 1], s[:, 2]
+    return R @ L
+
+
+def strip_symmetric(L):
+    """utils/general_utils.py:64-76 (upper triangle of the symmetric matrix)."""
+    return torch.stack([L[:, 0, 0], L[:, 0, 1], L[:, 0, 2], L[:, 1, 1], L[:, 1, 2], L[:, 2, 2]], dim=1)
+
+
+def build_covariance_from_scaling_rotation(scaling, scaling_modifier, rotation):
+    """scene/gaussian_model.py:634-638."""
+    L = build_scaling_rotation(scaling_modifier * scaling, rotation)
+    return strip_symmetric(L @ L.transpose(1, 2))
+
+
+class ZeroOffsets:
+    """Deformation producer returning the reference's pre-3000-iteration zeros
+    (scene/gaussian_model.py:305-313) -- (dx, dscale, drot, dSH)."""
+
+    def __call__(self, pts, time, iteration):
+        P = pts.shape[0]
+        z = pts.new_zeros
+        return z(P, 3), z(P, 3), z(P, 4), z(P, 48)
+
+
+class DeformableGaussians:
+    """The subset of scene/gaussian_model.py:GaussianModel that render() reads
+    (:632-801): raw parameters, activations, get_xyz_all, get_features,
+    get_covariance.  ``deform`` = "additive" (live reference path) or "se3"."""
+
+    def __init__(self, params, sh_degree=3, deform="additive", offset_model=None, twist_model=None,
+                 requires_grad=True):
+        p = params
+        mk = (lambda t: torch.nn.Parameter(t.contiguous(), requires_grad=requires_grad))
+        self._xyz = mk(p.xyz)
+        self._scaling = mk(p.scaling)
+        self._rotation = mk(p.rotation)
+        self._opacity = mk(p.opacity)
+        self._features_dc = mk(p.features_dc)
+        self._features_rest = mk(p.features_rest)
+        self._twist = None if p.twist is None else mk(p.twist)
+        self.max_sh_degree = sh_degree
+        self.active_sh_degree = sh_degree
+        self.deform = deform
+        self.offset_model = offset_model or ZeroOffsets()
+        self.twist_model = twist_model
+        self.scaling_activation = torch.exp
+        self.scaling_inverse_activation = torch.log
+        self.opacity_activation = torch.sigmoid
+        self.inverse_opacity_activation = inverse_sigmoid
+        self.rotation_activation = F.normalize
+        self.covariance_activation = build_covariance_from_scaling_rotation
+
+    def parameters(self):
+        ps = [self._xyz, self._features_dc, self._features_rest, self._opacity, self._scaling, self._rotation]
+        if self._twist is not None:
+            ps.append(self._twist)
+        return ps
+
+    @property
+    def get_xyz(self):
+        return self._xyz
+
+    @property
+    def get_scaling(self):
+        return self.scaling_activation(self._scaling)
+
+    @property
+    def get_rotation_ori(self):
+        return self.rotation_activation(self._rotation)
+
+    @property
+    def get_features(self):
+        return torch.cat((self._features_dc, self._features_rest), dim=1)
+
+    @property
+    def get_opacity(self):
+        return self.opacity_activation(self._opacity)
+
+    def get_covariance(self, scaling_modifier=1):
+        return self.covariance_activation(self.get_scaling, scaling_modifier, self._rotation)
+
+    def get_twist(self, pts, time, iteration):
+        if self.twist_model is not None:
+            return self.twist_model(pts, time, iteration)
+        return self._twist
+
+    def get_xyz_all(self, pts, time, iteration):
+        """scene/gaussian_model.py:761-763 -> (means3D, means3D_ori, offset, scale_off, rot_off, mlp_shs)."""
+        dx, ds, dq, dsh = self.offset_model(pts, time, iteration)
+        if self.deform == "se3":
+            twist = self.get_twist(pts, time, iteration)
+            means, _ = se3_deform(twist, self._xyz + dx)
+            return means, self._xyz, means - self._xyz, ds, dq, dsh
+        return self._xyz + dx, self._xyz, dx, ds, dq, dsh
+
+
+def se3_rot_or(pc, rot_offset, se3_rotations):
+    """Rotations fed to the rasterizer: normalize(q + dq) (additive, :122) or its SE(3)-moved version."""
+    if se3_rotations is not None:
+        return se3_rotations
+    return pc.rotation_activation(pc._rotation + rot_offset)
+
+
+def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1.0, override_color=None,
+           save_ply=False, control_time=None):
+    """gaussian_renderer/__init__.py:20-195."""
+    dev = pc.get_xyz.device
+    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True, device=dev) + 0
+    try:
+        screenspace_points.retain_grad()
+    except Exception:
+        pass
+    tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
+    tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=tanfovx, tanfovy=tanfovy, bg=bg_color, scale_modifier=scaling_modifier,
+        viewmatrix=viewpoint_camera.world_view_transform, projmatrix=viewpoint_camera.full_proj_transform,
+        sh_degree=pc.active_sh_degree, campos=viewpoint_camera.camera_center, prefiltered=False,
+        debug=getattr(pipe, "debug", False))
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    means3D = pc.get_xyz
+    t = control_time if control_time is not None else viewpoint_camera.time
+    time = torch.full((means3D.size(0), 1), t, device=means3D.device)
+    se3_rot = getattr(pc, "deform", "additive") == "se3" and not getattr(pipe, "compute_cov3D_python", False)
+    if se3_rot:
+        # one fused kernel moves means AND rotations by the same rigid motion
+        dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, time, iteration)
+        twist = pc.get_twist(means3D, time, iteration)
+        means3D_ori = pc._xyz
+        means3D, se3_rotations = se3_deform(twist, pc._xyz + dx, pc.rotation_activation(pc._rotation + rot_offset))
+        means3D_offset = means3D - means3D_ori
+    else:
+        means3D, means3D_ori, means3D_offset, scale_offset, rot_offset, mlp_shs = pc.get_xyz_all(means3D, time,
+                                                                                                 iteration)
+    means2D = screenspace_points
+    opacity = pc.get_opacity
+    scales = rotations = cov3D_precomp = None
+    if getattr(pipe, "compute_cov3D_python", False):
+        cov3D_precomp = pc.get_covariance(scaling_modifier)
+    else:
+        scales = pc.scaling_activation(pc._scaling + scale_offset)
+        rotations = se3_rot_or(pc, rot_offset, se3_rotations if se3_rot else None)
+    shs = colors_precomp = None
+    if override_color is None:
+        if getattr(pipe, "convert_SHs_python", False):
+            shs_view = pc.get_features.transpose(1, 2).view(-1, 3, (pc.max_sh_degree + 1) ** 2)
+            dir_pp = pc.get_xyz - viewpoint_camera.camera_center.repeat(pc.get_features.shape[0], 1)
+            dir_pp_normalized = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+            sh2rgb = eval_sh(pc.active_sh_degree, shs_view, dir_pp_normalized)
+            colors_precomp = torch.clamp_min(sh2rgb + 0.5, 0.0)
+        else:
+            shs = pc.get_features + mlp_shs.reshape(-1, 16, 3)
+    else:
+        colors_precomp = override_color
+    rendered_image, radii = rasterizer(means3D=means3D, means2D=means2D, shs=shs, colors_precomp=colors_precomp,
+                                       opacities=opacity, scales=scales, rotations=rotations,
+                                       cov3D_precomp=cov3D_precomp)
+    return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
+            "radii": radii, "means3D": means3D, "means3D_ori": means3D_ori, "rotations": rotations,
+            "means3D_offset": means3D_offset, "opacities": opacity, "rot_offset": rot_offset}
+
+
+def default_pipe(**kw):
+    """PipelineParams (arguments/__init__.py:64-69)."""
+    d = dict(convert_SHs_python=False, compute_cov3D_python=False, debug=False)
+    d.update(kw)
+    return SimpleNamespace(**d)

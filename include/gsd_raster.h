@@ -1,0 +1,145 @@
+/*
+ * gsd_raster.h -- C-ABI of the MI355X-native deformable Gaussian-splatting
+ * rasterizer (libgsd_hip.so, built from gaussian-splatting_deformable_amd/csrc).
+ *
+ * Plain pointers and sizes only: every tensor argument is a device pointer to
+ * contiguous float32/int32/uint8 memory owned by the caller, every `stream` is a
+ * hipStream_t (NULL = legacy default stream).  The library never allocates
+ * device memory on the data path and never frees caller memory; the three
+ * opaque state buffers are sized by the *_bytes() queries and allocated by the
+ * caller (the two-phase protocol that replaces the reference's resizable
+ * std::function<char*(size_t)> byte tensors, rasterize_points.cu:27-33).
+ *
+ * Every entry point returns GSD_OK (0) or an error code; gsd_last_error()
+ * returns the message (thread-local), using the reference's wording where the
+ * reference raises (rasterize_points.cu:57-59, rasterizer_impl.cu:242-245).
+ *
+ * Reference interfaces replaced (Heng14/gaussian-splatting_deformable):
+ *   gsd_rasterize_forward_bin + gsd_rasterize_forward_render
+ *        <- _C.rasterize_gaussians  / RasterizeGaussiansCUDA
+ *           (submodules/diff-gaussian-rasterization/rasterize_points.cu:35-115,
+ *            bound at ext.cpp:16) and CudaRasterizer::Rasterizer::forward
+ *           (cuda_rasterizer/rasterizer_impl.cu:198-336)
+ *   gsd_rasterize_backward
+ *        <- _C.rasterize_gaussians_backward / RasterizeGaussiansBackwardCUDA
+ *           (rasterize_points.cu:117-196, ext.cpp:17) and Rasterizer::backward
+ *           (rasterizer_impl.cu:340-434)
+ *   gsd_mark_visible
+ *        <- _C.mark_visible / markVisible (rasterize_points.cu:198-217, ext.cpp:18)
+ *           and Rasterizer::markVisible (rasterizer_impl.cu:141-153)
+ *   gsd_se3_deform_forward / gsd_se3_deform_backward
+ *        <- scene/rigid_body.py exp_se3 (:86-93) applied per Gaussian as in
+ *           gaussian_renderer/__init__.py:90-95 (commented out upstream), with
+ *           the twist normalisation of scene/gaussian_model.py:161-165 and
+ *           torch autograd as the reference backward.
+ */
+#ifndef GSD_RASTER_H
+#define GSD_RASTER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSD_ABI_VERSION 1
+
+enum {
+    GSD_OK = 0,
+    GSD_ERR_ARG = 1,     /* invalid argument (AT_ERROR / std::runtime_error upstream) */
+    GSD_ERR_HIP = 2,     /* HIP runtime error (CHECK_CUDA upstream, auxiliary.h:166-173) */
+    GSD_ERR_STATE = 3    /* inconsistent state buffers (wrong size / wrong call order) */
+};
+
+/* Raster settings + per-Gaussian inputs of one view.  Mirrors the 19 arguments
+ * of _C.rasterize_gaussians (rasterize_points.cu:36-55).  Absent optional
+ * inputs are NULL (the reference passes empty tensors -> nullptr). */
+typedef struct gsd_raster_args {
+    int32_t P;                  /* number of Gaussians */
+    int32_t D;                  /* active SH degree (0..3) */
+    int32_t M;                  /* SH coefficients per Gaussian (sh.size(1)); 0 if shs == NULL */
+    int32_t width, height;      /* image size in pixels */
+    float scale_modifier;
+    float tan_fovx, tan_fovy;
+    int32_t prefiltered;        /* bool */
+    int32_t debug;              /* bool: synchronise + check after every kernel */
+    const float* background;    /* (3) */
+    const float* means3D;       /* (P,3) */
+    const float* shs;           /* (P,M,3) or NULL */
+    const float* colors_precomp;/* (P,3) or NULL (exactly one of shs / colors_precomp) */
+    const float* opacities;     /* (P,1) */
+    const float* scales;        /* (P,3) or NULL */
+    const float* rotations;     /* (P,4) or NULL (quaternion r,x,y,z; NOT normalised here) */
+    const float* cov3D_precomp; /* (P,6) or NULL (exactly one of scales+rotations / cov3D_precomp) */
+    const float* viewmatrix;    /* (4,4), column-major as stored by scene/cameras.py:55 */
+    const float* projmatrix;    /* (4,4) full projection, scene/cameras.py:57 */
+    const float* campos;        /* (3) */
+} gsd_raster_args;
+
+int gsd_abi_version(void);
+const char* gsd_last_error(void);
+
+/* State-buffer sizes in bytes (GeometryState / ImageState / BinningState,
+ * rasterizer_impl.h:29-73; layouts are private to this library). */
+size_t gsd_geom_buffer_bytes(int32_t P);
+size_t gsd_image_buffer_bytes(int32_t width, int32_t height);
+size_t gsd_binning_buffer_bytes(int64_t num_rendered);
+
+/* Introspection (tests / debugging; the reference exposes none): byte offsets,
+ * from the state buffer's first 256-B aligned address, of
+ *   geom[6]  = means2D float2, conic_opacity float4, rgb float4, depths f32, radii i32, clamped u8
+ *   image[6] = final_T f32, n_contrib u32, ranges uint2, tile_count u32, tile_cursor u32, counters u32
+ *   bin[3]   = bucket keys u64, merge scratch u64, point_list u32                          */
+void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t num_rendered, size_t* geom_offsets,
+                      size_t* image_offsets, size_t* binning_offsets);
+
+/* Forward, phase 1: preprocess (EWA projection, SH -> RGB, radii) and per-tile
+ * binning counts.  Writes radii (P) and *num_rendered (the sum of tiles
+ * touched; one blocking device->host read, as rasterizer_impl.cu:281). */
+int gsd_rasterize_forward_bin(const gsd_raster_args* args, void* geom_buffer, void* image_buffer,
+                              int32_t* radii, int64_t* num_rendered, void* stream);
+
+/* Forward, phase 2: emit (tile, depth) instances, order them (bit-exact with a
+ * stable sort on the reference key |tile|depth bits|), composite front to
+ * back.  binning_buffer holds gsd_binning_buffer_bytes(num_rendered) bytes.
+ * out_color is (3,H,W). */
+int gsd_rasterize_forward_render(const gsd_raster_args* args, void* geom_buffer, void* image_buffer,
+                                 void* binning_buffer, int64_t num_rendered, const int32_t* radii,
+                                 float* out_color, void* stream);
+
+/* Backward (rasterizer_impl.cu:340-434).  Output arrays must be zero-filled
+ * by the caller (torch::zeros upstream, rasterize_points.cu:151-159):
+ * dL_dmeans2D (P,3), dL_dcolors (P,3), dL_dopacity (P,1), dL_dmeans3D (P,3),
+ * dL_dcov3D (P,6), dL_dsh (P,M,3) (may be NULL if M == 0), dL_dscales (P,3),
+ * dL_drotations (P,4), and the scratch dL_dconic (P,4) (float4 view of (P,2,2)). */
+int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, const void* geom_buffer,
+                           const void* binning_buffer, const void* image_buffer, int64_t num_rendered,
+                           const float* dL_dout_color, float* dL_dmeans2D, float* dL_dconic,
+                           float* dL_dopacity, float* dL_dcolors, float* dL_dmeans3D, float* dL_dcov3D,
+                           float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream);
+
+/* Near-plane visibility test (auxiliary.h:139-164): present[i] = 1/0. */
+int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream);
+
+/* Per-Gaussian SE(3) deform.  twist (P,6) = raw [w, v] as produced by the
+ * deformation network (scene/gaussian_model.py:156); theta = |w|,
+ * R = exp_so3(w/theta, theta), p = (theta I + (1-cos) W^ + (theta-sin) W^2) v/theta
+ * (rigid_body.py:61-93), evaluated through series near theta = 0 so a zero
+ * twist is the identity (the reference NaNs there).  means_out = R x + p;
+ * rot_out = normalize(q_R (x) q) with q_R = (cos theta/2, sin theta/2 * w/theta)
+ * (Hamilton product, helpers.py:63-70).  rot_in / rot_out may be NULL. */
+int gsd_se3_deform_forward(int32_t P, const float* twist, const float* means_in, const float* rot_in,
+                           float* means_out, float* rot_out, void* stream);
+
+/* Backward of gsd_se3_deform_forward: overwrites dL_dtwist (P,6), dL_dmeans_in
+ * (P,3) and (if rot_in != NULL) dL_drot_in (P,4). */
+int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in, const float* rot_in,
+                            const float* dL_dmeans_out, const float* dL_drot_out, float* dL_dtwist,
+                            float* dL_dmeans_in, float* dL_drot_in, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSD_RASTER_H */

@@ -1,0 +1,92 @@
+"""The C-ABI library: loads without a GPU, exports every symbol include/*.h
+declares, and its struct layout matches the ctypes mirror (no compute calls)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gsd_raster.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsd_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from gsd_amd import _native
+    lib = _native.load()
+    names = declared_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _native.SIGNATURES, f"{n} has no ctypes signature"
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (gsd_\w+)", out))
+    assert set(names) <= exported
+
+
+def test_abi_version_and_sizes():
+    from gsd_amd import _native
+    lib = _native.load()
+    assert lib.gsd_abi_version() == _native.ABI_VERSION
+    assert lib.gsd_geom_buffer_bytes(0) > 0
+    assert lib.gsd_geom_buffer_bytes(1000) > lib.gsd_geom_buffer_bytes(10)
+    assert lib.gsd_binning_buffer_bytes(1_000_000) >= 20_000_000    # 8 + 8 + 4 B per instance
+    assert lib.gsd_image_buffer_bytes(1920, 1080) >= 1920 * 1080 * 8
+
+
+def test_state_layout_is_aligned_and_disjoint():
+    from gsd_amd import _native
+    lib = _native.load()
+    go, io, bo = (ctypes.c_size_t * 6)(), (ctypes.c_size_t * 6)(), (ctypes.c_size_t * 3)()
+    lib.gsd_state_layout(1001, 333, 217, 12345, go, io, bo)
+    for arr in (list(go), list(io), list(bo)):
+        assert all(o % 256 == 0 for o in arr)
+        assert arr == sorted(arr) and len(set(arr)) == len(arr)
+    assert go[5] + 1001 <= lib.gsd_geom_buffer_bytes(1001) - 256
+
+
+def test_struct_layout_matches_c(tmp_path):
+    from gsd_amd._native import RasterArgs
+    c = tmp_path / "sz.c"
+    c.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\nint main(){printf("%%zu %%zu %%zu %%zu",'
+                 ' sizeof(gsd_raster_args), offsetof(gsd_raster_args, scale_modifier),'
+                 ' offsetof(gsd_raster_args, background), offsetof(gsd_raster_args, campos));}\n' % HEADER)
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", str(c), "-o", str(exe)])
+    size, sm, bgo, cpo = map(int, subprocess.check_output([str(exe)]).split())
+    assert size == ctypes.sizeof(RasterArgs)
+    assert (sm, bgo, cpo) == (RasterArgs.scale_modifier.offset, RasterArgs.background.offset,
+                              RasterArgs.campos.offset)
+
+
+def test_argument_errors_without_gpu():
+    """Validation happens before any device work, with the reference's messages."""
+    from gsd_amd import _native
+    lib = _native.load()
+    a = _native.RasterArgs(P=10, D=3, M=16, width=64, height=64, scale_modifier=1.0, tan_fovx=0.5, tan_fovy=0.5,
+                           means3D=8, opacities=8, viewmatrix=8, projmatrix=8, background=8, campos=8,
+                           scales=8, rotations=8)
+    K = ctypes.c_int64(0)
+    rc = lib.gsd_rasterize_forward_bin(ctypes.byref(a), None, None, None, ctypes.byref(K), None)
+    assert rc == 1 and b"excatly one of either SHs or precomputed colors" in lib.gsd_last_error()
+    a.shs = 8
+    a.cov3D_precomp = 8
+    rc = lib.gsd_rasterize_forward_bin(ctypes.byref(a), None, None, None, ctypes.byref(K), None)
+    assert rc == 1 and b"scale/rotation pair or precomputed 3D covariance" in lib.gsd_last_error()
+    a.cov3D_precomp = None
+    a.M = 9
+    rc = lib.gsd_rasterize_forward_bin(ctypes.byref(a), None, None, None, ctypes.byref(K), None)
+    assert rc == 1 and b"fewer coefficients" in lib.gsd_last_error()
+    a.P = -1
+    rc = lib.gsd_rasterize_forward_bin(ctypes.byref(a), None, None, None, ctypes.byref(K), None)
+    assert rc == 1 and b"means3D must have dimensions (num_points, 3)" in lib.gsd_last_error()
+    a.P = 0
+    assert lib.gsd_rasterize_forward_bin(ctypes.byref(a), None, None, None, ctypes.byref(K), None) == 0
+    assert K.value == 0

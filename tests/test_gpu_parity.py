@@ -1,0 +1,267 @@
+"""HIP path (through the C-ABI) vs the CPU oracle -- the parity tests proper.
+
+Bars (DESIGN.md "Parity"):
+  bit-exact   radii, depths, means2D, conic/opacity, rgb, clamp flags, num_rendered,
+              ranges, point_list (== the reference's stable sort of |tile|depth| keys)
+  tolerance   image |max abs| <= 1e-5 (expf ulp differences), n_contrib mismatches
+              <= 0.1% of pixels; gradients: per-tensor relative L2 <= 1e-4 (float atomics
+              reorder sums), SE(3) deform vs float64 autograd: rel L2 <= 1e-5.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import oracle_kwargs, scene_inputs
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def gpu_forward(d, *, colors=None, cov3D=None, scale_modifier=1.0, prefiltered=False, debug=False):
+    from gsd_amd import _C
+    empty = torch.empty(0)
+    shs = d["shs"] if colors is None else empty
+    scales, rots = (d["scales"], d["rotations"]) if cov3D is None else (empty, empty)
+    return _C.rasterize_gaussians(d["bg"], d["means3D"], empty if colors is None else colors, d["opacities"], scales,
+                                  rots, scale_modifier, empty if cov3D is None else cov3D, d["viewmatrix"],
+                                  d["projmatrix"], d["tanfovx"], d["tanfovy"], d["H"], d["W"], shs, d["sh_degree"],
+                                  d["campos"], prefiltered, debug)
+
+
+def gpu_backward(d, fwd, dpix, *, colors=None, cov3D=None, scale_modifier=1.0):
+    from gsd_amd import _C
+    num_rendered, color, radii, geom, binning, img = fwd
+    empty = torch.empty(0)
+    shs = d["shs"] if colors is None else empty
+    scales, rots = (d["scales"], d["rotations"]) if cov3D is None else (empty, empty)
+    return _C.rasterize_gaussians_backward(d["bg"], d["means3D"], radii, empty if colors is None else colors, scales,
+                                           rots, scale_modifier, empty if cov3D is None else cov3D, d["viewmatrix"],
+                                           d["projmatrix"], d["tanfovx"], d["tanfovy"], dpix, shs, d["sh_degree"],
+                                           d["campos"], geom, num_rendered, binning, img, False)
+
+
+def oracle_fwd_bwd(oracle_mod, d, dpix=None, *, colors=None, cov3D=None, scale_modifier=1.0):
+    kw = oracle_kwargs(d)
+    means = d["means3D"].cpu().numpy()
+    common = dict(viewmatrix=kw["viewmatrix"], projmatrix=kw["projmatrix"], campos=kw["campos"], W=d["W"], H=d["H"],
+                  tanfovx=kw["tanfovx"], tanfovy=kw["tanfovy"], sh_degree=d["sh_degree"], bg=kw["bg"],
+                  scale_modifier=scale_modifier)
+    mode = dict(shs=None if colors is not None else kw["shs"],
+                colors_precomp=None if colors is None else colors.cpu().numpy(),
+                scales=None if cov3D is not None else kw["scales"],
+                rotations=None if cov3D is not None else kw["rotations"],
+                cov3D_precomp=None if cov3D is None else cov3D.cpu().numpy())
+    fwd = oracle_mod.forward(means, kw["opacities"], **mode, **common)
+    bwd = None
+    if dpix is not None:
+        bwd = oracle_mod.backward(fwd, dpix.cpu().numpy(), means, **mode, **common)
+    return fwd, bwd
+
+
+def check_forward(oracle_mod, d, **mode):
+    from gsd_amd.introspect import decode
+    o, _ = oracle_fwd_bwd(oracle_mod, d, **mode)
+    fwd = gpu_forward(d, **mode)
+    K, color, radii, geom, binning, img = fwd
+    torch.cuda.synchronize()
+    st = {k: v.cpu().numpy() for k, v in decode(d["means3D"].shape[0], d["W"], d["H"], K, geom, binning, img).items()}
+    radii = radii.cpu().numpy()
+    vis = o["radii"] > 0
+    np.testing.assert_array_equal(radii, o["radii"])
+    assert K == o["num_rendered"]
+    np.testing.assert_array_equal(st["depths"][vis].view(np.uint32), o["depths"][vis].view(np.uint32))
+    np.testing.assert_array_equal(st["means2D"][vis].view(np.uint32), o["means2D"][vis].view(np.uint32))
+    np.testing.assert_array_equal(st["conic_opacity"][vis].view(np.uint32), o["conic_opacity"][vis].view(np.uint32))
+    if mode.get("colors") is None:
+        np.testing.assert_array_equal(st["rgb"][vis].view(np.uint32), o["rgb"][vis].view(np.uint32))
+        cl = np.stack([(st["clamped"] >> c) & 1 for c in range(3)], 1).astype(bool)
+        np.testing.assert_array_equal(cl[vis], o["clamped"][vis].astype(bool))
+    np.testing.assert_array_equal(st["ranges"].astype(np.uint32), o["ranges"])
+    np.testing.assert_array_equal(st["point_list"].astype(np.uint32), o["point_list"])
+    # the reference's sort keys, rebuilt from (tile of the range, depth bits of the id): identical
+    c = color.cpu().numpy()
+    assert np.abs(c - o["color"]).max() <= 1e-5, np.abs(c - o["color"]).max()
+    nc_mismatch = np.mean(st["n_contrib"].astype(np.uint32) != o["n_contrib"])
+    assert nc_mismatch <= 1e-3, nc_mismatch
+    assert np.abs(st["final_T"] - o["final_T"]).max() <= 1e-5
+    return o, fwd
+
+
+CASES = [  # (P, W, H, deg, seed): config-1 shape, odd sizes, every SH degree
+    (10_000, 400, 400, 0, 1),
+    (3_000, 333, 217, 1, 2),
+    (4_000, 256, 256, 2, 3),
+    (6_000, 640, 360, 3, 4),
+]
+
+
+@pytest.mark.parametrize("P,W,H,deg,seed", CASES)
+def test_forward_bit_exact(oracle_mod, P, W, H, deg, seed):
+    d = scene_inputs(P, W, H, deg, seed=seed, device=DEV)
+    check_forward(oracle_mod, d)
+
+
+@pytest.mark.parametrize("P,W,H,deg,seed", CASES)
+def test_backward_matches_oracle(oracle_mod, P, W, H, deg, seed):
+    d = scene_inputs(P, W, H, deg, seed=seed, device=DEV)
+    g = torch.Generator().manual_seed(seed)
+    dpix = torch.randn(3, H, W, generator=g).mul_(1e-3).to(DEV)
+    o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    fwd = gpu_forward(d)
+    grads = gpu_backward(d, fwd, dpix)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for name, gt in zip(names, grads):
+        got = gt.cpu().numpy().reshape(ob[name].shape)
+        assert np.isfinite(got).all(), name
+        assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+
+
+def test_precomputed_colors_and_cov3d(oracle_mod):
+    from gsd_amd.renderer import build_covariance_from_scaling_rotation
+    d = scene_inputs(5_000, 320, 240, 3, seed=7, device=DEV)
+    cov = build_covariance_from_scaling_rotation(d["scales"], 1.0, d["rotations"]).contiguous()
+    colors = torch.rand(5_000, 3, generator=torch.Generator().manual_seed(3)).to(DEV)
+    check_forward(oracle_mod, d, colors=colors, cov3D=cov)
+    dpix = torch.randn(3, 240, 320, generator=torch.Generator().manual_seed(5)).mul_(1e-3).to(DEV)
+    _, ob = oracle_fwd_bwd(oracle_mod, d, dpix, colors=colors, cov3D=cov)
+    grads = gpu_backward(d, gpu_forward(d, colors=colors, cov3D=cov), dpix, colors=colors, cov3D=cov)
+    for name, gt in zip(["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D"], grads[:5]):
+        assert rel_l2(gt.cpu().numpy().reshape(ob[name].shape), ob[name]) <= 1e-4, name
+
+
+def test_background_and_scale_modifier(oracle_mod):
+    d = scene_inputs(4_000, 200, 150, 2, seed=11, device=DEV)
+    d["bg"] = torch.tensor([0.2, 0.5, 0.9], device=DEV)
+    check_forward(oracle_mod, d, scale_modifier=0.7)
+    dpix = torch.randn(3, 150, 200, generator=torch.Generator().manual_seed(2)).mul_(1e-3).to(DEV)
+    _, ob = oracle_fwd_bwd(oracle_mod, d, dpix, scale_modifier=0.7)
+    grads = gpu_backward(d, gpu_forward(d, scale_modifier=0.7), dpix, scale_modifier=0.7)
+    for name, gt in zip(["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D"], grads[:4]):
+        assert rel_l2(gt.cpu().numpy().reshape(ob[name].shape), ob[name]) <= 1e-4, name
+
+
+def test_dense_tile_merge_path(oracle_mod):
+    """A tile holding > 4096 instances takes the chunk-sort + merge-path branch."""
+    d = scene_inputs(12_000, 128, 128, 0, seed=5, device=DEV)
+    g = torch.Generator().manual_seed(9)
+    z = torch.rand(12_000, generator=g) * 4 + 3
+    xy = (torch.rand(12_000, 2, generator=g) - 0.5) * 0.02 * z[:, None]
+    d["means3D"] = torch.cat([xy, z[:, None]], 1).to(DEV)
+    d["scales"] = torch.full((12_000, 3), 0.002).to(DEV)
+    o, _ = check_forward(oracle_mod, d)
+    counts = o["ranges"][:, 1].astype(np.int64) - o["ranges"][:, 0]
+    assert counts.max() > 4096
+
+
+def test_empty_and_culled():
+    d = scene_inputs(100, 64, 64, 0, seed=1, device=DEV)
+    d["means3D"] = d["means3D"] * torch.tensor([1.0, 1.0, -1.0], device=DEV)   # all behind the camera
+    K, color, radii, *_ = gpu_forward(d)
+    assert K == 0 and int(radii.abs().sum()) == 0
+    assert torch.equal(color, torch.zeros_like(color))
+    d0 = scene_inputs(1, 64, 64, 0, seed=1, device=DEV)
+    d0 = {k: (v[:0] if k in ("means3D", "scales", "rotations", "opacities", "shs") else v) for k, v in d0.items()}
+    K0, c0, r0, *_ = gpu_forward(d0)
+    assert K0 == 0 and r0.numel() == 0 and c0.shape == (3, 64, 64)
+
+
+def test_prefiltered_raises():
+    from gsd_amd._native import NativeError
+    d = scene_inputs(100, 64, 64, 0, seed=1, device=DEV)
+    d["means3D"][0, 2] = -1.0
+    with pytest.raises(NativeError, match="prefiltered"):
+        gpu_forward(d, prefiltered=True)
+
+
+def test_mark_visible(oracle_mod):
+    from gsd_amd import _C
+    d = scene_inputs(5_000, 64, 64, 0, seed=2, device=DEV)
+    d["means3D"][::3, 2] *= -1
+    got = _C.mark_visible(d["means3D"], d["viewmatrix"], d["projmatrix"]).cpu().numpy()
+    want = oracle_mod.mark_visible(d["means3D"].cpu().numpy(), d["viewmatrix"].cpu().numpy(),
+                                   d["projmatrix"].cpu().numpy())
+    np.testing.assert_array_equal(got, want)
+
+
+def test_se3_deform_matches_float64_autograd():
+    from gsd_amd.deform import se3_deform
+    from oracle import se3_ref
+    g = torch.Generator().manual_seed(0)
+    P = 4096
+    tw = torch.cat([torch.randn(P, 3, generator=g) * 0.5, torch.randn(P, 3, generator=g) * 0.2], 1)
+    tw[:8, :3] *= torch.tensor([0.0, 1e-9, 1e-7, 1e-5, 1e-3, 1e-2, 0.1, 3.0])[:, None]   # across the series switch
+    x = torch.randn(P, 3, generator=g) * 3
+    q = torch.nn.functional.normalize(torch.randn(P, 4, generator=g), dim=1)
+    gm, gq = torch.randn(P, 3, generator=g), torch.randn(P, 4, generator=g)
+    tw64, x64, q64 = (t.double().requires_grad_(True) for t in (tw, x, q))
+    m_ref, q_ref = se3_ref.deform(tw64, x64, q64)
+    ((m_ref * gm.double()).sum() + (q_ref * gq.double()).sum()).backward()
+    twd, xd, qd = (t.to(DEV).requires_grad_(True) for t in (tw, x, q))
+    m, qo = se3_deform(twd, xd, qd)
+    ((m * gm.to(DEV)).sum() + (qo * gq.to(DEV)).sum()).backward()
+    assert rel_l2(m.detach().cpu(), m_ref.detach()) <= 1e-6
+    assert rel_l2(qo.detach().cpu(), q_ref.detach()) <= 1e-6
+    for got, want in [(twd.grad, tw64.grad), (xd.grad, x64.grad), (qd.grad, q64.grad)]:
+        assert rel_l2(got.cpu(), want) <= 1e-5
+    # zero twist is exactly the identity on the means
+    z, _ = se3_deform(torch.zeros(4, 6, device=DEV), xd[:4].detach())
+    assert torch.equal(z, xd[:4].detach())
+
+
+def test_render_end_to_end_autograd():
+    """render() drop-in: additive and SE(3) modes, gradients reach every parameter."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.scene import make_gaussians
+    for mode, se3 in (("additive", None), ("se3", "random")):
+        params = make_gaussians(20_000, 320, 240, seed=3, se3=se3, device=DEV)
+        pc = DeformableGaussians(params, sh_degree=3, deform=mode)
+        cam = synthetic_camera(320, 240).to(DEV)
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+        assert out["render"].shape == (3, 240, 320)
+        loss = (out["render"] - 0.5).abs().mean()
+        loss.backward()
+        for p in pc.parameters():
+            assert p.grad is not None and torch.isfinite(p.grad).all()
+        assert out["viewspace_points"].grad is not None
+        assert int(out["visibility_filter"].sum()) > 0
+
+
+def test_config4_invariants():
+    """Full-size (1M Gaussians, 1080p, SH3) size-independent properties."""
+    from gsd_amd.introspect import decode
+    d = scene_inputs(1_000_000, 1920, 1080, 3, seed=4, device=DEV)
+    K, color, radii, geom, binning, img = gpu_forward(d)
+    st = decode(1_000_000, 1920, 1080, K, geom, binning, img)
+    ranges = st["ranges"].cpu().numpy().astype(np.int64)
+    counts = st["tile_count"].cpu().numpy().astype(np.int64)
+    nz = counts > 0
+    assert counts.sum() == K
+    np.testing.assert_array_equal(ranges[nz, 1] - ranges[nz, 0], counts[nz])
+    starts = ranges[nz, 0]
+    assert starts[0] == 0 and np.all(starts[1:] == (ranges[nz, 1])[:-1])   # ranges partition [0, K)
+    pl = st["point_list"].cpu().numpy().astype(np.int64)
+    depth_bits = st["depths"].cpu().numpy().view(np.uint32).astype(np.int64)
+    key = (depth_bits[pl] << 32) | pl
+    tile_of = np.repeat(np.nonzero(nz)[0], counts[nz])
+    order_ok = (tile_of[1:] > tile_of[:-1]) | (key[1:] > key[:-1])
+    assert order_ok.all()                                  # (tile, depth, id) strictly increasing
+    r = radii.cpu().numpy()
+    assert set(np.unique(pl)) == set(np.nonzero(r > 0)[0])  # every visible Gaussian is binned
+    T = st["final_T"].cpu().numpy()
+    assert T.min() >= 1e-4 and T.max() <= 1.0
+    nc = st["n_contrib"].cpu().numpy().astype(np.int64)
+    W = 1920
+    tiles = (np.arange(1080)[:, None] // 16) * ((W + 15) // 16) + (np.arange(W)[None] // 16)
+    assert np.all(nc <= counts[tiles])
+    assert torch.isfinite(color).all()
