@@ -1,0 +1,220 @@
+#!/usr/bin/env python
+"""Training-throughput bench (BASELINE.json metric): views/s and fwd+bwd ms/view,
+1M Gaussians @ 1920x1080, SH degree 3, one view per GPU.
+
+A step = on every rank (one process per GPU): render() of that rank's view
+(activation preamble + HIP rasterizer forward), L1 loss against a synthetic
+target, backward (HIP rasterizer backward + autograd through the
+activations), ONE RCCL all-reduce of the flat per-Gaussian gradient slab, and
+the reference's Adam step (scene/gaussian_model.py:834-864 param groups,
+eps 1e-15).  Inputs live in HBM before the timed region.  ``value`` = views
+processed by all ranks / max-over-ranks wall time.
+
+Also reported (rank 0): per-kernel device times (hipEvents inside the C-ABI
+over the timed region), the roofline of the dominant kernel, and the CPU
+baseline -- the single-threaded C oracle on one full view of the same workload.
+
+  python bench.py [--gpus N --steps K --warmup W --config 4 --cpu-baseline auto|off]
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "gaussian-splatting_deformable_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training views/sec + fwd+bwd ms/view, 1M Gaussians @1080p SH3, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(P, V, K, W, H, C):
+    """Per-launch algorithmic HBM bytes of each kernel (DESIGN.md 'Roofline');
+    P Gaussians, V visible, K instances, C = (D+1)^2 SH coefficients."""
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    npix = W * H
+    return {
+        "preprocess_fwd": 44 * P + 12 * C * V + 4 * P + 45 * V,
+        "tile_scan": 16 * T,
+        "scatter_keys": 4 * P + 12 * V + 8 * K,
+        "tile_sort": 8 * T + 8 * K + 4 * K,
+        "render_fwd": 8 * T + 44 * K + 20 * npix,
+        "render_bwd": 8 * T + 44 * K + 20 * npix + 44 * V,
+        "preprocess_bwd": 4 * P + (85 + 12 * C) * V + (64 + 12 * C) * V,
+    }
+
+
+def make_optimizer(pc):
+    """training_setup (scene/gaussian_model.py:834-864) param groups; spatial_lr_scale = 1."""
+    groups = [
+        {"params": [pc._xyz], "lr": 0.00016, "name": "xyz"},
+        {"params": [pc._features_dc], "lr": 0.0025, "name": "f_dc"},
+        {"params": [pc._features_rest], "lr": 0.0025 / 20.0, "name": "f_rest"},
+        {"params": [pc._opacity], "lr": 0.05, "name": "opacity"},
+        {"params": [pc._scaling], "lr": 0.005, "name": "scaling"},
+        {"params": [pc._rotation], "lr": 0.001, "name": "rotation"},
+    ]
+    try:
+        return torch.optim.Adam(groups, lr=0.0, eps=1e-15, fused=True)
+    except (RuntimeError, TypeError):
+        return torch.optim.Adam(groups, lr=0.0, eps=1e-15, foreach=True)
+
+
+def cpu_baseline(cfg, seed):
+    """Single-threaded C oracle (oracle/raster_oracle.c), one full view fwd+bwd of the same workload."""
+    import numpy as np
+
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.scene import make_gaussians
+    from oracle import oracle
+
+    P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
+    g = make_gaussians(P, W, H, seed=seed)
+    cam = synthetic_camera(W, H)
+    kw = dict(shs=torch.cat([g.features_dc, g.features_rest], 1).numpy(), scales=torch.exp(g.scaling).numpy(),
+              rotations=torch.nn.functional.normalize(g.rotation, dim=1).numpy(),
+              viewmatrix=cam.world_view_transform.numpy(), projmatrix=cam.full_proj_transform.numpy(),
+              campos=cam.camera_center.numpy(), W=W, H=H, tanfovx=math.tan(cam.FoVx / 2),
+              tanfovy=math.tan(cam.FoVy / 2), sh_degree=D)
+    opac = torch.sigmoid(g.opacity).numpy()
+    dpix = np.random.default_rng(0).standard_normal((3, H, W)).astype(np.float32) * 1e-3
+    oracle.build()
+    t0 = time.perf_counter()
+    fwd = oracle.forward(g.xyz.numpy(), opac, **kw)
+    oracle.backward(fwd, dpix, g.xyz.numpy(), **kw)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "views/s", "cores": 1, "kind": "port",
+            "sample": f"1 full view of the bench workload (P={P}, {W}x{H}, SH{D}) forward+backward with the "
+                      f"single-threaded C oracle: {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=4)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    args = ap.parse_args()
+
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd import _C as gsdC
+    from gsd_amd._native import kernel_times
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.parallel import FlatGrads, init_from_env
+    from gsd_amd.scene import CONFIGS, make_gaussians
+
+    rank, local, world = init_from_env()
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    cfg = CONFIGS[args.config]
+    P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
+
+    params = make_gaussians(P, W, H, seed=args.config).to(dev)   # replicated on every rank
+    pc = DeformableGaussians(params, sh_degree=D)
+    cam = synthetic_camera(W, H, yaw_deg=2.0 * rank).to(dev)     # one view per GPU, yaw offsets k*2 deg
+    target = torch.rand(3, H, W, generator=torch.Generator().manual_seed(100 + rank)).to(dev)
+    bg = torch.zeros(3, device=dev)
+    pipe = default_pipe()
+    opt = make_optimizer(pc)
+    flat = FlatGrads(pc.parameters())
+
+    def step():
+        out = render(cam, pc, pipe, bg)
+        loss = (out["render"] - target).abs().mean()     # utils/loss_utils.py:17-18
+        loss.backward()
+        flat.allreduce()
+        opt.step()
+        flat.zero()
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kernel_times(enable=True, reset=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = kernel_times(enable=False, reset=True)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # fwd+bwd ms/view: render + backward only (no optimizer / collective), hipEvents, median
+    times = []
+    for _ in range(max(5, min(20, args.steps))):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        o = render(cam, pc, pipe, bg)
+        (o["render"] - target).abs().mean().backward()
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+        flat.zero()
+    times.sort()
+    fwd_bwd_ms = times[len(times) // 2]
+
+    if rank == 0:
+        V = int((out["radii"] > 0).sum())
+        K = int(gsdC.last_forward.get("num_rendered", 0))
+        steps = args.steps
+        per_kernel = {k: tot / max(n, 1) for k, (tot, n) in kt.items()}
+        dom = max(kt, key=lambda k: kt[k][0]) if kt else None
+        roof = None
+        if dom:
+            nbytes = algorithmic_bytes(P, V, K, W, H, (min(D, 3) + 1) ** 2).get(dom)
+            if nbytes:
+                ach = nbytes / (per_kernel[dom] * 1e-3) / 1e9
+                roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(per_kernel[dom], 4)}
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            cpu = cpu_baseline(cfg, args.config)
+        res = {
+            "metric": METRIC,
+            "value": round(world * steps / elapsed, 3),
+            "unit": "views/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"cfg{args.config}: {P} Gaussians, SH deg {D}, {W}x{H}, 1 view/GPU; render fwd + "
+                                   "L1 + bwd + RCCL all-reduce of per-Gaussian grads + Adam",
+                       "P": P, "width": W, "height": H, "sh_degree": D, "views_per_step": world,
+                       "parallelism": f"dp{world}", "visible": V, "num_rendered": K},
+            "fwd_bwd_ms_per_view": round(fwd_bwd_ms, 4),
+            "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -9,7 +9,9 @@
 
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gsd_raster.h"
 #include "gsd_kernels.h"
@@ -148,6 +150,51 @@ int validate(const gsd_raster_args* a, bool forward) {
 
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---- optional per-kernel device timing (gsd_timing_*) ----
+enum KernelId { kPreFwd, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd, kSe3Bwd,
+                kMarkVis, kNumKernels };
+const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_scan",  "scatter_keys", "tile_sort",
+                                               "render_fwd",     "render_bwd", "preprocess_bwd", "se3_fwd",
+                                               "se3_bwd",        "mark_visible"};
+struct TimingState {
+    bool on = false;
+    struct Rec {
+        int id;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    double total_ms[kNumKernels] = {};
+    int64_t launches[kNumKernels] = {};
+    std::mutex mu;
+};
+TimingState g_timing;
+
+hipEvent_t pooled_event() {
+    if (!g_timing.pool.empty()) {
+        hipEvent_t e = g_timing.pool.back();
+        g_timing.pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+template <class F>
+void timed(int id, hipStream_t s, F&& launch) {
+    if (!g_timing.on) {
+        launch();
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    TimingState::Rec r{id, pooled_event(), pooled_event()};
+    (void)hipEventRecord(r.a, s);
+    launch();
+    (void)hipEventRecord(r.b, s);
+    g_timing.pending.push_back(r);
+}
+
 }  // namespace
 
 extern "C" {
@@ -215,9 +262,9 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     p.radii = radii ? radii : g.radii;
     p.means2D = g.means2D; p.depths = g.depths; p.conic_opacity = g.conic_opacity; p.rgb = g.rgb;
     p.clamped = g.clamped; p.tile_count = im.tile_count; p.err_flags = im.counters + 1;
-    gsd::launch_preprocess_fwd(p, s);
+    timed(kPreFwd, s, [&] { gsd::launch_preprocess_fwd(p, s); });
     GSD_CHECK(a->debug, s);
-    gsd::launch_tile_scan(T, im.tile_count, im.ranges, im.tile_cursor, im.counters, s);
+    timed(kTileScan, s, [&] { gsd::launch_tile_scan(T, im.tile_count, im.ranges, im.tile_cursor, im.counters, s); });
     GSD_CHECK(a->debug, s);
     if (!g_pinned) GSD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_pinned), 16, hipHostMallocDefault));
     GSD_HIP(hipMemcpyAsync(g_pinned, im.counters, 8, hipMemcpyDeviceToHost, s));
@@ -249,9 +296,9 @@ int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, vo
         bp.P = a->P; bp.grid_x = gx; bp.grid_y = gy; bp.num_tiles = T;
         bp.radii = radii ? radii : g.radii;
         bp.means2D = g.means2D; bp.depths = g.depths; bp.tile_cursor = im.tile_cursor; bp.bucket_keys = b.keys;
-        gsd::launch_scatter_keys(bp, s);
+        timed(kScatter, s, [&] { gsd::launch_scatter_keys(bp, s); });
         GSD_CHECK(a->debug, s);
-        gsd::launch_tile_sort(T, im.ranges, b.keys, b.scratch, b.point_list, s);
+        timed(kTileSort, s, [&] { gsd::launch_tile_sort(T, im.ranges, b.keys, b.scratch, b.point_list, s); });
         GSD_CHECK(a->debug, s);
     }
     gsd::RenderParams rp{};
@@ -259,7 +306,7 @@ int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, vo
     rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
     rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
     rp.out_color = out_color;
-    gsd::launch_render_fwd(rp, s);
+    timed(kRenderFwd, s, [&] { gsd::launch_render_fwd(rp, s); });
     GSD_CHECK(a->debug, s);
     return GSD_OK;
 }
@@ -294,7 +341,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     rp.dL_dpix = dL_dout_color; rp.dL_dmean2D = dL_dmeans2D; rp.dL_dconic = dL_dconic;
     rp.dL_dopacity = dL_dopacity; rp.dL_dcolors = dL_dcolors;
     if (K > 0) {
-        gsd::launch_render_bwd(rp, s);
+        timed(kRenderBwd, s, [&] { gsd::launch_render_bwd(rp, s); });
         GSD_CHECK(a->debug, s);
     }
     gsd::PreprocessBwdParams p{};
@@ -308,7 +355,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     p.dL_dmean2D = dL_dmeans2D; p.dL_dconic = dL_dconic; p.dL_dcolor = dL_dcolors;
     p.dL_dmeans3D = dL_dmeans3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = dL_dsh; p.dL_dscales = dL_dscales;
     p.dL_drotations = dL_drotations;
-    gsd::launch_preprocess_bwd(p, s);
+    timed(kPreBwd, s, [&] { gsd::launch_preprocess_bwd(p, s); });
     GSD_CHECK(a->debug, s);
     return GSD_OK;
 }
@@ -319,7 +366,7 @@ int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, c
     if (P < 0) return fail(GSD_ERR_ARG, "means3D must have dimensions (num_points, 3)");
     if (P == 0) return GSD_OK;
     if (!means3D || !viewmatrix || !present) return fail(GSD_ERR_ARG, "null pointer argument");
-    gsd::launch_mark_visible(P, means3D, viewmatrix, present, as_stream(stream));
+    timed(kMarkVis, as_stream(stream), [&] { gsd::launch_mark_visible(P, means3D, viewmatrix, present, as_stream(stream)); });
     GSD_CHECK(false, as_stream(stream));
     return GSD_OK;
 }
@@ -329,7 +376,7 @@ int gsd_se3_deform_forward(int32_t P, const float* twist, const float* means_in,
     if (P < 0) return fail(GSD_ERR_ARG, "twist must have dimensions (num_points, 6)");
     if (P == 0) return GSD_OK;
     if (!twist || !means_in || !means_out || (rot_in && !rot_out)) return fail(GSD_ERR_ARG, "null pointer argument");
-    gsd::launch_se3_fwd(P, twist, means_in, rot_in, means_out, rot_out, as_stream(stream));
+    timed(kSe3Fwd, as_stream(stream), [&] { gsd::launch_se3_fwd(P, twist, means_in, rot_in, means_out, rot_out, as_stream(stream)); });
     GSD_CHECK(false, as_stream(stream));
     return GSD_OK;
 }
@@ -342,10 +389,52 @@ int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in
     if (!twist || !means_in || !dL_dmeans_out || !dL_dtwist || !dL_dmeans_in ||
         (rot_in && (!dL_drot_out || !dL_drot_in)))
         return fail(GSD_ERR_ARG, "null pointer argument");
-    gsd::launch_se3_bwd(P, twist, means_in, rot_in, dL_dmeans_out, dL_drot_out, dL_dtwist, dL_dmeans_in, dL_drot_in,
-                        as_stream(stream));
+    timed(kSe3Bwd, as_stream(stream), [&] {
+        gsd::launch_se3_bwd(P, twist, means_in, rot_in, dL_dmeans_out, dL_drot_out, dL_dtwist, dL_dmeans_in,
+                            dL_drot_in, as_stream(stream));
+    });
     GSD_CHECK(false, as_stream(stream));
     return GSD_OK;
+}
+
+int gsd_timing_enable(int32_t on) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    g_timing.on = on != 0;
+    return GSD_OK;
+}
+
+int gsd_timing_collect(int32_t max_kernels, char* names, double* total_ms, int64_t* launches) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    for (const auto& r : g_timing.pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_timing.total_ms[r.id] += ms;
+            g_timing.launches[r.id] += 1;
+        }
+        g_timing.pool.push_back(r.a);
+        g_timing.pool.push_back(r.b);
+    }
+    g_timing.pending.clear();
+    int n = 0;
+    for (int k = 0; k < kNumKernels && n < max_kernels; ++k) {
+        if (!g_timing.launches[k]) continue;
+        if (names) {
+            std::strncpy(names + 32 * n, kKernelNames[k], 31);
+            names[32 * n + 31] = 0;
+        }
+        if (total_ms) total_ms[n] = g_timing.total_ms[k];
+        if (launches) launches[n] = g_timing.launches[k];
+        ++n;
+    }
+    return n;
+}
+
+void gsd_timing_reset(void) {
+    std::lock_guard<std::mutex> lk(g_timing.mu);
+    for (int k = 0; k < kNumKernels; ++k) {
+        g_timing.total_ms[k] = 0;
+        g_timing.launches[k] = 0;
+    }
 }
 
 }  // extern "C"

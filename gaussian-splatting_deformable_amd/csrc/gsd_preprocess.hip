@@ -42,16 +42,15 @@ __device__ __forceinline__ void load_sh(const float* __restrict__ row, float (&s
     for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
 }
 
-__device__ __forceinline__ float3 sh_to_rgb(int deg, const float* __restrict__ row, float3 pos, float3 cam,
+template <int DEG>
+__device__ __forceinline__ float3 sh_to_rgb(const float* __restrict__ row, float3 pos, float3 cam,
                                             uint8_t& clamp_bits) {
+    constexpr int deg = DEG;
     float3 d = make_float3(pos.x - cam.x, pos.y - cam.y, pos.z - cam.z);
     const float len = sqrtf(dot3(d, d));
     d = make_float3(d.x / len, d.y / len, d.z / len);
     float s[48];
-    if (deg >= 3) load_sh<16>(row, s);
-    else if (deg == 2) load_sh<9>(row, s);
-    else if (deg == 1) load_sh<4>(row, s);
-    else load_sh<1>(row, s);
+    load_sh<(DEG + 1) * (DEG + 1)>(row, s);
     float3 rgb;
     rgb.x = sh_channel(deg, s + 0, d.x, d.y, d.z);
     rgb.y = sh_channel(deg, s + 1, d.x, d.y, d.z);
@@ -85,6 +84,7 @@ __device__ __forceinline__ float3 cov2d_fwd(const float3 mean, float fx, float f
 // Forward preprocess: forward.cu:155-256 (+ the per-tile instance count of
 // the binning stage, folded in so the rect is computed once).
 // ---------------------------------------------------------------------------
+template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= p.P) return;
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
         col = make_float4(p.colors_precomp[3 * idx], p.colors_precomp[3 * idx + 1], p.colors_precomp[3 * idx + 2], 0.f);
     } else {
         const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-        const float3 rgb = sh_to_rgb(p.D, p.shs + (size_t)idx * p.M * 3, mean, cam, cl);
+        const float3 rgb = sh_to_rgb<DEG>(p.shs + (size_t)idx * p.M * 3, mean, cam, cl);
         col = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
     }
     p.clamped[idx] = cl;
@@ -307,6 +307,7 @@ __device__ __forceinline__ void cov3d_bwd(const float3 scale, float mod, const f
     drot.w = 2 * r * (D01 - D10) + 2 * x * (D20 + D02) + 2 * y * (D12 + D21) - 4 * z * (D11 + D00);
 }
 
+template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= p.P || !(p.radii[idx] > 0)) return;
@@ -358,13 +359,15 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
                                       p.dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0 : 1));
         const float* row = p.shs + (size_t)idx * p.M * 3;
         float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
+        constexpr int nc = (DEG + 1) * (DEG + 1);
         float s[48];
-        const int nc = p.D >= 3 ? 16 : (p.D + 1) * (p.D + 1);
+#pragma unroll
         for (int k = 0; k < nc * 3; ++k) s[k] = row[k];
         float ds[48];
-        const float3 gx = sh_channel_bwd(p.D, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
-        const float3 gy = sh_channel_bwd(p.D, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
-        const float3 gz = sh_channel_bwd(p.D, s + 2, dc.z, dir.x, dir.y, dir.z, ds + 2);
+        const float3 gx = sh_channel_bwd(DEG, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
+        const float3 gy = sh_channel_bwd(DEG, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
+        const float3 gz = sh_channel_bwd(DEG, s + 2, dc.z, dir.x, dir.y, dir.z, ds + 2);
+#pragma unroll
         for (int k = 0; k < nc * 3; ++k) drow[k] = ds[k];
         // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
         const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
@@ -391,10 +394,24 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
 
 namespace gsd {
 void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
-    if (p.P > 0) hipLaunchKernelGGL(k_preprocess_fwd, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    if (p.P <= 0) return;
+    const dim3 g((p.P + 255) / 256), b(256);
+    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {  // degrees > 3 evaluate as 3, like forward.cu:32-60
+        case 0: hipLaunchKernelGGL(k_preprocess_fwd<0>, g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL(k_preprocess_fwd<1>, g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL(k_preprocess_fwd<2>, g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL(k_preprocess_fwd<3>, g, b, 0, s, p); break;
+    }
 }
 void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s) {
-    if (p.P > 0) hipLaunchKernelGGL(k_preprocess_bwd, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    if (p.P <= 0) return;
+    const dim3 g((p.P + 255) / 256), b(256);
+    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+        case 0: hipLaunchKernelGGL(k_preprocess_bwd<0>, g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL(k_preprocess_bwd<1>, g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL(k_preprocess_bwd<2>, g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL(k_preprocess_bwd<3>, g, b, 0, s, p); break;
+    }
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s) {
     if (P > 0) hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);

@@ -17,6 +17,9 @@ from . import _native
 
 _i64 = ctypes.c_int64
 
+# host-side record of the most recent forward on this process (bench / diagnostics)
+last_forward: dict = {}
+
 
 def _stream(dev: torch.device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -98,6 +101,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         _native.check(lib.gsd_rasterize_forward_bin(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(radii),
                                                     ctypes.byref(K), stream))
         num_rendered = int(K.value)
+        last_forward.update(P=P, W=W, H=H, num_rendered=num_rendered)
         binning = torch.empty(lib.gsd_binning_buffer_bytes(num_rendered), **byte)
         color = torch.empty(3, H, W, dtype=torch.float32, device=dev)
         _native.check(lib.gsd_rasterize_forward_render(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(binning),

@@ -49,7 +49,30 @@ SIGNATURES = {
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),
     "gsd_se3_deform_forward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_se3_deform_backward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_timing_enable": (_i32, [_i32]),
+    "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
+    "gsd_timing_reset": (None, []),
 }
+
+
+def kernel_times(enable: bool | None = None, reset: bool = False) -> dict:
+    """Per-kernel device time of this library's launches: {name: (total_ms, launches)}.
+    Synchronises on the last timed launch.  enable=True/False switches recording."""
+    lib = load()
+    out = {}
+    n_max = 16
+    names = ctypes.create_string_buffer(32 * n_max)
+    tot = (ctypes.c_double * n_max)()
+    cnt = (_i64 * n_max)()
+    n = lib.gsd_timing_collect(n_max, names, tot, cnt)
+    for i in range(n):
+        nm = names.raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
+        out[nm] = (tot[i], int(cnt[i]))
+    if reset:
+        lib.gsd_timing_reset()
+    if enable is not None:
+        lib.gsd_timing_enable(1 if enable else 0)
+    return out
 
 _lib = None
 

@@ -139,6 +139,17 @@ int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in
                             const float* dL_dmeans_out, const float* dL_drot_out, float* dL_dtwist,
                             float* dL_dmeans_in, float* dL_drot_in, void* stream);
 
+/* Per-kernel device timing.  While enabled, every kernel this library
+ * launches is bracketed by hipEvents on its own stream (a few us of overhead
+ * per launch); gsd_timing_collect() synchronises on the last recorded event
+ * and writes, for up to max_kernels kernels, the name (NUL-terminated, 32 B
+ * per slot), the summed device time in ms and the launch count; it returns
+ * the number of kernels written and keeps accumulating.  gsd_timing_reset()
+ * clears the totals. */
+int gsd_timing_enable(int32_t on);
+int gsd_timing_collect(int32_t max_kernels, char* names, double* total_ms, int64_t* launches);
+void gsd_timing_reset(void);
+
 #ifdef __cplusplus
 }
 #endif
