@@ -9,13 +9,17 @@
 //
 // Backward: the reference issues 9 float atomicAdds per (pixel, Gaussian) pair
 // (backward.cu:523,545-554), all 256 lanes on the same address.  Here each
-// wave reduces its 64 lanes' partials with DPP (wave_sum), one lane adds the
-// wave total into an LDS accumulator per record, and after each 256-record
-// batch every record's 9 sums go to HBM as one set of global atomics: at most
-// 9 global atomics per (Gaussian, tile) instance instead of per pixel.
+// wave computes 8 records' partials, reduces them across its 64 lanes with one
+// transposed butterfly per quantity (wave_sum8: permlane32/16 swaps + DPP),
+// 8 lanes add the 8 wave totals into LDS accumulators, and after each
+// 256-record batch every record's 9 sums go to HBM as one set of global
+// atomics: at most 9 global atomics per (Gaussian, tile) instance instead of
+// 9 per (Gaussian, pixel) pair.
 #include "gsd_kernels.h"
 
 namespace gsd {
+
+constexpr int kFwdBatch = 8;  // records whose alphas are evaluated together (ILP across the exps)
 
 __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     __shared__ float2 s_xy[kTilePix];
@@ -47,26 +51,37 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        for (int j = 0; !done && j < n; ++j) {
-            contributor++;
-            const float2 xy = s_xy[j];
-            const float dx = xy.x - pxf, dy = xy.y - pyf;
-            const float4 co = s_co[j];
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, co.w * expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1 - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
+        for (int j0 = 0; j0 < n; j0 += kFwdBatch) {
+            if (!__ballot(!done)) break;  // every pixel of this wave has saturated
+            // branch-free alphas of kFwdBatch records (independent: the exps overlap) ...
+            float a[kFwdBatch];
+#pragma unroll
+            for (int u = 0; u < kFwdBatch; ++u) {
+                const float2 xy = s_xy[j0 + u];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float4 co = s_co[j0 + u];
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                a[u] = power > 0.0f ? 0.0f : fminf(0.99f, co.w * expf(power));  // 0 => skipped below
             }
-            const float4 c = s_rgb[j];
-            C0 += c.x * alpha * T;
-            C1 += c.y * alpha * T;
-            C2 += c.z * alpha * T;
-            T = test_T;
-            last_contributor = contributor;
+            // ... then the sequential front-to-back recurrence (forward.cu:325-362)
+#pragma unroll
+            for (int u = 0; u < kFwdBatch; ++u) {
+                if (done || j0 + u >= n) continue;
+                contributor++;
+                const float alpha = a[u];
+                if (alpha < 1.0f / 255.0f) continue;
+                const float test_T = T * (1 - alpha);
+                if (test_T < 0.0001f) {
+                    done = true;
+                    continue;
+                }
+                const float4 c = s_rgb[j0 + u];
+                C0 += c.x * alpha * T;
+                C1 += c.y * alpha * T;
+                C2 += c.z * alpha * T;
+                T = test_T;
+                last_contributor = contributor;
+            }
         }
     }
     if (inside) {
@@ -79,6 +94,15 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
         p.out_color[2 * plane + pid] = C2 + T * p.bg[2];
     }
 }
+
+// Per-pixel state of the back-to-front replay (backward.cu:441-461).
+struct BwdPixel {
+    float T, T_final, last_alpha;
+    float acc0, acc1, acc2, lc0, lc1, lc2;
+    float dpix0, dpix1, dpix2, bg_dot;
+};
+
+constexpr int kRedBatch = 8;  // records reduced together by wave_sum8
 
 __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
@@ -97,20 +121,21 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     int toDo = (int)(rg.y - rg.x);
     const int pid = p.W * py + px;
     const int plane = p.H * p.W;
-    const float T_final = inside ? p.final_T[pid] : 0.f;
-    float T = T_final;
+    BwdPixel st;
+    st.T_final = inside ? p.final_T[pid] : 0.f;
+    st.T = st.T_final;
     uint32_t contributor = (uint32_t)toDo;
     const uint32_t last_contributor = inside ? p.n_contrib[pid] : 0u;
-    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
+    st.dpix0 = st.dpix1 = st.dpix2 = 0.f;
     if (inside) {
-        dpix0 = p.dL_dpix[pid];
-        dpix1 = p.dL_dpix[plane + pid];
-        dpix2 = p.dL_dpix[2 * plane + pid];
+        st.dpix0 = p.dL_dpix[pid];
+        st.dpix1 = p.dL_dpix[plane + pid];
+        st.dpix2 = p.dL_dpix[2 * plane + pid];
     }
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;      // accum_rec
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;         // last_color
-    float last_alpha = 0.f;
-    const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
+    st.acc0 = st.acc1 = st.acc2 = 0.f;  // accum_rec
+    st.lc0 = st.lc1 = st.lc2 = 0.f;     // last_color
+    st.last_alpha = 0.f;
+    st.bg_dot = p.bg[0] * st.dpix0 + p.bg[1] * st.dpix1 + p.bg[2] * st.dpix2;
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)px, pyf = (float)py;
 
@@ -128,69 +153,77 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        for (int j = 0; j < n; ++j) {
-            float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f, v4 = 0.f, v5 = 0.f, v6 = 0.f, v7 = 0.f, v8 = 0.f;
-            bool has = false;
-            if (inside) {
-                contributor--;
-                if (contributor < last_contributor) {
-                    const float2 xy = s_xy[j];
-                    const float dx = xy.x - pxf, dy = xy.y - pyf;
-                    const float4 co = s_co[j];
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    if (power <= 0.0f) {
-                        const float G = expf(power);
-                        const float alpha = fminf(0.99f, co.w * G);
-                        if (!(alpha < 1.0f / 255.0f)) {
-                            has = true;
-                            T = T / (1.f - alpha);
-                            const float dchannel_dcolor = alpha * T;
-                            const float4 c = s_rgb[j];
-                            // backward.cu:511-524
-                            acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                            acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                            acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                            lc0 = c.x;
-                            lc1 = c.y;
-                            lc2 = c.z;
-                            float dL_dalpha = 0.0f;
-                            dL_dalpha += (c.x - acc0) * dpix0;
-                            dL_dalpha += (c.y - acc1) * dpix1;
-                            dL_dalpha += (c.z - acc2) * dpix2;
-                            v6 = dchannel_dcolor * dpix0;
-                            v7 = dchannel_dcolor * dpix1;
-                            v8 = dchannel_dcolor * dpix2;
-                            dL_dalpha *= T;
-                            last_alpha = alpha;
-                            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                            const float dL_dG = co.w * dL_dalpha;
-                            const float gdx = G * dx, gdy = G * dy;
-                            const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                            const float dG_ddely = -gdy * co.z - gdx * co.y;
-                            v0 = dL_dG * dG_ddelx * ddelx_dx;
-                            v1 = dL_dG * dG_ddely * ddely_dy;
-                            v2 = -0.5f * gdx * dx * dL_dG;
-                            v3 = -0.5f * gdx * dy * dL_dG;
-                            v4 = -0.5f * gdy * dy * dL_dG;
-                            v5 = G * dL_dalpha;
+        for (int j0 = 0; j0 < n; j0 += kRedBatch) {
+            // branch-free G / alpha of kRedBatch records (independent: the exps overlap) ...
+            float Gs[kRedBatch], As[kRedBatch];
+#pragma unroll
+            for (int u = 0; u < kRedBatch; ++u) {
+                const float2 xy = s_xy[j0 + u];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float4 co = s_co[j0 + u];
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                const float G = expf(power);
+                Gs[u] = G;
+                As[u] = power > 0.0f ? 0.0f : fminf(0.99f, co.w * G);  // 0 => skipped below
+            }
+            // ... then the sequential back-to-front recurrence (backward.cu:482-555)
+            float v[9][kRedBatch];
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < kRedBatch; ++u) {
+#pragma unroll
+                for (int q = 0; q < 9; ++q) v[q][u] = 0.f;
+                const int j = j0 + u;
+                if (inside && j < n) {
+                    contributor--;
+                    if (contributor < last_contributor) {
+                        const float2 xy = s_xy[j];
+                        const float dx = xy.x - pxf, dy = xy.y - pyf;
+                        const float4 co = s_co[j];
+                        {
+                            const float G = Gs[u];
+                            const float alpha = As[u];
+                            if (!(alpha < 1.0f / 255.0f)) {
+                                any = true;
+                                const float inv1ma = 1.f / (1.f - alpha);
+                                st.T = st.T * inv1ma;  // backward.cu:503 (T recovered by division)
+                                const float dchannel_dcolor = alpha * st.T;
+                                const float4 c = s_rgb[j];
+                                st.acc0 = st.last_alpha * st.lc0 + (1.f - st.last_alpha) * st.acc0;
+                                st.acc1 = st.last_alpha * st.lc1 + (1.f - st.last_alpha) * st.acc1;
+                                st.acc2 = st.last_alpha * st.lc2 + (1.f - st.last_alpha) * st.acc2;
+                                st.lc0 = c.x;
+                                st.lc1 = c.y;
+                                st.lc2 = c.z;
+                                float dL_dalpha = (c.x - st.acc0) * st.dpix0;
+                                dL_dalpha += (c.y - st.acc1) * st.dpix1;
+                                dL_dalpha += (c.z - st.acc2) * st.dpix2;
+                                v[6][u] = dchannel_dcolor * st.dpix0;
+                                v[7][u] = dchannel_dcolor * st.dpix1;
+                                v[8][u] = dchannel_dcolor * st.dpix2;
+                                dL_dalpha *= st.T;
+                                st.last_alpha = alpha;
+                                dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
+                                const float dL_dG = co.w * dL_dalpha;
+                                const float gdx = G * dx, gdy = G * dy;
+                                const float dG_ddelx = -gdx * co.x - gdy * co.y;
+                                const float dG_ddely = -gdy * co.z - gdx * co.y;
+                                v[0][u] = dL_dG * dG_ddelx * ddelx_dx;
+                                v[1][u] = dL_dG * dG_ddely * ddely_dy;
+                                v[2][u] = -0.5f * gdx * dx * dL_dG;
+                                v[3][u] = -0.5f * gdx * dy * dL_dG;
+                                v[4][u] = -0.5f * gdy * dy * dL_dG;
+                                v[5][u] = G * dL_dalpha;
+                            }
                         }
                     }
                 }
             }
-            if (__ballot(has)) {  // wave-uniform: reduce only when some lane of this wave contributed
-                const float r0 = wave_sum(v0), r1 = wave_sum(v1), r2 = wave_sum(v2), r3 = wave_sum(v3),
-                            r4 = wave_sum(v4), r5 = wave_sum(v5), r6 = wave_sum(v6), r7 = wave_sum(v7),
-                            r8 = wave_sum(v8);
-                if (lane == 0) {
-                    atomicAdd(&s_acc[0][j], r0);
-                    atomicAdd(&s_acc[1][j], r1);
-                    atomicAdd(&s_acc[2][j], r2);
-                    atomicAdd(&s_acc[3][j], r3);
-                    atomicAdd(&s_acc[4][j], r4);
-                    atomicAdd(&s_acc[5][j], r5);
-                    atomicAdd(&s_acc[6][j], r6);
-                    atomicAdd(&s_acc[7][j], r7);
-                    atomicAdd(&s_acc[8][j], r8);
+            if (__ballot(any)) {  // wave-uniform
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    const float r = wave_sum8(v[q]);
+                    if ((lane & 7) == 0) atomicAdd(&s_acc[q][j0 + (lane >> 3)], r);
                 }
             }
         }
