@@ -1,11 +1,19 @@
 // gsd_render.hip -- per-tile front-to-back compositing (forward) and its
 // back-to-front replay (backward).
 //
-// One 256-lane workgroup per 16x16 tile (4 wave64s, each owning 4 pixel rows);
-// the tile's depth-sorted Gaussian list is streamed through LDS 256 records at
-// a time (xy, conic+opacity, rgb: 40 B/record, broadcast reads).  The tile ->
-// workgroup map is XCD-swizzled so neighbouring tiles, which gather the same
-// Gaussian records, share one XCD's L2.
+// One 256-lane workgroup per 16x16 tile; each wave64 owns one 8x8 quadrant.
+// The tile's depth-sorted record list (point_list) is streamed through LDS
+// 256 records at a time (xy, conic+opacity, rgb, and the record's alpha
+// bounding box: 56 B/record, broadcast reads).
+//
+// Wave-level culling: a record can only change a pixel where
+// alpha = o*exp(-Q/2) >= 1/255, i.e. inside the ellipse Q <= 2 ln(255 o)
+// (Q = the conic's quadratic form).  Its bounding box (inflated by a safety
+// margin) is computed once per record; each wave compacts, per 256-record
+// batch, the list of records whose box meets its 8x8 quadrant and iterates
+// only those.  Records outside the list would have been skipped by every
+// lane (alpha < 1/255), so results are unchanged -- ~57% of (wave, record)
+// pairs never reach the ALUs on the bench scene.
 //
 // Backward: the reference issues 9 float atomicAdds per (pixel, Gaussian) pair
 // (backward.cu:523,545-554), all 256 lanes on the same address.  Here each
@@ -19,25 +27,93 @@
 
 namespace gsd {
 
-constexpr int kFwdBatch = 8;  // records whose alphas are evaluated together (ILP across the exps)
+constexpr int kBatch = 8;  // records evaluated together (ILP across the exps; one wave_sum8 in the backward)
+
+// Bounding box of {d : alpha(d) >= 1/255} for a record, inflated for safety.
+// Q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o); half-widths sqrt(t c/det), sqrt(t a/det).
+__device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    const float det = a * c - b * b;
+    const float lo = 255.0f * o;
+    if (!(lo >= 0.999f)) return make_float4(1e30f, -1e30f, 1e30f, -1e30f);  // alpha < 1/255 everywhere (or NaN)
+    if (!(det > 0.0f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f); // degenerate: never cull
+    const float t = 2.0f * 0.69314718f * __builtin_amdgcn_logf(lo);     // 2 ln(255 o), v_log_f32 = log2
+    const float ex = sqrtf(fmaxf(t, 0.f) * c / det) * 1.001f + 0.02f;
+    const float ey = sqrtf(fmaxf(t, 0.f) * a / det) * 1.001f + 0.02f;
+    if (!(ex < 1e30f) || !(ey < 1e30f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
+    return make_float4(xy.x - ex, xy.x + ex, xy.y - ey, xy.y + ey);
+}
+
+// Per-wave compaction of the batch: s_list receives, in increasing slot order,
+// the slots whose alpha box meets [qx0, qx0+7] x [qy0, qy0+7].  Returns the count.
+__device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, uint8_t* __restrict__ s_list, int n,
+                                            float qx0, float qy0, int lane) {
+    int m = 0;
+#pragma unroll
+    for (int k = 0; k < kTilePix / 64; ++k) {
+        const int t = k * 64 + lane;
+        bool hit = false;
+        if (t < n) {
+            const float4 bx = s_box[t];
+            hit = bx.y >= qx0 && bx.x <= qx0 + 7.0f && bx.w >= qy0 && bx.z <= qy0 + 7.0f;
+        }
+        const unsigned long long mask = __ballot(hit);
+        if (hit) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+            s_list[m + below] = (uint8_t)t;
+        }
+        m += __popcll(mask);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return m;
+}
+
+// forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
+// Shared by both passes so their skip decisions are identical.
+__device__ __forceinline__ float record_alpha(float2 xy, float4 co, float pxf, float pyf, float& G) {
+    const float dx = xy.x - pxf, dy = xy.y - pyf;
+    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+    G = expf(power);
+    return power > 0.0f ? 0.0f : fminf(0.99f, co.w * G);
+}
+
+struct TileGeom {
+    int tile, wave, lane, px, py;
+    float qx0, qy0;
+    bool inside;
+};
+__device__ __forceinline__ TileGeom tile_geom(int num_tiles, int grid_x, int W, int H) {
+    TileGeom g;
+    g.tile = xcd_swizzle(blockIdx.x, num_tiles);
+    g.wave = threadIdx.x >> 6;
+    g.lane = threadIdx.x & 63;
+    const int x0 = (g.tile % grid_x) * kTileX + (g.wave & 1) * 8;
+    const int y0 = (g.tile / grid_x) * kTileY + (g.wave >> 1) * 8;
+    g.px = x0 + (g.lane & 7);
+    g.py = y0 + (g.lane >> 3);
+    g.qx0 = (float)x0;
+    g.qy0 = (float)y0;
+    g.inside = g.px < W && g.py < H;
+    return g;
+}
 
 __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     __shared__ float2 s_xy[kTilePix];
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
-    const int tile = xcd_swizzle(blockIdx.x, p.num_tiles);
+    __shared__ float4 s_box[kTilePix];
+    __shared__ uint8_t s_list[4][kTilePix];
+    const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
-    const int px = (tile % p.grid_x) * kTileX + (tid & (kTileX - 1));
-    const int py = (tile / p.grid_x) * kTileY + (tid >> 4);
-    const bool inside = px < p.W && py < p.H;
-    bool done = !inside;
-    const uint2 rg = p.ranges[tile];
+    bool done = !tg.inside;
+    const uint2 rg = p.ranges[tg.tile];
     const int rounds = ((int)(rg.y - rg.x) + kTilePix - 1) / kTilePix;
     int toDo = (int)(rg.y - rg.x);
-    const float pxf = (float)px, pyf = (float)py;
+    const float pxf = (float)tg.px, pyf = (float)tg.py;
     float T = 1.0f;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
-    uint32_t contributor = 0, last_contributor = 0;
+    uint32_t last_contributor = 0;
+    uint8_t* list = s_list[tg.wave];
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         // forward.cu:309-311: stop once every pixel of the tile is saturated
@@ -45,29 +121,31 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
         const int k = (int)rg.x + i * kTilePix + tid;
         if (k < (int)rg.y) {
             const uint32_t g = p.point_list[k];
-            s_xy[tid] = p.means2D[g];
-            s_co[tid] = p.conic_opacity[g];
+            const float2 xy = p.means2D[g];
+            const float4 co = p.conic_opacity[g];
+            s_xy[tid] = xy;
+            s_co[tid] = co;
             s_rgb[tid] = p.rgb[g];
+            s_box[tid] = alpha_box(xy, co);
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        for (int j0 = 0; j0 < n; j0 += kFwdBatch) {
+        const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, tg.lane);
+        for (int j0 = 0; j0 < m; j0 += kBatch) {
             if (!__ballot(!done)) break;  // every pixel of this wave has saturated
-            // branch-free alphas of kFwdBatch records (independent: the exps overlap) ...
-            float a[kFwdBatch];
+            // branch-free alphas of kBatch records (independent: the exps overlap) ...
+            float a[kBatch];
+            int slot[kBatch];
 #pragma unroll
-            for (int u = 0; u < kFwdBatch; ++u) {
-                const float2 xy = s_xy[j0 + u];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float4 co = s_co[j0 + u];
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                a[u] = power > 0.0f ? 0.0f : fminf(0.99f, co.w * expf(power));  // 0 => skipped below
+            for (int u = 0; u < kBatch; ++u) {
+                slot[u] = list[min(j0 + u, m - 1)];
+                float G;
+                a[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, G);
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
 #pragma unroll
-            for (int u = 0; u < kFwdBatch; ++u) {
-                if (done || j0 + u >= n) continue;
-                contributor++;
+            for (int u = 0; u < kBatch; ++u) {
+                if (done || j0 + u >= m) continue;
                 const float alpha = a[u];
                 if (alpha < 1.0f / 255.0f) continue;
                 const float test_T = T * (1 - alpha);
@@ -75,17 +153,17 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
                     done = true;
                     continue;
                 }
-                const float4 c = s_rgb[j0 + u];
+                const float4 c = s_rgb[slot[u]];
                 C0 += c.x * alpha * T;
                 C1 += c.y * alpha * T;
                 C2 += c.z * alpha * T;
                 T = test_T;
-                last_contributor = contributor;
+                last_contributor = (uint32_t)(i * kTilePix + slot[u] + 1);  // the record's 1-based list position
             }
         }
     }
-    if (inside) {
-        const int pid = p.W * py + px;
+    if (tg.inside) {
+        const int pid = p.W * tg.py + tg.px;
         const int plane = p.H * p.W;
         p.final_T[pid] = T;
         p.n_contrib[pid] = last_contributor;
@@ -95,135 +173,124 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     }
 }
 
-// Per-pixel state of the back-to-front replay (backward.cu:441-461).
-struct BwdPixel {
-    float T, T_final, last_alpha;
-    float acc0, acc1, acc2, lc0, lc1, lc2;
-    float dpix0, dpix1, dpix2, bg_dot;
-};
-
-constexpr int kRedBatch = 8;  // records reduced together by wave_sum8
-
 __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
     __shared__ float2 s_xy[kTilePix];
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
+    __shared__ float4 s_box[kTilePix];
     __shared__ float s_acc[9][kTilePix];
-    const int tile = xcd_swizzle(blockIdx.x, p.num_tiles);
+    __shared__ uint8_t s_list[4][kTilePix];
+    const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
-    const int lane = lane_id();
-    const int px = (tile % p.grid_x) * kTileX + (tid & (kTileX - 1));
-    const int py = (tile / p.grid_x) * kTileY + (tid >> 4);
-    const bool inside = px < p.W && py < p.H;
-    const uint2 rg = p.ranges[tile];
-    const int rounds = ((int)(rg.y - rg.x) + kTilePix - 1) / kTilePix;
-    int toDo = (int)(rg.y - rg.x);
-    const int pid = p.W * py + px;
+    const int lane = tg.lane;
+    const uint2 rg = p.ranges[tg.tile];
+    const int total = (int)(rg.y - rg.x);
+    const int rounds = (total + kTilePix - 1) / kTilePix;
+    int toDo = total;
+    const int pid = p.W * tg.py + tg.px;
     const int plane = p.H * p.W;
-    BwdPixel st;
-    st.T_final = inside ? p.final_T[pid] : 0.f;
-    st.T = st.T_final;
-    uint32_t contributor = (uint32_t)toDo;
-    const uint32_t last_contributor = inside ? p.n_contrib[pid] : 0u;
-    st.dpix0 = st.dpix1 = st.dpix2 = 0.f;
+    const bool inside = tg.inside;
+    // per-pixel replay state (backward.cu:441-461)
+    const float T_final = inside ? p.final_T[pid] : 0.f;
+    float T = T_final;
+    const int last_contributor = inside ? (int)p.n_contrib[pid] : 0;
+    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
     if (inside) {
-        st.dpix0 = p.dL_dpix[pid];
-        st.dpix1 = p.dL_dpix[plane + pid];
-        st.dpix2 = p.dL_dpix[2 * plane + pid];
+        dpix0 = p.dL_dpix[pid];
+        dpix1 = p.dL_dpix[plane + pid];
+        dpix2 = p.dL_dpix[2 * plane + pid];
     }
-    st.acc0 = st.acc1 = st.acc2 = 0.f;  // accum_rec
-    st.lc0 = st.lc1 = st.lc2 = 0.f;     // last_color
-    st.last_alpha = 0.f;
-    st.bg_dot = p.bg[0] * st.dpix0 + p.bg[1] * st.dpix1 + p.bg[2] * st.dpix2;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;  // accum_rec
+    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;     // last_color
+    float last_alpha = 0.f;
+    const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
-    const float pxf = (float)px, pyf = (float)py;
+    const float pxf = (float)tg.px, pyf = (float)tg.py;
+    uint8_t* list = s_list[tg.wave];
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         __syncthreads();
         const int progress = i * kTilePix + tid;
-        if ((int)rg.x + progress < (int)rg.y) {
+        if ((int)rg.x + progress < (int)rg.y) {  // loaded back to front (backward.cu:466-478)
             const uint32_t g = p.point_list[rg.y - progress - 1];
+            const float2 xy = p.means2D[g];
+            const float4 co = p.conic_opacity[g];
             s_id[tid] = g;
-            s_xy[tid] = p.means2D[g];
-            s_co[tid] = p.conic_opacity[g];
+            s_xy[tid] = xy;
+            s_co[tid] = co;
             s_rgb[tid] = p.rgb[g];
+            s_box[tid] = alpha_box(xy, co);
         }
 #pragma unroll
         for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        for (int j0 = 0; j0 < n; j0 += kRedBatch) {
-            // branch-free G / alpha of kRedBatch records (independent: the exps overlap) ...
-            float Gs[kRedBatch], As[kRedBatch];
+        const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane);
+        // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
+        const int front_base = total - 1 - i * kTilePix;
+        for (int j0 = 0; j0 < m; j0 += kBatch) {
+            // branch-free G / alpha of kBatch records (independent: the exps overlap) ...
+            float Gs[kBatch], As[kBatch];
+            int slot[kBatch];
 #pragma unroll
-            for (int u = 0; u < kRedBatch; ++u) {
-                const float2 xy = s_xy[j0 + u];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float4 co = s_co[j0 + u];
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                const float G = expf(power);
-                Gs[u] = G;
-                As[u] = power > 0.0f ? 0.0f : fminf(0.99f, co.w * G);  // 0 => skipped below
+            for (int u = 0; u < kBatch; ++u) {
+                slot[u] = list[min(j0 + u, m - 1)];
+                As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u]);
             }
             // ... then the sequential back-to-front recurrence (backward.cu:482-555)
-            float v[9][kRedBatch];
+            float v[9][kBatch];
             bool any = false;
 #pragma unroll
-            for (int u = 0; u < kRedBatch; ++u) {
+            for (int u = 0; u < kBatch; ++u) {
 #pragma unroll
                 for (int q = 0; q < 9; ++q) v[q][u] = 0.f;
-                const int j = j0 + u;
-                if (inside && j < n) {
-                    contributor--;
-                    if (contributor < last_contributor) {
-                        const float2 xy = s_xy[j];
-                        const float dx = xy.x - pxf, dy = xy.y - pyf;
-                        const float4 co = s_co[j];
-                        {
-                            const float G = Gs[u];
-                            const float alpha = As[u];
-                            if (!(alpha < 1.0f / 255.0f)) {
-                                any = true;
-                                const float inv1ma = 1.f / (1.f - alpha);
-                                st.T = st.T * inv1ma;  // backward.cu:503 (T recovered by division)
-                                const float dchannel_dcolor = alpha * st.T;
-                                const float4 c = s_rgb[j];
-                                st.acc0 = st.last_alpha * st.lc0 + (1.f - st.last_alpha) * st.acc0;
-                                st.acc1 = st.last_alpha * st.lc1 + (1.f - st.last_alpha) * st.acc1;
-                                st.acc2 = st.last_alpha * st.lc2 + (1.f - st.last_alpha) * st.acc2;
-                                st.lc0 = c.x;
-                                st.lc1 = c.y;
-                                st.lc2 = c.z;
-                                float dL_dalpha = (c.x - st.acc0) * st.dpix0;
-                                dL_dalpha += (c.y - st.acc1) * st.dpix1;
-                                dL_dalpha += (c.z - st.acc2) * st.dpix2;
-                                v[6][u] = dchannel_dcolor * st.dpix0;
-                                v[7][u] = dchannel_dcolor * st.dpix1;
-                                v[8][u] = dchannel_dcolor * st.dpix2;
-                                dL_dalpha *= st.T;
-                                st.last_alpha = alpha;
-                                dL_dalpha += (-st.T_final * inv1ma) * st.bg_dot;
-                                const float dL_dG = co.w * dL_dalpha;
-                                const float gdx = G * dx, gdy = G * dy;
-                                const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                                const float dG_ddely = -gdy * co.z - gdx * co.y;
-                                v[0][u] = dL_dG * dG_ddelx * ddelx_dx;
-                                v[1][u] = dL_dG * dG_ddely * ddely_dy;
-                                v[2][u] = -0.5f * gdx * dx * dL_dG;
-                                v[3][u] = -0.5f * gdx * dy * dL_dG;
-                                v[4][u] = -0.5f * gdy * dy * dL_dG;
-                                v[5][u] = G * dL_dalpha;
-                            }
-                        }
-                    }
-                }
+                const float alpha = As[u];
+                if (!inside || j0 + u >= m || front_base - slot[u] >= last_contributor || alpha < 1.0f / 255.0f)
+                    continue;
+                any = true;
+                const float G = Gs[u];
+                const float2 xy = s_xy[slot[u]];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float4 co = s_co[slot[u]];
+                const float inv1ma = 1.f / (1.f - alpha);
+                T = T * inv1ma;  // backward.cu:503 (T recovered by division)
+                const float dchannel_dcolor = alpha * T;
+                const float4 c = s_rgb[slot[u]];
+                acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
+                acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
+                acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
+                lc0 = c.x;
+                lc1 = c.y;
+                lc2 = c.z;
+                float dL_dalpha = (c.x - acc0) * dpix0;
+                dL_dalpha += (c.y - acc1) * dpix1;
+                dL_dalpha += (c.z - acc2) * dpix2;
+                v[6][u] = dchannel_dcolor * dpix0;
+                v[7][u] = dchannel_dcolor * dpix1;
+                v[8][u] = dchannel_dcolor * dpix2;
+                dL_dalpha *= T;
+                last_alpha = alpha;
+                dL_dalpha += (-T_final * inv1ma) * bg_dot;
+                const float dL_dG = co.w * dL_dalpha;
+                const float gdx = G * dx, gdy = G * dy;
+                const float dG_ddelx = -gdx * co.x - gdy * co.y;
+                const float dG_ddely = -gdy * co.z - gdx * co.y;
+                v[0][u] = dL_dG * dG_ddelx * ddelx_dx;
+                v[1][u] = dL_dG * dG_ddely * ddely_dy;
+                v[2][u] = -0.5f * gdx * dx * dL_dG;
+                v[3][u] = -0.5f * gdx * dy * dL_dG;
+                v[4][u] = -0.5f * gdy * dy * dL_dG;
+                v[5][u] = G * dL_dalpha;
             }
             if (__ballot(any)) {  // wave-uniform
+                const int col = lane >> 3;
+                const bool writer = (lane & 7) == 0 && j0 + col < m;
+                const int dst = list[min(j0 + col, m - 1)];
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
                     const float r = wave_sum8(v[q]);
-                    if ((lane & 7) == 0) atomicAdd(&s_acc[q][j0 + (lane >> 3)], r);
+                    if (writer) atomicAdd(&s_acc[q][dst], r);
                 }
             }
         }
