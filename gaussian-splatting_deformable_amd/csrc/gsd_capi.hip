@@ -152,10 +152,10 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd, kSe3Bwd,
-                kMarkVis, kNumKernels };
-const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_scan",  "scatter_keys", "tile_sort",
+                kMarkVis, kActFwd, kActBwd, kNumKernels };
+const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_scan",  "scatter_keys",   "tile_sort",
                                                "render_fwd",     "render_bwd", "preprocess_bwd", "se3_fwd",
-                                               "se3_bwd",        "mark_visible"};
+                                               "se3_bwd",        "mark_visible", "activate_fwd", "activate_bwd"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -394,6 +394,48 @@ int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in
                             dL_drot_in, as_stream(stream));
     });
     GSD_CHECK(false, as_stream(stream));
+    return GSD_OK;
+}
+
+int gsd_activate_forward(int32_t P, int32_t R, const float* xyz, const float* dxyz, const float* scaling,
+                         const float* dscale, const float* rotation, const float* drot, const float* opacity,
+                         const float* f_dc, const float* f_rest, const float* dsh, float* means_out,
+                         float* scales_out, float* rot_out, float* opac_out, float* shs_out, void* stream) {
+    if (P < 0 || R < 0) return fail(GSD_ERR_ARG, "invalid P / R");
+    if (P == 0) return GSD_OK;
+    if ((unsigned long long)P * 3ull * (1ull + R) >= (1ull << 32)) return fail(GSD_ERR_ARG, "P too large");
+    if (!xyz || !scaling || !rotation || !opacity || !f_dc || (R > 0 && !f_rest) || !means_out || !scales_out ||
+        !rot_out || !opac_out || !shs_out)
+        return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::ActivateParams p{};
+    p.P = P; p.R = R; p.xyz = xyz; p.dxyz = dxyz; p.scaling = scaling; p.dscale = dscale; p.rotation = rotation;
+    p.drot = drot; p.opacity = opacity; p.f_dc = f_dc; p.f_rest = f_rest; p.dsh = dsh; p.means_out = means_out;
+    p.scales_out = scales_out; p.rot_out = rot_out; p.opac_out = opac_out; p.shs_out = shs_out;
+    hipStream_t s = as_stream(stream);
+    timed(kActFwd, s, [&] { gsd::launch_activate_fwd(p, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float* scaling, const float* dscale,
+                          const float* rotation, const float* drot, const float* opacity, const float* g_means,
+                          const float* g_scales, const float* g_rot, const float* g_opac, const float* g_shs,
+                          float* g_xyz, float* g_scaling, float* g_rotation, float* g_opacity, float* g_fdc,
+                          float* g_frest, float* g_dxyz, float* g_dscale, float* g_drot, float* g_dsh, void* stream) {
+    if (P < 0 || R < 0) return fail(GSD_ERR_ARG, "invalid P / R");
+    if (P == 0) return GSD_OK;
+    if ((unsigned long long)P * 3ull * (1ull + R) >= (1ull << 32)) return fail(GSD_ERR_ARG, "P too large");
+    if (!scaling || !rotation || !opacity || !g_means || !g_scales || !g_rot || !g_opac || !g_shs)
+        return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::ActivateBwdParams p{};
+    p.P = P; p.R = R; p.accumulate = accumulate; p.scaling = scaling; p.dscale = dscale; p.rotation = rotation;
+    p.drot = drot; p.opacity = opacity; p.g_means = g_means; p.g_scales = g_scales; p.g_rot = g_rot;
+    p.g_opac = g_opac; p.g_shs = g_shs; p.g_xyz = g_xyz; p.g_scaling = g_scaling; p.g_rotation = g_rotation;
+    p.g_opacity = g_opacity; p.g_fdc = g_fdc; p.g_frest = g_frest; p.g_dxyz = g_dxyz; p.g_dscale = g_dscale;
+    p.g_drot = g_drot; p.g_dsh = g_dsh;
+    hipStream_t s = as_stream(stream);
+    timed(kActBwd, s, [&] { gsd::launch_activate_bwd(p, s); });
+    GSD_CHECK(false, s);
     return GSD_OK;
 }
 

@@ -101,7 +101,52 @@ struct RenderBwdParams {
     float* dL_dcolors;  // (P,3)
 };
 
+struct ActivateParams {
+    int P, R;  // R = rest SH coefficients per Gaussian (f_rest is (P,R,3))
+    const float* xyz;
+    const float* dxyz;     // optional offsets (NULL = 0)
+    const float* scaling;
+    const float* dscale;
+    const float* rotation;
+    const float* drot;
+    const float* opacity;
+    const float* f_dc;
+    const float* f_rest;
+    const float* dsh;      // (P,1+R,3) or NULL
+    float* means_out;
+    float* scales_out;
+    float* rot_out;
+    float* opac_out;
+    float* shs_out;
+};
+
+struct ActivateBwdParams {
+    int P, R, accumulate;
+    const float* scaling;
+    const float* dscale;
+    const float* rotation;
+    const float* drot;
+    const float* opacity;
+    const float* g_means;
+    const float* g_scales;
+    const float* g_rot;
+    const float* g_opac;
+    const float* g_shs;
+    float* g_xyz;        // parameter grads: written, or added to when accumulate != 0 (NULL = skip)
+    float* g_scaling;
+    float* g_rotation;
+    float* g_opacity;
+    float* g_fdc;
+    float* g_frest;
+    float* g_dxyz;       // offset grads: always written (NULL = skip)
+    float* g_dscale;
+    float* g_drot;
+    float* g_dsh;
+};
+
 // Host-side launchers (one per kernel; each lives in the .hip file that defines the kernel).
+void launch_activate_fwd(const ActivateParams& p, hipStream_t s);
+void launch_activate_bwd(const ActivateBwdParams& p, hipStream_t s);
 void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s);
 void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);

@@ -190,3 +190,64 @@ def se3_deform_backward(twist, means, rotations, dL_dmeans_out, dL_drot_out):
         _native.check(lib.gsd_se3_deform_backward(P, _ptr(tw), _ptr(m), _ptr(q), _ptr(gm), _ptr(gq), _ptr(dtw),
                                                   _ptr(dm), _ptr(dq), _stream(dev)))
     return dtw, dm, dq
+
+
+def _opt_f32(t, name, dev):
+    return None if t is None else _dev_f32(t, name, dev)
+
+
+def activate_forward(xyz, scaling, rotation, opacity, f_dc, f_rest, dxyz=None, dscale=None, drot=None, dsh=None):
+    """Fused render() preamble (gsd_activate_forward) -> (means3D, scales, rotations, opacities, shs)."""
+    lib = _native.load()
+    dev = xyz.device
+    P = int(xyz.size(0))
+    R = int(f_rest.size(1)) if f_rest.dim() == 3 else int(f_rest.numel() // max(P * 3, 1))
+    ins = [_dev_f32(t, n, dev) for t, n in ((xyz, "xyz"), (scaling, "scaling"), (rotation, "rotation"),
+                                           (opacity, "opacity"), (f_dc, "f_dc"), (f_rest, "f_rest"))]
+    offs = [_opt_f32(t, n, dev) for t, n in ((dxyz, "dxyz"), (dscale, "dscale"), (drot, "drot"), (dsh, "dsh"))]
+    means = torch.empty(P, 3, device=dev)
+    scales = torch.empty(P, 3, device=dev)
+    rots = torch.empty(P, 4, device=dev)
+    opac = torch.empty(P, 1, device=dev)
+    shs = torch.empty(P, 1 + R, 3, device=dev)
+    x, s, q, o, fdc, frest = ins
+    dx, ds, dq, dsh_ = offs
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_activate_forward(P, R, _ptr(x), _ptr(dx), _ptr(s), _ptr(ds), _ptr(q), _ptr(dq), _ptr(o),
+                                               _ptr(fdc), _ptr(frest), _ptr(dsh_), _ptr(means), _ptr(scales),
+                                               _ptr(rots), _ptr(opac), _ptr(shs), _stream(dev)))
+    return means, scales, rots, opac, shs
+
+
+def activate_backward(scaling, rotation, opacity, dscale, drot, g_means, g_scales, g_rot, g_opac, g_shs, sinks,
+                      has_off, rest_shape):
+    """Backward of activate_forward.  sinks: None, or the 6 parameter .grad buffers to add into in place.
+    -> ((g_xyz, g_scaling, g_rotation, g_opacity, g_fdc, g_frest), (g_dxyz, g_dscale, g_drot, g_dsh))."""
+    lib = _native.load()
+    dev = scaling.device
+    P = int(scaling.size(0))
+    R = int(rest_shape[1])
+    z = lambda t, shape: torch.zeros(shape, device=dev) if t is None else t  # noqa: E731  (unused grads)
+    gm = _dev_f32(z(g_means, (P, 3)), "g_means", dev)
+    gs = _dev_f32(z(g_scales, (P, 3)), "g_scales", dev)
+    gr = _dev_f32(z(g_rot, (P, 4)), "g_rot", dev)
+    go = _dev_f32(z(g_opac, (P, 1)), "g_opac", dev)
+    gsh = _dev_f32(z(g_shs, (P, 1 + R, 3)), "g_shs", dev)
+    if sinks is None:
+        outs = [torch.empty(P, 3, device=dev), torch.empty(P, 3, device=dev), torch.empty(P, 4, device=dev),
+                torch.empty(P, 1, device=dev), torch.empty(P, 1, 3, device=dev), torch.empty(rest_shape, device=dev)]
+        acc = 0
+    else:
+        outs = list(sinks)
+        acc = 1
+    offg = [torch.empty(P, 3, device=dev) if has_off[0] else None,
+            torch.empty(P, 3, device=dev) if has_off[1] else None,
+            torch.empty(P, 4, device=dev) if has_off[2] else None,
+            torch.empty(P, 1 + R, 3, device=dev) if has_off[3] else None]
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_activate_backward(
+            P, R, acc, _ptr(scaling.contiguous()), _ptr(None if dscale is None else dscale.contiguous()),
+            _ptr(rotation.contiguous()), _ptr(None if drot is None else drot.contiguous()),
+            _ptr(opacity.contiguous()), _ptr(gm), _ptr(gs), _ptr(gr), _ptr(go), _ptr(gsh),
+            *[_ptr(t) for t in outs], *[_ptr(t) for t in offg], _stream(dev)))
+    return tuple(outs), tuple(offg)

@@ -49,6 +49,8 @@ SIGNATURES = {
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),
     "gsd_se3_deform_forward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_se3_deform_backward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_activate_forward": (_i32, [_i32, _i32] + [_vp] * 15 + [_vp]),
+    "gsd_activate_backward": (_i32, [_i32, _i32, _i32] + [_vp] * 20 + [_vp]),
     "gsd_timing_enable": (_i32, [_i32]),
     "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "gsd_timing_reset": (None, []),

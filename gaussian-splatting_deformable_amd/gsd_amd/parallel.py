@@ -52,6 +52,7 @@ class FlatGrads:
     def attach(self):
         for p, v in zip(self.params, self.views):
             p.grad = v
+            p._gsd_inplace_grad = True  # fused HIP backwards may add into this .grad directly
 
     def zero(self):
         self.slab.zero_()

@@ -17,6 +17,7 @@ from types import SimpleNamespace
 import torch
 import torch.nn.functional as F
 
+from .activate import activate
 from .deform import se3_deform
 from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
 from .sh import eval_sh
@@ -64,13 +65,16 @@ def build_covariance_from_scaling_rotation(scaling, scaling_modifier, rotation):
 
 
 class ZeroOffsets:
-    """Deformation producer returning the reference's pre-3000-iteration zeros
-    (scene/gaussian_model.py:305-313) -- (dx, dscale, drot, dSH)."""
+    """Deformation producer equivalent to the reference's pre-3000-iteration zeros
+    (scene/gaussian_model.py:305-313) -- (dx, dscale, drot, dSH).  Returns None for
+    each offset ("zero"), which the fused preamble skips instead of adding zeros."""
 
     def __call__(self, pts, time, iteration):
-        P = pts.shape[0]
-        z = pts.new_zeros
-        return z(P, 3), z(P, 3), z(P, 4), z(P, 48)
+        return None, None, None, None
+
+
+def _zeros_if_none(t, P, w, like):
+    return like.new_zeros(P, w) if t is None else t
 
 
 class DeformableGaussians:
@@ -138,6 +142,9 @@ class DeformableGaussians:
     def get_xyz_all(self, pts, time, iteration):
         """scene/gaussian_model.py:761-763 -> (means3D, means3D_ori, offset, scale_off, rot_off, mlp_shs)."""
         dx, ds, dq, dsh = self.offset_model(pts, time, iteration)
+        P = self._xyz.shape[0]
+        dx, ds = _zeros_if_none(dx, P, 3, self._xyz), _zeros_if_none(ds, P, 3, self._xyz)
+        dq, dsh = _zeros_if_none(dq, P, 4, self._xyz), _zeros_if_none(dsh, P, 48, self._xyz)
         if self.deform == "se3":
             twist = self.get_twist(pts, time, iteration)
             means, _ = se3_deform(twist, self._xyz + dx)
@@ -173,10 +180,36 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
     means3D = pc.get_xyz
     t = control_time if control_time is not None else viewpoint_camera.time
     time = torch.full((means3D.size(0), 1), t, device=means3D.device)
+    means2D = screenspace_points
+    python_modes = (getattr(pipe, "compute_cov3D_python", False) or getattr(pipe, "convert_SHs_python", False)
+                    or override_color is not None)
+    if not python_modes and hasattr(pc, "_features_rest") and getattr(pc, "fused_preamble", True):
+        # fused preamble: offsets + activations + SH concat in one HIP pass (gsd_amd.activate)
+        P = means3D.size(0)
+        dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, time, iteration)
+        dsh = None if mlp_shs is None else mlp_shs.reshape(P, -1, 3)
+        means3D, scales, rotations, opacity, shs = activate(pc._xyz, pc._scaling, pc._rotation, pc._opacity,
+                                                            pc._features_dc, pc._features_rest, dx, scale_offset,
+                                                            rot_offset, dsh)
+        if getattr(pc, "deform", "additive") == "se3":
+            # one fused kernel moves means AND rotations by the same rigid motion
+            means3D, rotations = se3_deform(pc.get_twist(pc.get_xyz, time, iteration), means3D, rotations)
+        means3D_ori = pc._xyz
+        moved = dx is not None or getattr(pc, "deform", "additive") == "se3"
+        means3D_offset = means3D - means3D_ori if moved else torch.zeros_like(means3D_ori)
+        rot_offset = rot_offset if rot_offset is not None else means3D.new_zeros(P, 4)
+        rendered_image, radii = rasterizer(means3D=means3D, means2D=means2D, shs=shs, opacities=opacity,
+                                           scales=scales, rotations=rotations)
+        return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
+                "radii": radii, "means3D": means3D, "means3D_ori": means3D_ori, "rotations": rotations,
+                "means3D_offset": means3D_offset, "opacities": opacity, "rot_offset": rot_offset}
+    # reference-literal path (Python covariance / SH modes, override colours)
     se3_rot = getattr(pc, "deform", "additive") == "se3" and not getattr(pipe, "compute_cov3D_python", False)
     if se3_rot:
-        # one fused kernel moves means AND rotations by the same rigid motion
         dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, time, iteration)
+        P = means3D.size(0)
+        dx, scale_offset = _zeros_if_none(dx, P, 3, pc._xyz), _zeros_if_none(scale_offset, P, 3, pc._xyz)
+        rot_offset, mlp_shs = _zeros_if_none(rot_offset, P, 4, pc._xyz), _zeros_if_none(mlp_shs, P, 48, pc._xyz)
         twist = pc.get_twist(means3D, time, iteration)
         means3D_ori = pc._xyz
         means3D, se3_rotations = se3_deform(twist, pc._xyz + dx, pc.rotation_activation(pc._rotation + rot_offset))
@@ -184,7 +217,6 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
     else:
         means3D, means3D_ori, means3D_offset, scale_offset, rot_offset, mlp_shs = pc.get_xyz_all(means3D, time,
                                                                                                  iteration)
-    means2D = screenspace_points
     opacity = pc.get_opacity
     scales = rotations = cov3D_precomp = None
     if getattr(pipe, "compute_cov3D_python", False):

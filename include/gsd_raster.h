@@ -139,6 +139,23 @@ int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in
                             const float* dL_dmeans_out, const float* dL_drot_out, float* dL_dtwist,
                             float* dL_dmeans_in, float* dL_drot_in, void* stream);
 
+/* Fused render() preamble (gaussian_renderer/__init__.py:79-140, gaussian_model.py:761-797):
+ *   means = xyz + dxyz, scales = exp(scaling + dscale), rotations = normalize(rotation + drot),
+ *   opacities = sigmoid(opacity), shs = cat(f_dc, f_rest) + dsh.
+ * Offsets (dxyz (P,3), dscale (P,3), drot (P,4), dsh (P,1+R,3)) may be NULL = zero; f_rest is (P,R,3). */
+int gsd_activate_forward(int32_t P, int32_t R, const float* xyz, const float* dxyz, const float* scaling,
+                         const float* dscale, const float* rotation, const float* drot, const float* opacity,
+                         const float* f_dc, const float* f_rest, const float* dsh, float* means_out,
+                         float* scales_out, float* rot_out, float* opac_out, float* shs_out, void* stream);
+
+/* Backward of gsd_activate_forward.  Parameter gradients (g_xyz .. g_frest) are written, or added into the
+ * existing values when accumulate != 0; offset gradients (g_dxyz .. g_dsh) are written.  Any output may be NULL. */
+int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float* scaling, const float* dscale,
+                          const float* rotation, const float* drot, const float* opacity, const float* g_means,
+                          const float* g_scales, const float* g_rot, const float* g_opac, const float* g_shs,
+                          float* g_xyz, float* g_scaling, float* g_rotation, float* g_opacity, float* g_fdc,
+                          float* g_frest, float* g_dxyz, float* g_dscale, float* g_drot, float* g_dsh, void* stream);
+
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead
  * per launch); gsd_timing_collect() synchronises on the last recorded event

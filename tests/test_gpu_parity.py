@@ -237,6 +237,57 @@ def test_render_end_to_end_autograd():
         assert int(out["visibility_filter"].sum()) > 0
 
 
+@pytest.mark.parametrize("with_offsets", [False, True])
+def test_fused_activation_matches_torch(with_offsets):
+    """gsd_activate_forward/backward == the reference's torch preamble (gaussian_renderer/__init__.py:79-140)."""
+    from gsd_amd.activate import activate
+    g = torch.Generator().manual_seed(3)
+    P = 5000
+    mk = lambda *s: torch.randn(*s, generator=g).to(DEV).requires_grad_(True)  # noqa: E731
+    xyz, sc, rot, op, fdc, frest = mk(P, 3), mk(P, 3), mk(P, 4), mk(P, 1), mk(P, 1, 3), mk(P, 15, 3)
+    offs = [mk(P, 3), mk(P, 3), mk(P, 4), mk(P, 16, 3)] if with_offsets else [None] * 4
+    outs = activate(xyz, sc, rot, op, fdc, frest, *offs)
+    z = lambda t, s: torch.zeros(s, device=DEV) if t is None else t  # noqa: E731
+    ref = (xyz + z(offs[0], (P, 3)), torch.exp(sc + z(offs[1], (P, 3))),
+           torch.nn.functional.normalize(rot + z(offs[2], (P, 4))), torch.sigmoid(op),
+           torch.cat([fdc, frest], 1) + z(offs[3], (P, 16, 3)))
+    for a, b in zip(outs, ref):
+        assert rel_l2(a.detach().cpu(), b.detach().cpu()) <= 1e-6
+    ws = [torch.randn(o.shape, generator=g).to(DEV) for o in outs]
+    leaves = [xyz, sc, rot, op, fdc, frest] + [o for o in offs if o is not None]
+    got = torch.autograd.grad(sum((o * w).sum() for o, w in zip(outs, ws)), leaves)
+    want = torch.autograd.grad(sum((o * w).sum() for o, w in zip(ref, ws)), leaves)
+    for a, b in zip(got, want):
+        assert rel_l2(a.cpu(), b.cpu()) <= 1e-5
+    # in-place accumulation into existing .grad buffers
+    for t in (xyz, sc, rot, op, fdc, frest):
+        t.grad = torch.ones_like(t)
+        t._gsd_inplace_grad = True
+    outs = activate(xyz, sc, rot, op, fdc, frest, *offs)
+    sum((o * w).sum() for o, w in zip(outs, ws)).backward()
+    for t, w in zip((xyz, sc, rot, op, fdc, frest), want):
+        assert rel_l2((t.grad - 1).cpu(), w.cpu()) <= 1e-5
+
+
+def test_fused_preamble_render_matches_reference_path():
+    """render(): fused HIP preamble vs the reference-literal torch preamble, same image and parameter grads."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.scene import make_gaussians
+    params = make_gaussians(20_000, 320, 240, seed=9, device=DEV)
+    cam = synthetic_camera(320, 240).to(DEV)
+    res = []
+    for fused in (True, False):
+        pc = DeformableGaussians(params, sh_degree=3)
+        pc.fused_preamble = fused
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+        (out["render"] * torch.linspace(0, 1, 320, device=DEV)).sum().backward()
+        res.append((out["render"].detach(), [p.grad.clone() for p in pc.parameters()]))
+    assert (res[0][0] - res[1][0]).abs().max() <= 1e-5
+    for a, b in zip(res[0][1], res[1][1]):
+        assert rel_l2(a.cpu(), b.cpu()) <= 1e-4
+
+
 def test_config4_invariants():
     """Full-size (1M Gaussians, 1080p, SH3) size-independent properties."""
     from gsd_amd.introspect import decode
