@@ -17,9 +17,9 @@
 //
 // Backward: the reference issues 9 float atomicAdds per (pixel, Gaussian) pair
 // (backward.cu:523,545-554), all 256 lanes on the same address.  Here each
-// wave computes 8 records' partials, reduces them across its 64 lanes with one
-// transposed butterfly per quantity (wave_sum8: permlane32/16 swaps + DPP),
-// 8 lanes add the 8 wave totals into LDS accumulators, and after each
+// wave computes 4 records' partials, reduces them across its 64 lanes with one
+// transposed butterfly per quantity (wave_sum4: permlane32/16 swaps + DPP),
+// 4 lanes add the 4 wave totals into LDS accumulators, and after each
 // 256-record batch every record's 9 sums go to HBM as one set of global
 // atomics: at most 9 global atomics per (Gaussian, tile) instance instead of
 // 9 per (Gaussian, pixel) pair.
@@ -27,7 +27,8 @@
 
 namespace gsd {
 
-constexpr int kBatch = 8;  // records evaluated together (ILP across the exps; one wave_sum8 in the backward)
+constexpr int kBatch = 8;     // forward: records whose alphas are evaluated together (ILP across the exps)
+constexpr int kBwdBatch = 4;  // backward: records per reduction (wave_sum4; keeps 36 partials live, not 72)
 
 // Bounding box of {d : alpha(d) >= 1/255} for a record, inflated for safety.
 // Q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o); half-widths sqrt(t c/det), sqrt(t a/det).
@@ -70,11 +71,29 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, ui
 
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
 // Shared by both passes so their skip decisions are identical.
+// exp via the hardware 2^x (v_exp_f32, 1 ulp) on power * log2(e): <= ~5 ulp over the range that matters
+// (power in [-12, 0]), against ~10 VALU ops for the libm-accurate expf.  Results stay inside the image /
+// n_contrib tolerances of DESIGN.md 4; GSD_PRECISE_EXP restores expf.
+__device__ __forceinline__ float gauss_exp(float power) {
+#ifdef GSD_PRECISE_EXP
+    return expf(power);
+#else
+    return __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
+#endif
+}
+
 __device__ __forceinline__ float record_alpha(float2 xy, float4 co, float pxf, float pyf, float& G) {
     const float dx = xy.x - pxf, dy = xy.y - pyf;
     const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-    G = expf(power);
+    G = gauss_exp(power);
     return power > 0.0f ? 0.0f : fminf(0.99f, co.w * G);
+}
+
+// 1/d from v_rcp_f32 (1 ulp) plus one Newton step: ~0.5 ulp in 3 VALU ops instead of the ~10 of the
+// correctly rounded division sequence.
+__device__ __forceinline__ float fast_recip(float d) {
+    float r = __builtin_amdgcn_rcpf(d);
+    return fmaf(fmaf(-d, r, 1.0f), r, r);
 }
 
 struct TileGeom {
@@ -229,20 +248,22 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
-        for (int j0 = 0; j0 < m; j0 += kBatch) {
-            // branch-free G / alpha of kBatch records (independent: the exps overlap) ...
-            float Gs[kBatch], As[kBatch];
-            int slot[kBatch];
+        for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
+            // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
+            float Gs[kBwdBatch], As[kBwdBatch];
+            int slot[kBwdBatch];
 #pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
+            for (int u = 0; u < kBwdBatch; ++u) {
                 slot[u] = list[min(j0 + u, m - 1)];
                 As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u]);
             }
             // ... then the sequential back-to-front recurrence (backward.cu:482-555)
-            float v[9][kBatch];
+            float v[9][kBwdBatch];
             bool any = false;
 #pragma unroll
-            for (int u = 0; u < kBatch; ++u) {
+            for (int u = 0; u < kBwdBatch; ++u) {
+                // gradient arithmetic has no bit-exact contract: let the compiler fuse to FMA
+#pragma clang fp contract(fast)
 #pragma unroll
                 for (int q = 0; q < 9; ++q) v[q][u] = 0.f;
                 const float alpha = As[u];
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 const float2 xy = s_xy[slot[u]];
                 const float dx = xy.x - pxf, dy = xy.y - pyf;
                 const float4 co = s_co[slot[u]];
-                const float inv1ma = 1.f / (1.f - alpha);
+                const float inv1ma = fast_recip(1.f - alpha);
                 T = T * inv1ma;  // backward.cu:503 (T recovered by division)
                 const float dchannel_dcolor = alpha * T;
                 const float4 c = s_rgb[slot[u]];
@@ -284,12 +305,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 v[5][u] = G * dL_dalpha;
             }
             if (__ballot(any)) {  // wave-uniform
-                const int col = lane >> 3;
-                const bool writer = (lane & 7) == 0 && j0 + col < m;
+                const int col = lane >> 4;
+                const bool writer = (lane & 15) == 0 && j0 + col < m;
                 const int dst = list[min(j0 + col, m - 1)];
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
-                    const float r = wave_sum8(v[q]);
+                    const float r = wave_sum4(v[q]);
                     if (writer) atomicAdd(&s_acc[q][dst], r);
                 }
             }
