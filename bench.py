@@ -45,6 +45,7 @@ def algorithmic_bytes(P, V, K, W, H, C):
     npix = W * H
     return {
         "preprocess_fwd": 44 * P + 12 * C * V + 4 * P + 45 * V,
+        "tile_hist": 4 * P + 8 * V,
         "tile_scan": 16 * T,
         "scatter_keys": 4 * P + 12 * V + 8 * K,
         "tile_sort": 8 * T + 8 * K + 4 * K,

@@ -51,11 +51,22 @@ struct Geom {
     float* depths;
     int* radii;
     uint8_t* clamped;
+    uint32_t* hist;  // LDS-histogram binning workspace [num_blocks][T] + [segments][T]
+    uint32_t* part;
+    int chunk, num_blocks;
 };
+
+bool hist_binning(size_t T) { return T <= (size_t)gsd::kHistMaxTiles; }
+
+void hist_shape(size_t P, int* chunk, int* nblocks) {
+    const size_t c = (P + gsd::kHistTargetBlocks - 1) / gsd::kHistTargetBlocks;
+    *chunk = (int)(c < 256 ? 256 : c);
+    *nblocks = (int)((P + *chunk - 1) / *chunk);
+}
 // GeometryState (rasterizer_impl.h:29-41), re-laid out: what render gathers per
 // instance (xy, conic/opacity, rgb) is 16-B aligned; cov3D is recomputed in
 // the backward instead of stored; no P-wide scan space is needed.
-size_t carve_geom(void* base, size_t P, Geom* g) {
+size_t carve_geom(void* base, size_t P, size_t T, Geom* g) {
     char* p = base ? align_ptr(base) : nullptr;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -70,8 +81,17 @@ size_t carve_geom(void* base, size_t P, Geom* g) {
     v.depths = reinterpret_cast<float*>(take(P * sizeof(float)));
     v.radii = reinterpret_cast<int*>(take(P * sizeof(int)));
     v.clamped = reinterpret_cast<uint8_t*>(take(P));
+    hist_shape(P, &v.chunk, &v.num_blocks);
+    const size_t segs = ((size_t)v.num_blocks + gsd::kColSeg - 1) / gsd::kColSeg;
+    const bool use_hist = hist_binning(T) && P > 0;
+    v.hist = reinterpret_cast<uint32_t*>(take(use_hist ? (size_t)v.num_blocks * T * sizeof(uint32_t) : 0));
+    v.part = reinterpret_cast<uint32_t*>(take(use_hist ? segs * T * sizeof(uint32_t) : 0));
     if (g) *g = v;
     return off + kAlign;
+}
+
+size_t grid_tiles(int W, int H) {
+    return (size_t)((W + gsd::kTileX - 1) / gsd::kTileX) * (size_t)((H + gsd::kTileY - 1) / gsd::kTileY);
 }
 
 struct Img {
@@ -125,6 +145,14 @@ size_t carve_bin(void* base, size_t K, Bin* g) {
 int grid_x(const gsd_raster_args* a) { return (a->width + gsd::kTileX - 1) / gsd::kTileX; }
 int grid_y(const gsd_raster_args* a) { return (a->height + gsd::kTileY - 1) / gsd::kTileY; }
 
+gsd::HistParams hist_params(const gsd_raster_args* a, const Geom& g, int T) {
+    gsd::HistParams hp{};
+    hp.P = a->P; hp.chunk = g.chunk; hp.num_blocks = g.num_blocks; hp.num_tiles = T;
+    hp.grid_x = grid_x(a); hp.grid_y = grid_y(a);
+    hp.radii = g.radii; hp.means2D = g.means2D; hp.hist = g.hist; hp.part = g.part;
+    return hp;
+}
+
 int validate(const gsd_raster_args* a, bool forward) {
     if (!a) return fail(GSD_ERR_ARG, "null gsd_raster_args");
     if (a->P < 0) return fail(GSD_ERR_ARG, "means3D must have dimensions (num_points, 3)");
@@ -151,11 +179,12 @@ int validate(const gsd_raster_args* a, bool forward) {
 hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
-enum KernelId { kPreFwd, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd, kSe3Bwd,
-                kMarkVis, kActFwd, kActBwd, kNumKernels };
-const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_scan",  "scatter_keys",   "tile_sort",
-                                               "render_fwd",     "render_bwd", "preprocess_bwd", "se3_fwd",
-                                               "se3_bwd",        "mark_visible", "activate_fwd", "activate_bwd"};
+enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kNumKernels };
+const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
+                                               "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
+                                               "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
+                                               "activate_bwd"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -202,7 +231,9 @@ extern "C" {
 int gsd_abi_version(void) { return GSD_ABI_VERSION; }
 const char* gsd_last_error(void) { return g_err.c_str(); }
 
-size_t gsd_geom_buffer_bytes(int32_t P) { return carve_geom(nullptr, (size_t)(P < 0 ? 0 : P), nullptr); }
+size_t gsd_geom_buffer_bytes(int32_t P, int32_t width, int32_t height) {
+    return carve_geom(nullptr, (size_t)(P < 0 ? 0 : P), grid_tiles(width, height), nullptr);
+}
 size_t gsd_image_buffer_bytes(int32_t width, int32_t height) {
     const size_t gx = (size_t)(width + gsd::kTileX - 1) / gsd::kTileX, gy = (size_t)(height + gsd::kTileY - 1) / gsd::kTileY;
     return carve_img(nullptr, (size_t)width * (size_t)height, gx * gy, nullptr);
@@ -217,7 +248,7 @@ void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t K, size_
     Geom g;
     Img im;
     Bin b;
-    carve_geom(base, (size_t)(P < 0 ? 0 : P), &g);
+    carve_geom(base, (size_t)(P < 0 ? 0 : P), gx * gy, &g);
     carve_img(base, (size_t)width * (size_t)height, gx * gy, &im);
     carve_bin(base, (size_t)(K < 0 ? 0 : K), &b);
     if (go) {
@@ -244,10 +275,11 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     hipStream_t s = as_stream(stream);
     Geom g;
     Img im;
-    carve_geom(geom_buffer, a->P, &g);
     const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_geom(geom_buffer, a->P, T, &g);
     carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
-    GSD_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
+    const bool use_hist = hist_binning(T);
+    if (!use_hist) GSD_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
     GSD_HIP(hipMemsetAsync(im.counters, 0, 16, s));
 
     gsd::PreprocessParams p{};
@@ -261,9 +293,15 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
     p.radii = radii ? radii : g.radii;
     p.means2D = g.means2D; p.depths = g.depths; p.conic_opacity = g.conic_opacity; p.rgb = g.rgb;
-    p.clamped = g.clamped; p.tile_count = im.tile_count; p.err_flags = im.counters + 1;
+    p.clamped = g.clamped; p.tile_count = use_hist ? nullptr : im.tile_count; p.err_flags = im.counters + 1;
     timed(kPreFwd, s, [&] { gsd::launch_preprocess_fwd(p, s); });
     GSD_CHECK(a->debug, s);
+    if (use_hist) {
+        gsd::HistParams hp = hist_params(a, g, T);
+        hp.radii = p.radii;
+        timed(kTileHist, s, [&] { gsd::launch_tile_hist(hp, im.tile_count, s); });
+        GSD_CHECK(a->debug, s);
+    }
     timed(kTileScan, s, [&] { gsd::launch_tile_scan(T, im.tile_count, im.ranges, im.tile_cursor, im.counters, s); });
     GSD_CHECK(a->debug, s);
     if (!g_pinned) GSD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_pinned), 16, hipHostMallocDefault));
@@ -287,16 +325,22 @@ int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, vo
     Geom g;
     Img im;
     Bin b;
-    carve_geom(geom_buffer, a->P, &g);
     const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_geom(geom_buffer, a->P, T, &g);
     carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
     carve_bin(binning_buffer, (size_t)K, &b);
     if (K > 0) {
-        gsd::BinParams bp{};
-        bp.P = a->P; bp.grid_x = gx; bp.grid_y = gy; bp.num_tiles = T;
-        bp.radii = radii ? radii : g.radii;
-        bp.means2D = g.means2D; bp.depths = g.depths; bp.tile_cursor = im.tile_cursor; bp.bucket_keys = b.keys;
-        timed(kScatter, s, [&] { gsd::launch_scatter_keys(bp, s); });
+        if (hist_binning(T)) {
+            gsd::HistParams hp = hist_params(a, g, T);
+            hp.radii = radii ? radii : g.radii;
+            timed(kScatter, s, [&] { gsd::launch_scatter_hist(hp, im.tile_cursor, g.depths, b.keys, s); });
+        } else {
+            gsd::BinParams bp{};
+            bp.P = a->P; bp.grid_x = gx; bp.grid_y = gy; bp.num_tiles = T;
+            bp.radii = radii ? radii : g.radii;
+            bp.means2D = g.means2D; bp.depths = g.depths; bp.tile_cursor = im.tile_cursor; bp.bucket_keys = b.keys;
+            timed(kScatter, s, [&] { gsd::launch_scatter_keys(bp, s); });
+        }
         GSD_CHECK(a->debug, s);
         timed(kTileSort, s, [&] { gsd::launch_tile_sort(T, im.ranges, b.keys, b.scratch, b.point_list, s); });
         GSD_CHECK(a->debug, s);
@@ -329,8 +373,8 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     Geom g;
     Img im;
     Bin b;
-    carve_geom(const_cast<void*>(geom_buffer), a->P, &g);
     const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_geom(const_cast<void*>(geom_buffer), a->P, T, &g);
     carve_img(const_cast<void*>(image_buffer), (size_t)a->width * a->height, T, &im);
     carve_bin(const_cast<void*>(binning_buffer), (size_t)K, &b);
 

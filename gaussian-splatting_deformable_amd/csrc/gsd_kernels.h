@@ -71,6 +71,15 @@ struct BinParams {
     unsigned long long* bucket_keys;
 };
 
+// LDS-histogram binning (gsd_binning.hip): block b owns Gaussians [b*chunk, (b+1)*chunk)
+struct HistParams {
+    int P, chunk, num_blocks, num_tiles, grid_x, grid_y;
+    const int* radii;
+    const float2* means2D;
+    uint32_t* hist;  // [num_blocks][num_tiles]
+    uint32_t* part;  // [ceil(num_blocks / kColSeg)][num_tiles]
+};
+
 struct RenderParams {
     int W, H, grid_x, num_tiles;
     const uint2* ranges;
@@ -162,6 +171,14 @@ void launch_se3_fwd(int P, const float* twist, const float* means_in, const floa
 void launch_se3_bwd(int P, const float* twist, const float* means_in, const float* rot_in, const float* dmeans_out,
                     const float* drot_out, float* dtwist, float* dmeans_in, float* drot_in, hipStream_t s);
 
+void launch_tile_hist(const HistParams& p, uint32_t* tile_count, hipStream_t s);
+void launch_scatter_hist(const HistParams& p, const uint32_t* tile_base, const float* depths,
+                         unsigned long long* keys, hipStream_t s);
+
+constexpr int kHistThreads = 512;       // LDS-histogram binning workgroup
+constexpr int kHistMaxTiles = 40960;    // 160 KiB of u32 bins; larger grids use global-atomic binning
+constexpr int kHistTargetBlocks = 512;  // Gaussian chunks per view
+constexpr int kColSeg = 32;             // histogram rows per column-scan segment
 constexpr int kScanThreads = 1024;
 constexpr int kSortCap = 4096;  // instances sorted in one LDS pass (32 KiB of u64 keys)
 

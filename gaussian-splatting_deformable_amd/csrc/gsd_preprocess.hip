@@ -139,7 +139,9 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     p.radii[idx] = (int)my_radius;
     p.means2D[idx] = pix;
     p.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, p.opacities[idx]);
-    // per-tile instance counts (the binning histogram)
+    // per-tile instance counts by global atomics -- only on the fallback path for very
+    // large tile grids; normally k_tile_hist builds them from LDS histograms instead
+    if (!p.tile_count) return;
     for (int y = r.y0; y < r.y1; ++y)
         for (int x = r.x0; x < r.x1; ++x)
             __hip_atomic_fetch_add(p.tile_count + (y * p.grid_x + x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

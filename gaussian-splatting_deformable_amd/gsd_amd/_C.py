@@ -95,7 +95,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         return 0, torch.zeros(3, H, W, dtype=torch.float32, device=dev), radii, empty, empty.clone(), empty.clone()
     with torch.cuda.device(dev):
         stream = _stream(dev)
-        geom = torch.empty(lib.gsd_geom_buffer_bytes(P), **byte)
+        geom = torch.empty(lib.gsd_geom_buffer_bytes(P, W, H), **byte)
         img = torch.empty(lib.gsd_image_buffer_bytes(W, H), **byte)
         K = _i64(0)
         _native.check(lib.gsd_rasterize_forward_bin(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(radii),

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 1
+#define GSD_ABI_VERSION 2
 
 enum {
     GSD_OK = 0,
@@ -82,7 +82,7 @@ const char* gsd_last_error(void);
 
 /* State-buffer sizes in bytes (GeometryState / ImageState / BinningState,
  * rasterizer_impl.h:29-73; layouts are private to this library). */
-size_t gsd_geom_buffer_bytes(int32_t P);
+size_t gsd_geom_buffer_bytes(int32_t P, int32_t width, int32_t height);
 size_t gsd_image_buffer_bytes(int32_t width, int32_t height);
 size_t gsd_binning_buffer_bytes(int64_t num_rendered);
 

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--timing", action="store_true", help="print per-kernel device times (gsd_timing_*)")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
@@ -36,7 +37,10 @@ def main():
     e = torch.empty(0)
     tx, ty = math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2)
     dpix = torch.randn(3, H, W, device=dev) * 1e-3
-    for _ in range(a.iters):
+    from gsd_amd._native import kernel_times
+    for it in range(a.iters):
+        if a.timing and it == 1:
+            kernel_times(enable=True, reset=True)
         K, color, radii, geom, binning, img = _C.rasterize_gaussians(
             bg, means, e, opac, scales, rots, 1.0, e, cam.world_view_transform, cam.full_proj_transform, tx, ty, H, W,
             shs, D, cam.camera_center, False, False)
@@ -44,6 +48,9 @@ def main():
                                         cam.full_proj_transform, tx, ty, dpix, shs, D, cam.camera_center, geom, K,
                                         binning, img, False)
     torch.cuda.synchronize()
+    if a.timing:
+        for k, (tot, n) in kernel_times(enable=False).items():
+            print("%-16s %8.4f ms/launch (%d launches)" % (k, tot / n, n))
     print("done K=%d" % K)
 
 

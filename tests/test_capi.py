@@ -35,8 +35,8 @@ def test_abi_version_and_sizes():
     from gsd_amd import _native
     lib = _native.load()
     assert lib.gsd_abi_version() == _native.ABI_VERSION
-    assert lib.gsd_geom_buffer_bytes(0) > 0
-    assert lib.gsd_geom_buffer_bytes(1000) > lib.gsd_geom_buffer_bytes(10)
+    assert lib.gsd_geom_buffer_bytes(0, 64, 64) > 0
+    assert lib.gsd_geom_buffer_bytes(1000, 64, 64) > lib.gsd_geom_buffer_bytes(10, 64, 64)
     assert lib.gsd_binning_buffer_bytes(1_000_000) >= 20_000_000    # 8 + 8 + 4 B per instance
     assert lib.gsd_image_buffer_bytes(1920, 1080) >= 1920 * 1080 * 8
 
@@ -49,7 +49,7 @@ def test_state_layout_is_aligned_and_disjoint():
     for arr in (list(go), list(io), list(bo)):
         assert all(o % 256 == 0 for o in arr)
         assert arr == sorted(arr) and len(set(arr)) == len(arr)
-    assert go[5] + 1001 <= lib.gsd_geom_buffer_bytes(1001) - 256
+    assert go[5] + 1001 <= lib.gsd_geom_buffer_bytes(1001, 333, 217) - 256
 
 
 def test_struct_layout_matches_c(tmp_path):
