@@ -120,6 +120,7 @@ static unsigned grid_for(long long n) {
 void launch_activate_fwd(const ActivateParams& p, hipStream_t s) {
     if (p.P <= 0) return;
     hipLaunchKernelGGL(k_activate_fwd, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    if (!p.shs_out) return;  // split SH: the rasterizer reads f_dc / f_rest / dsh in place
     const long long n = (long long)p.P * 3 * (1 + p.R);
     hipLaunchKernelGGL(k_pack_sh, dim3(grid_for(n)), dim3(256), 0, s, p.P, p.R, p.f_dc, p.f_rest, p.dsh, p.shs_out);
 }
@@ -127,6 +128,7 @@ void launch_activate_fwd(const ActivateParams& p, hipStream_t s) {
 void launch_activate_bwd(const ActivateBwdParams& p, hipStream_t s) {
     if (p.P <= 0) return;
     hipLaunchKernelGGL(k_activate_bwd, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
+    if (!p.g_shs) return;  // split SH: the rasterizer backward wrote the SH gradients itself
     const long long n = (long long)p.P * 3 * (1 + p.R);
     hipLaunchKernelGGL(k_unpack_sh_bwd, dim3(grid_for(n)), dim3(256), 0, s, p.P, p.R, p.accumulate, p.g_shs, p.g_fdc,
                        p.g_frest, p.g_dsh);

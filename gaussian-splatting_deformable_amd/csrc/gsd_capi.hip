@@ -160,13 +160,17 @@ int validate(const gsd_raster_args* a, bool forward) {
     if (a->P == 0) return GSD_OK;
     if (!a->means3D || (forward && !a->opacities) || !a->viewmatrix || !a->projmatrix || !a->background)
         return fail(GSD_ERR_ARG, "means3D, opacities, viewmatrix, projmatrix and bg are required");
-    if ((a->shs == nullptr) == (a->colors_precomp == nullptr))
+    if (a->shs && a->sh_split) return fail(GSD_ERR_ARG, "shs and sh_split are mutually exclusive");
+    const bool have_sh = a->shs || a->sh_split;
+    if (have_sh == (a->colors_precomp != nullptr))
         return fail(GSD_ERR_ARG, "Please provide excatly one of either SHs or precomputed colors!");
+    if (a->sh_split && (!a->sh_split->dc || (a->M > 1 && !a->sh_split->rest)))
+        return fail(GSD_ERR_ARG, "sh_split needs dc, and rest when M > 1");
     const bool have_sr = a->scales && a->rotations;
     if (have_sr == (a->cov3D_precomp != nullptr) || ((a->scales == nullptr) != (a->rotations == nullptr)))
         return fail(GSD_ERR_ARG,
                     "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
-    if (a->shs) {
+    if (have_sh) {
         if (!a->campos) return fail(GSD_ERR_ARG, "campos is required with SHs");
         const int d = a->D < 0 ? 0 : (a->D > 3 ? 3 : a->D);
         if (a->D < 0) return fail(GSD_ERR_ARG, "sh_degree must be >= 0");
@@ -290,6 +294,9 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     p.focal_x = a->width / (2.0f * a->tan_fovx);
     p.means3D = a->means3D; p.scales = a->scales; p.rotations = a->rotations; p.opacities = a->opacities;
     p.shs = a->shs; p.cov3D_precomp = a->cov3D_precomp; p.colors_precomp = a->colors_precomp;
+    if (const gsd_sh_split* sp = a->sh_split) {
+        p.sh_dc = sp->dc; p.sh_rest = sp->rest; p.sh_off = sp->offset;
+    }
     p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
     p.radii = radii ? radii : g.radii;
     p.means2D = g.means2D; p.depths = g.depths; p.conic_opacity = g.conic_opacity; p.rgb = g.rgb;
@@ -365,7 +372,8 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     if (a->P == 0) return GSD_OK;
     if (!geom_buffer || !image_buffer || (K > 0 && !binning_buffer))
         return fail(GSD_ERR_STATE, "state buffers from the matching forward are required");
-    if (!dL_dout_color || !dL_dmeans2D || !dL_dconic || !dL_dopacity || !dL_dcolors || !dL_dmeans3D || !dL_dcov3D)
+    if (!dL_dout_color || !dL_dmeans2D || !dL_dconic || !dL_dopacity || !dL_dcolors || !dL_dmeans3D ||
+        (a->cov3D_precomp && !dL_dcov3D))
         return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
     if ((a->shs && !dL_dsh) || (a->scales && (!dL_dscales || !dL_drotations)))
         return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
@@ -399,6 +407,11 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     p.dL_dmean2D = dL_dmeans2D; p.dL_dconic = dL_dconic; p.dL_dcolor = dL_dcolors;
     p.dL_dmeans3D = dL_dmeans3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = dL_dsh; p.dL_dscales = dL_dscales;
     p.dL_drotations = dL_drotations;
+    if (const gsd_sh_split* sp = a->sh_split) {
+        p.sh_dc = sp->dc; p.sh_rest = sp->rest; p.sh_off = sp->offset;
+        p.dL_dsh = nullptr; p.dsh_dc = sp->d_dc; p.dsh_rest = sp->d_rest; p.dsh_off = sp->d_offset;
+        p.sh_accumulate = sp->accumulate;
+    }
     timed(kPreBwd, s, [&] { gsd::launch_preprocess_bwd(p, s); });
     GSD_CHECK(a->debug, s);
     return GSD_OK;
@@ -448,8 +461,8 @@ int gsd_activate_forward(int32_t P, int32_t R, const float* xyz, const float* dx
     if (P < 0 || R < 0) return fail(GSD_ERR_ARG, "invalid P / R");
     if (P == 0) return GSD_OK;
     if ((unsigned long long)P * 3ull * (1ull + R) >= (1ull << 32)) return fail(GSD_ERR_ARG, "P too large");
-    if (!xyz || !scaling || !rotation || !opacity || !f_dc || (R > 0 && !f_rest) || !means_out || !scales_out ||
-        !rot_out || !opac_out || !shs_out)
+    if (!xyz || !scaling || !rotation || !opacity || !means_out || !scales_out || !rot_out || !opac_out ||
+        (shs_out && (!f_dc || (R > 0 && !f_rest))))
         return fail(GSD_ERR_ARG, "null pointer argument");
     gsd::ActivateParams p{};
     p.P = P; p.R = R; p.xyz = xyz; p.dxyz = dxyz; p.scaling = scaling; p.dscale = dscale; p.rotation = rotation;
@@ -469,7 +482,7 @@ int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float*
     if (P < 0 || R < 0) return fail(GSD_ERR_ARG, "invalid P / R");
     if (P == 0) return GSD_OK;
     if ((unsigned long long)P * 3ull * (1ull + R) >= (1ull << 32)) return fail(GSD_ERR_ARG, "P too large");
-    if (!scaling || !rotation || !opacity || !g_means || !g_scales || !g_rot || !g_opac || !g_shs)
+    if (!scaling || !rotation || !opacity || !g_means || !g_scales || !g_rot || !g_opac)
         return fail(GSD_ERR_ARG, "null pointer argument");
     gsd::ActivateBwdParams p{};
     p.P = P; p.R = R; p.accumulate = accumulate; p.scaling = scaling; p.dscale = dscale; p.rotation = rotation;

@@ -24,6 +24,9 @@ struct PreprocessParams {
     const float* rotations;
     const float* opacities;
     const float* shs;
+    const float* sh_dc;    // split SH operand (gsd_sh_split), used when shs == nullptr
+    const float* sh_rest;
+    const float* sh_off;
     const float* cov3D_precomp;
     const float* colors_precomp;
     const float* view;
@@ -45,6 +48,9 @@ struct PreprocessBwdParams {
     const float* means3D;
     const int* radii;
     const float* shs;
+    const float* sh_dc;    // split SH operand, used when shs == nullptr
+    const float* sh_rest;
+    const float* sh_off;
     const uint8_t* clamped;
     const float* scales;
     const float* rotations;
@@ -58,6 +64,10 @@ struct PreprocessBwdParams {
     float* dL_dmeans3D;
     float* dL_dcov3D;
     float* dL_dsh;
+    float* dsh_dc;         // split SH sinks (when dL_dsh == nullptr)
+    float* dsh_rest;
+    float* dsh_off;
+    int sh_accumulate;
     float* dL_dscales;
     float* dL_drotations;
 };

@@ -35,22 +35,37 @@ __device__ __forceinline__ float sh_channel(int deg, const float* __restrict__ s
 }
 
 // Stage one Gaussian's active SH coefficients (3*(D+1)^2 floats, <= 48) into
-// registers with the widest aligned loads the (P,M,3) row allows.
+// registers: from its (P,M,3) row, or from the split operand (dc | rest, plus
+// the optional offset -- the same float add as the reference's
+// get_features + mlp_shs, gaussian_renderer/__init__.py:134).
 template <int NC>
-__device__ __forceinline__ void load_sh(const float* __restrict__ row, float (&s)[48]) {
+__device__ __forceinline__ void load_sh(const float* __restrict__ shs, const float* __restrict__ dc,
+                                        const float* __restrict__ rest, const float* __restrict__ off, int M,
+                                        int idx, float (&s)[48]) {
+    if (shs) {
+        const float* row = shs + (size_t)idx * M * 3;
 #pragma unroll
-    for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
+        for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[k] = dc[(size_t)idx * 3 + k];
+    const float* r = rest + (size_t)idx * (M - 1) * 3;
+#pragma unroll
+    for (int k = 3; k < NC * 3; ++k) s[k] = r[k - 3];
+    if (off) {
+        const float* o = off + (size_t)idx * M * 3;
+#pragma unroll
+        for (int k = 0; k < NC * 3; ++k) s[k] = s[k] + o[k];
+    }
 }
 
 template <int DEG>
-__device__ __forceinline__ float3 sh_to_rgb(const float* __restrict__ row, float3 pos, float3 cam,
-                                            uint8_t& clamp_bits) {
+__device__ __forceinline__ float3 sh_to_rgb(const float (&s)[48], float3 pos, float3 cam, uint8_t& clamp_bits) {
     constexpr int deg = DEG;
     float3 d = make_float3(pos.x - cam.x, pos.y - cam.y, pos.z - cam.z);
     const float len = sqrtf(dot3(d, d));
     d = make_float3(d.x / len, d.y / len, d.z / len);
-    float s[48];
-    load_sh<(DEG + 1) * (DEG + 1)>(row, s);
     float3 rgb;
     rgb.x = sh_channel(deg, s + 0, d.x, d.y, d.z);
     rgb.y = sh_channel(deg, s + 1, d.x, d.y, d.z);
@@ -130,7 +145,9 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
         col = make_float4(p.colors_precomp[3 * idx], p.colors_precomp[3 * idx + 1], p.colors_precomp[3 * idx + 2], 0.f);
     } else {
         const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-        const float3 rgb = sh_to_rgb<DEG>(p.shs + (size_t)idx * p.M * 3, mean, cam, cl);
+        float sh[48];
+        load_sh<(DEG + 1) * (DEG + 1)>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, sh);
+        const float3 rgb = sh_to_rgb<DEG>(sh, mean, cam, cl);
         col = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
     }
     p.clamped[idx] = cl;
@@ -309,6 +326,16 @@ __device__ __forceinline__ void cov3d_bwd(const float3 scale, float mod, const f
     drot.w = 2 * r * (D01 - D10) + 2 * x * (D20 + D02) + 2 * y * (D12 + D21) - 4 * z * (D11 + D00);
 }
 
+// dst[k - K0] (+)= ds[k] for k in [K0, K1)
+template <int K0, int K1>
+__device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&ds)[48], bool acc) {
+    float old[K1 - K0 > 0 ? K1 - K0 : 1];
+#pragma unroll
+    for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[k - K0] : 0.f;
+#pragma unroll
+    for (int k = K0; k < K1; ++k) dst[k - K0] = old[k - K0] + ds[k];
+}
+
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -334,8 +361,10 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     Cov6 dcov;
     cov2d_bwd(m, c3, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, Vm, make_float3(dcon4.x, dcon4.y, dcon4.w), dmean,
               dcov);
+    if (p.dL_dcov3D) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = dcov.v[k];
+        for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = dcov.v[k];
+    }
 
     // backward.cu:373-387 projective term from dL/dmean2D
     const float4 mh = xform_point4(m, Pm);
@@ -350,7 +379,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     dm2.z = (P[8] * mw - P[11] * mul1) * d2x + (P[9] * mw - P[11] * mul2) * d2y;
     dmean = make_float3(dmean.x + dm2.x, dmean.y + dm2.y, dmean.z + dm2.z);
 
-    if (p.shs) {
+    if (p.shs || p.sh_dc) {
         const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         const float3 dir_orig = make_float3(m.x - cam.x, m.y - cam.y, m.z - cam.z);
         const float len = sqrtf(dot3(dir_orig, dir_orig));
@@ -359,18 +388,25 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         const float3 dc = make_float3(p.dL_dcolor[3 * idx] * ((cl & 1) ? 0 : 1),
                                       p.dL_dcolor[3 * idx + 1] * ((cl & 2) ? 0 : 1),
                                       p.dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0 : 1));
-        const float* row = p.shs + (size_t)idx * p.M * 3;
-        float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
         constexpr int nc = (DEG + 1) * (DEG + 1);
         float s[48];
-#pragma unroll
-        for (int k = 0; k < nc * 3; ++k) s[k] = row[k];
+        load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s);
         float ds[48];
         const float3 gx = sh_channel_bwd(DEG, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
         const float3 gy = sh_channel_bwd(DEG, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
         const float3 gz = sh_channel_bwd(DEG, s + 2, dc.z, dir.x, dir.y, dir.z, ds + 2);
+        if (p.dL_dsh) {
+            float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
 #pragma unroll
-        for (int k = 0; k < nc * 3; ++k) drow[k] = ds[k];
+            for (int k = 0; k < nc * 3; ++k) drow[k] = ds[k];
+        } else {  // split sinks: dSH/d dc = dSH/d rest = dSH/d offset = identity
+            // accumulate: every old value is loaded before the first store, so the loads issue together
+            // instead of each waiting behind a store it might alias
+            const bool acc = p.sh_accumulate != 0;
+            if (p.dsh_dc) sink_sh<0, 3>(p.dsh_dc + (size_t)idx * 3, ds, acc);
+            if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + (size_t)idx * (p.M - 1) * 3, ds, acc);
+            if (p.dsh_off) sink_sh<0, nc * 3>(p.dsh_off + (size_t)idx * p.M * 3, ds, acc);
+        }
         // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
         const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
                                         gx.z * dc.x + gy.z * dc.y + gz.z * dc.z);

@@ -47,16 +47,18 @@ __device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
 
 // Per-wave compaction of the batch: s_list receives, in increasing slot order,
 // the slots whose alpha box meets [qx0, qx0+7] x [qy0, qy0+7].  Returns the count.
+// Slots below t_min are skipped too (the backward's last-contributor bound).
+template <int RW = 8, int RH = 8>
 __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, uint8_t* __restrict__ s_list, int n,
-                                            float qx0, float qy0, int lane) {
+                                            float qx0, float qy0, int lane, int t_min = 0) {
     int m = 0;
 #pragma unroll
     for (int k = 0; k < kTilePix / 64; ++k) {
         const int t = k * 64 + lane;
         bool hit = false;
-        if (t < n) {
+        if (t < n && t >= t_min) {
             const float4 bx = s_box[t];
-            hit = bx.y >= qx0 && bx.x <= qx0 + 7.0f && bx.w >= qy0 && bx.z <= qy0 + 7.0f;
+            hit = bx.y >= qx0 && bx.x <= qx0 + (float)(RW - 1) && bx.w >= qy0 && bx.z <= qy0 + (float)(RH - 1);
         }
         const unsigned long long mask = __ballot(hit);
         if (hit) {
@@ -203,10 +205,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
     const int lane = tg.lane;
+    __shared__ int s_tile_lc;
     const uint2 rg = p.ranges[tg.tile];
-    const int total = (int)(rg.y - rg.x);
-    const int rounds = (total + kTilePix - 1) / kTilePix;
-    int toDo = total;
     const int pid = p.W * tg.py + tg.px;
     const int plane = p.H * p.W;
     const bool inside = tg.inside;
@@ -214,15 +214,26 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     const float T_final = inside ? p.final_T[pid] : 0.f;
     float T = T_final;
     const int last_contributor = inside ? (int)p.n_contrib[pid] : 0;
+    // Every pixel skips list positions >= its last contributor (backward.cu:487-488), so the replay starts
+    // at the tile's largest last contributor, and each wave compacts away positions beyond its own.
+    int wave_lc = last_contributor;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wave_lc = max(wave_lc, __shfl_xor(wave_lc, off));
+    if (tid == 0) s_tile_lc = 0;
+    __syncthreads();
+    if (lane == 0) atomicMax(&s_tile_lc, wave_lc);
+    __syncthreads();
+    const int total = min((int)(rg.y - rg.x), s_tile_lc);
+    const uint32_t end = rg.x + (uint32_t)total;
+    const int rounds = (total + kTilePix - 1) / kTilePix;
+    int toDo = total;
     float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
     if (inside) {
         dpix0 = p.dL_dpix[pid];
         dpix1 = p.dL_dpix[plane + pid];
         dpix2 = p.dL_dpix[2 * plane + pid];
     }
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;  // accum_rec
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;     // last_color
-    float last_alpha = 0.f;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;  // accum_rec (with last_color / last_alpha folded in)
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
@@ -231,8 +242,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         __syncthreads();
         const int progress = i * kTilePix + tid;
-        if ((int)rg.x + progress < (int)rg.y) {  // loaded back to front (backward.cu:466-478)
-            const uint32_t g = p.point_list[rg.y - progress - 1];
+        if (progress < total) {  // loaded back to front (backward.cu:466-478)
+            const uint32_t g = p.point_list[end - progress - 1];
             const float2 xy = p.means2D[g];
             const float4 co = p.conic_opacity[g];
             s_id[tid] = g;
@@ -245,9 +256,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
+#ifdef GSD_EXP_NOCOMPUTE
+        const int m = 0 * wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
+#else
+        const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
+#endif
         for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
             // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
             float Gs[kBwdBatch], As[kBwdBatch];
@@ -257,20 +272,23 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 slot[u] = list[min(j0 + u, m - 1)];
                 As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u]);
             }
-            // ... then the sequential back-to-front recurrence (backward.cu:482-555)
+            // ... then the sequential back-to-front recurrence (backward.cu:482-555), branch-free: a record
+            // a lane skips (past its last contributor, alpha < 1/255, or beyond the list) gets alpha = G = 0,
+            // which leaves T unchanged (1/(1-0) == 1 exactly) and zeroes its partials.  accum_rec is folded
+            // forward at the end of each record (acc = alpha c + (1-alpha) acc) rather than at the start of
+            // the next contributing one (backward.cu:516-520): the same operations on the same values, and a
+            // skipped record (alpha = 0) leaves it unchanged without a select.
             float v[9][kBwdBatch];
             bool any = false;
 #pragma unroll
             for (int u = 0; u < kBwdBatch; ++u) {
                 // gradient arithmetic has no bit-exact contract: let the compiler fuse to FMA
 #pragma clang fp contract(fast)
-#pragma unroll
-                for (int q = 0; q < 9; ++q) v[q][u] = 0.f;
-                const float alpha = As[u];
-                if (!inside || j0 + u >= m || front_base - slot[u] >= last_contributor || alpha < 1.0f / 255.0f)
-                    continue;
-                any = true;
-                const float G = Gs[u];
+                const bool valid = inside && j0 + u < m && front_base - slot[u] < last_contributor &&
+                                   As[u] >= 1.0f / 255.0f;
+                any |= valid;
+                const float alpha = valid ? As[u] : 0.f;
+                const float G = valid ? Gs[u] : 0.f;
                 const float2 xy = s_xy[slot[u]];
                 const float dx = xy.x - pxf, dy = xy.y - pyf;
                 const float4 co = s_co[slot[u]];
@@ -278,12 +296,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 T = T * inv1ma;  // backward.cu:503 (T recovered by division)
                 const float dchannel_dcolor = alpha * T;
                 const float4 c = s_rgb[slot[u]];
-                acc0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-                acc1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-                acc2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-                lc0 = c.x;
-                lc1 = c.y;
-                lc2 = c.z;
                 float dL_dalpha = (c.x - acc0) * dpix0;
                 dL_dalpha += (c.y - acc1) * dpix1;
                 dL_dalpha += (c.z - acc2) * dpix2;
@@ -291,7 +303,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 v[7][u] = dchannel_dcolor * dpix1;
                 v[8][u] = dchannel_dcolor * dpix2;
                 dL_dalpha *= T;
-                last_alpha = alpha;
                 dL_dalpha += (-T_final * inv1ma) * bg_dot;
                 const float dL_dG = co.w * dL_dalpha;
                 const float gdx = G * dx, gdy = G * dy;
@@ -303,15 +314,25 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 v[3][u] = -0.5f * gdx * dy * dL_dG;
                 v[4][u] = -0.5f * gdy * dy * dL_dG;
                 v[5][u] = G * dL_dalpha;
+                acc0 = alpha * c.x + (1.f - alpha) * acc0;
+                acc1 = alpha * c.y + (1.f - alpha) * acc1;
+                acc2 = alpha * c.z + (1.f - alpha) * acc2;
             }
             if (__ballot(any)) {  // wave-uniform
-                const int col = lane >> 4;
-                const bool writer = (lane & 15) == 0 && j0 + col < m;
-                const int dst = list[min(j0 + col, m - 1)];
+                // all nine reductions first (independent: their DPP chains interleave), then one masked store
+                float r[9];
 #pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    const float r = wave_sum4(v[q]);
-                    if (writer) atomicAdd(&s_acc[q][dst], r);
+                for (int q = 0; q < 9; ++q)
+#ifdef GSD_EXP_NORED
+                    r[q] = v[q][0] + v[q][1] + v[q][2] + v[q][3];
+#else
+                    r[q] = wave_sum4(v[q]);
+#endif
+                const int col = lane >> 4;
+                if ((lane & 15) == 0 && j0 + col < m) {
+                    const int dst = list[j0 + col];
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) atomicAdd(&s_acc[q][dst], r[q]);
                 }
             }
         }
@@ -321,6 +342,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float a0 = s_acc[0][tid], a1 = s_acc[1][tid], a2 = s_acc[2][tid], a3 = s_acc[3][tid],
                         a4 = s_acc[4][tid], a5 = s_acc[5][tid], a6 = s_acc[6][tid], a7 = s_acc[7][tid],
                         a8 = s_acc[8][tid];
+#ifdef GSD_EXP_NOATOMIC
+#define atomicAdd(ptr, v) (*(ptr) = (v))
+#endif
             if (a0 != 0.f) atomicAdd(p.dL_dmean2D + 3 * g, a0);
             if (a1 != 0.f) atomicAdd(p.dL_dmean2D + 3 * g + 1, a1);
             if (a2 != 0.f) atomicAdd(p.dL_dconic + 4 * g, a2);
@@ -330,6 +354,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             if (a6 != 0.f) atomicAdd(p.dL_dcolors + 3 * g, a6);
             if (a7 != 0.f) atomicAdd(p.dL_dcolors + 3 * g + 1, a7);
             if (a8 != 0.f) atomicAdd(p.dL_dcolors + 3 * g + 2, a8);
+#ifdef GSD_EXP_NOATOMIC
+#undef atomicAdd
+#endif
         }
     }
 }

@@ -42,12 +42,32 @@ def _ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
 
+class ShSplit:
+    """The split SH operand (gsd_sh_split): features_dc (P,1,3), features_rest (P,R,3) and an optional
+    additive offset (P,1+R,3) read in place instead of shs = cat(dc, rest) + offset; for the backward,
+    the gradient sinks (any may be None) and whether they are added into (accumulate) or stored."""
+
+    def __init__(self, dc, rest, offset=None, d_dc=None, d_rest=None, d_offset=None, accumulate=False):
+        dev = dc.device
+        self.dc = _dev_f32(dc, "features_dc", dev)
+        self.rest = _dev_f32(rest, "features_rest", dev)
+        self.offset = None if offset is None else _dev_f32(offset, "sh offset", dev)
+        self.sinks = [None if t is None else t for t in (d_dc, d_rest, d_offset)]
+        for t in self.sinks:
+            if t is not None and (not t.is_contiguous() or t.dtype != torch.float32 or t.device != dev):
+                raise RuntimeError("sh_split gradient sinks must be contiguous float32 on the same device")
+        self.M = 1 + int(self.rest.size(1))
+        self.c = _native.ShSplit(dc=_ptr(self.dc).value, rest=_ptr(self.rest).value, offset=_ptr(self.offset).value,
+                                 d_dc=_ptr(self.sinks[0]).value, d_rest=_ptr(self.sinks[1]).value,
+                                 d_offset=_ptr(self.sinks[2]).value, accumulate=int(bool(accumulate)))
+
+
 class _Args:
     """Holds the contiguous device tensors alive for the duration of one native call."""
 
     def __init__(self, background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                  viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                 prefiltered, debug):
+                 prefiltered, debug, sh_split=None):
         dev = means3D.device
         if dev.type != "cuda":
             raise RuntimeError("means3D must be a HIP device tensor: this rasterizer has no CPU implementation")
@@ -65,6 +85,9 @@ class _Args:
         self.proj = _dev_f32(projmatrix, "projmatrix", dev)
         self.campos = _dev_f32(campos, "campos", dev)
         self.M = 0 if self.sh is None else int(self.sh.size(1))  # rasterize_points.cu:83-87
+        self.sh_split = sh_split
+        if sh_split is not None:
+            self.M = sh_split.M
         self.H, self.W = int(image_height), int(image_width)
         self.c = _native.RasterArgs(
             P=self.P, D=int(degree), M=self.M, width=self.W, height=self.H,
@@ -74,19 +97,22 @@ class _Args:
             colors_precomp=_ptr(self.colors).value, opacities=_ptr(self.opacity).value,
             scales=_ptr(self.scales).value, rotations=_ptr(self.rotations).value,
             cov3D_precomp=_ptr(self.cov3D).value, viewmatrix=_ptr(self.view).value,
-            projmatrix=_ptr(self.proj).value, campos=_ptr(self.campos).value)
+            projmatrix=_ptr(self.proj).value, campos=_ptr(self.campos).value,
+            sh_split=None if sh_split is None else ctypes.addressof(sh_split.c))
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug):
+                        prefiltered, debug, sh_split=None):
     """RasterizeGaussiansCUDA (rasterize_points.cu:35-115):
-    -> (num_rendered, color (3,H,W), radii (P,) int32, geomBuffer, binningBuffer, imgBuffer)."""
+    -> (num_rendered, color (3,H,W), radii (P,) int32, geomBuffer, binningBuffer, imgBuffer).
+    ``sh_split`` (a ShSplit, with ``sh`` empty) is this library's extension for the fused render path."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     lib = _native.load()
     a = _Args(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
-              projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug)
+              projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
+              sh_split)
     dev, P, H, W = a.dev, a.P, a.H, a.W
     radii = torch.zeros(P, dtype=torch.int32, device=dev)
     byte = dict(dtype=torch.uint8, device=dev)
@@ -111,24 +137,29 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
-                                 campos, geomBuffer, R, binningBuffer, imageBuffer, debug):
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer, debug, sh_split=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196):
-    -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)."""
+    -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
+    With ``sh_split`` the SH gradients go to its sinks and dL_dsh is None; so is dL_dcov3D when no
+    cov3D_precomp was given (the scales/rotations gradients are what such a caller uses)."""
     lib = _native.load()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))  # rasterize_points.cu:142-143
     a = _Args(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
-              projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug)
+              projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug, sh_split)
     dev, P, M = a.dev, a.P, a.M
+    split = sh_split is not None
+    want_cov = not split or a.cov3D is not None
     # one zero-filled slab for every gradient (a single memset instead of nine);
     # the float4-accessed arrays (conic, rotation) first so they stay 16-B aligned
-    widths = [4, 4, 3, 3, 1, 3, 6, M * 3, 3]
+    widths = [4, 4, 3, 3, 1, 3, 6 if want_cov else 0, 0 if split else M * 3, 3]
     slab = torch.zeros(P * sum(widths), dtype=torch.float32, device=dev)
     views, off = [], 0
     for w in widths:
-        views.append(slab[off:off + P * w].view(P, w))
+        views.append(slab[off:off + P * w].view(P, w) if w else None)
         off += P * w
     dconic, drot, dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales = views
-    dsh = dsh.view(P, M, 3)
+    if dsh is not None:
+        dsh = dsh.view(P, M, 3)
     if P != 0:
         dout = _dev_f32(dL_dout_color, "dL_dout_color", dev)
         radii_c = radii.contiguous()
@@ -197,19 +228,22 @@ def _opt_f32(t, name, dev):
 
 
 def activate_forward(xyz, scaling, rotation, opacity, f_dc, f_rest, dxyz=None, dscale=None, drot=None, dsh=None):
-    """Fused render() preamble (gsd_activate_forward) -> (means3D, scales, rotations, opacities, shs)."""
+    """Fused render() preamble (gsd_activate_forward) -> (means3D, scales, rotations, opacities, shs).
+    With f_dc = f_rest = None the SH are left split (shs is None; see ShSplit)."""
     lib = _native.load()
     dev = xyz.device
     P = int(xyz.size(0))
-    R = int(f_rest.size(1)) if f_rest.dim() == 3 else int(f_rest.numel() // max(P * 3, 1))
-    ins = [_dev_f32(t, n, dev) for t, n in ((xyz, "xyz"), (scaling, "scaling"), (rotation, "rotation"),
+    split = f_dc is None
+    R = 0 if split else (int(f_rest.size(1)) if f_rest.dim() == 3 else int(f_rest.numel() // max(P * 3, 1)))
+    ins = [_opt_f32(t, n, dev) for t, n in ((xyz, "xyz"), (scaling, "scaling"), (rotation, "rotation"),
                                            (opacity, "opacity"), (f_dc, "f_dc"), (f_rest, "f_rest"))]
-    offs = [_opt_f32(t, n, dev) for t, n in ((dxyz, "dxyz"), (dscale, "dscale"), (drot, "drot"), (dsh, "dsh"))]
+    offs = [_opt_f32(t, n, dev) for t, n in ((dxyz, "dxyz"), (dscale, "dscale"), (drot, "drot"),
+                                            (None if split else dsh, "dsh"))]
     means = torch.empty(P, 3, device=dev)
     scales = torch.empty(P, 3, device=dev)
     rots = torch.empty(P, 4, device=dev)
     opac = torch.empty(P, 1, device=dev)
-    shs = torch.empty(P, 1 + R, 3, device=dev)
+    shs = None if split else torch.empty(P, 1 + R, 3, device=dev)
     x, s, q, o, fdc, frest = ins
     dx, ds, dq, dsh_ = offs
     with torch.cuda.device(dev):
@@ -221,29 +255,32 @@ def activate_forward(xyz, scaling, rotation, opacity, f_dc, f_rest, dxyz=None, d
 
 def activate_backward(scaling, rotation, opacity, dscale, drot, g_means, g_scales, g_rot, g_opac, g_shs, sinks,
                       has_off, rest_shape):
-    """Backward of activate_forward.  sinks: None, or the 6 parameter .grad buffers to add into in place.
+    """Backward of activate_forward.  sinks: None, or the parameter .grad buffers to add into in place
+    (6, or 4 when the SH were left split: rest_shape None).
     -> ((g_xyz, g_scaling, g_rotation, g_opacity, g_fdc, g_frest), (g_dxyz, g_dscale, g_drot, g_dsh))."""
     lib = _native.load()
     dev = scaling.device
     P = int(scaling.size(0))
-    R = int(rest_shape[1])
+    split = rest_shape is None
+    R = 0 if split else int(rest_shape[1])
     z = lambda t, shape: torch.zeros(shape, device=dev) if t is None else t  # noqa: E731  (unused grads)
     gm = _dev_f32(z(g_means, (P, 3)), "g_means", dev)
     gs = _dev_f32(z(g_scales, (P, 3)), "g_scales", dev)
     gr = _dev_f32(z(g_rot, (P, 4)), "g_rot", dev)
     go = _dev_f32(z(g_opac, (P, 1)), "g_opac", dev)
-    gsh = _dev_f32(z(g_shs, (P, 1 + R, 3)), "g_shs", dev)
+    gsh = None if split else _dev_f32(z(g_shs, (P, 1 + R, 3)), "g_shs", dev)
     if sinks is None:
         outs = [torch.empty(P, 3, device=dev), torch.empty(P, 3, device=dev), torch.empty(P, 4, device=dev),
-                torch.empty(P, 1, device=dev), torch.empty(P, 1, 3, device=dev), torch.empty(rest_shape, device=dev)]
+                torch.empty(P, 1, device=dev)]
+        outs += [None, None] if split else [torch.empty(P, 1, 3, device=dev), torch.empty(rest_shape, device=dev)]
         acc = 0
     else:
-        outs = list(sinks)
+        outs = list(sinks) + ([None, None] if split else [])
         acc = 1
     offg = [torch.empty(P, 3, device=dev) if has_off[0] else None,
             torch.empty(P, 3, device=dev) if has_off[1] else None,
             torch.empty(P, 4, device=dev) if has_off[2] else None,
-            torch.empty(P, 1 + R, 3, device=dev) if has_off[3] else None]
+            torch.empty(P, 1 + R, 3, device=dev) if (has_off[3] and not split) else None]
     with torch.cuda.device(dev):
         _native.check(lib.gsd_activate_backward(
             P, R, acc, _ptr(scaling.contiguous()), _ptr(None if dscale is None else dscale.contiguous()),

@@ -11,13 +11,20 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
 _sz = ctypes.c_size_t
+
+
+class ShSplit(ctypes.Structure):
+    """Mirror of ``gsd_sh_split`` (include/gsd_raster.h)."""
+
+    _fields_ = [("dc", _vp), ("rest", _vp), ("offset", _vp), ("d_dc", _vp), ("d_rest", _vp), ("d_offset", _vp),
+                ("accumulate", _i32)]
 
 
 class RasterArgs(ctypes.Structure):
@@ -29,7 +36,7 @@ class RasterArgs(ctypes.Structure):
         ("prefiltered", _i32), ("debug", _i32),
         ("background", _vp), ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp),
         ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp), ("projmatrix", _vp),
-        ("campos", _vp),
+        ("campos", _vp), ("sh_split", _vp),
     ]
 
 

@@ -82,6 +82,59 @@ class _RasterizeGaussians(torch.autograd.Function):
                      for i, g in enumerate(grads))
 
 
+def rasterize_gaussians_split_sh(means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations,
+                                 raster_settings):
+    """The fused render() path's rasterizer call (no reference counterpart: the reference builds
+    shs = cat(f_dc, f_rest) + sh_offset in torch first, gaussian_renderer/__init__.py:129-134).  The SH
+    pieces are read in place, and their gradients are written by the rasterizer backward -- added
+    straight into ``.grad`` for parameters registered with FlatGrads.  -> (color, radii)."""
+    return _RasterizeSplitSH.apply(means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations,
+                                   raster_settings)
+
+
+class _RasterizeSplitSH(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations, raster_settings):
+        rs = raster_settings
+        split = _C.ShSplit(f_dc, f_rest, sh_offset)
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(
+            rs.bg, means3D, None, opacities, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
+            rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, None, rs.sh_degree, rs.campos, rs.prefiltered,
+            rs.debug, sh_split=split)
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        ctx.has_offset = sh_offset is not None
+        ctx.params = (f_dc, f_rest)
+        ctx.save_for_backward(means3D, scales, rotations, radii, f_dc, f_rest,
+                              sh_offset if sh_offset is not None else torch.empty(0), geomBuffer, binningBuffer,
+                              imgBuffer)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _):
+        from .activate import _sinks
+        rs = ctx.raster_settings
+        means3D, scales, rotations, radii, f_dc, f_rest, sh_offset, geomBuffer, binningBuffer, imgBuffer = \
+            ctx.saved_tensors
+        sinks = _sinks(ctx.params)
+        if sinks is not None:
+            d_dc, d_rest = sinks
+        else:
+            d_dc, d_rest = torch.zeros_like(f_dc), torch.zeros_like(f_rest)
+        offset = sh_offset if ctx.has_offset else None
+        d_off = None
+        if ctx.has_offset:
+            d_off = torch.zeros(f_dc.size(0), 1 + f_rest.size(1), 3, device=f_dc.device)
+        split = _C.ShSplit(f_dc, f_rest, offset, d_dc, d_rest, d_off, accumulate=sinks is not None)
+        g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
+            rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
+            rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
+            binningBuffer, imgBuffer, rs.debug, sh_split=split)
+        if sinks is not None:
+            d_dc = d_rest = None
+        return g_m3d, g_m2d, d_dc, d_rest, d_off, g_op, g_sc, g_rot, None
+
+
 class GaussianRasterizationSettings(NamedTuple):
     image_height: int
     image_width: int

@@ -17,9 +17,9 @@ from types import SimpleNamespace
 import torch
 import torch.nn.functional as F
 
-from .activate import activate
+from .activate import activate_split_sh
 from .deform import se3_deform
-from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_split_sh
 from .sh import eval_sh
 
 
@@ -184,13 +184,13 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
     python_modes = (getattr(pipe, "compute_cov3D_python", False) or getattr(pipe, "convert_SHs_python", False)
                     or override_color is not None)
     if not python_modes and hasattr(pc, "_features_rest") and getattr(pc, "fused_preamble", True):
-        # fused preamble: offsets + activations + SH concat in one HIP pass (gsd_amd.activate)
+        # fused preamble: offsets + activations in one HIP pass (gsd_amd.activate); the SH are not
+        # concatenated -- the rasterizer reads features_dc / features_rest / the SH offset in place
         P = means3D.size(0)
         dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, time, iteration)
         dsh = None if mlp_shs is None else mlp_shs.reshape(P, -1, 3)
-        means3D, scales, rotations, opacity, shs = activate(pc._xyz, pc._scaling, pc._rotation, pc._opacity,
-                                                            pc._features_dc, pc._features_rest, dx, scale_offset,
-                                                            rot_offset, dsh)
+        means3D, scales, rotations, opacity = activate_split_sh(pc._xyz, pc._scaling, pc._rotation, pc._opacity, dx,
+                                                                scale_offset, rot_offset)
         if getattr(pc, "deform", "additive") == "se3":
             # one fused kernel moves means AND rotations by the same rigid motion
             means3D, rotations = se3_deform(pc.get_twist(pc.get_xyz, time, iteration), means3D, rotations)
@@ -198,8 +198,8 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
         moved = dx is not None or getattr(pc, "deform", "additive") == "se3"
         means3D_offset = means3D - means3D_ori if moved else torch.zeros_like(means3D_ori)
         rot_offset = rot_offset if rot_offset is not None else means3D.new_zeros(P, 4)
-        rendered_image, radii = rasterizer(means3D=means3D, means2D=means2D, shs=shs, opacities=opacity,
-                                           scales=scales, rotations=rotations)
+        rendered_image, radii = rasterize_gaussians_split_sh(means3D, means2D, pc._features_dc, pc._features_rest,
+                                                             dsh, opacity, scales, rotations, raster_settings)
         return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
                 "radii": radii, "means3D": means3D, "means3D_ori": means3D_ori, "rotations": rotations,
                 "means3D_offset": means3D_offset, "opacities": opacity, "rot_offset": rot_offset}

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 2
+#define GSD_ABI_VERSION 3
 
 enum {
     GSD_OK = 0,
@@ -51,6 +51,25 @@ enum {
     GSD_ERR_HIP = 2,     /* HIP runtime error (CHECK_CUDA upstream, auxiliary.h:166-173) */
     GSD_ERR_STATE = 3    /* inconsistent state buffers (wrong size / wrong call order) */
 };
+
+/* Split SH operand (optional, ABI 3).  The reference's render() materialises
+ * shs = cat(features_dc, features_rest) + dSH (gaussian_renderer/__init__.py:129-134,
+ * scene/gaussian_model.py:647-650) before calling the rasterizer.  A caller that
+ * sets gsd_raster_args.sh_split instead hands over the pieces: the rasterizer
+ * reads them in place (dc + offset is the same float add torch does) and the
+ * backward writes dL/dSH straight into the pieces' gradient buffers.  With
+ * sh_split set, args.shs must be NULL and args.M = 1 + rest coefficients. */
+typedef struct gsd_sh_split {
+    const float* dc;       /* (P,1,3) */
+    const float* rest;     /* (P,M-1,3); may be NULL when M == 1 */
+    const float* offset;   /* (P,M,3) additive SH offset, or NULL */
+    float* d_dc;           /* backward sink dL/d dc (P,1,3), or NULL */
+    float* d_rest;         /* backward sink dL/d rest (P,M-1,3), or NULL */
+    float* d_offset;       /* backward sink dL/d offset (P,M,3), or NULL */
+    int32_t accumulate;    /* backward: 1 = add into the sinks, 0 = store.  Entries of Gaussians with
+                              radii == 0 and of coefficients above the active degree are not touched
+                              (zero-fill the sinks first when storing, as for every backward output). */
+} gsd_sh_split;
 
 /* Raster settings + per-Gaussian inputs of one view.  Mirrors the 19 arguments
  * of _C.rasterize_gaussians (rasterize_points.cu:36-55).  Absent optional
@@ -75,6 +94,7 @@ typedef struct gsd_raster_args {
     const float* viewmatrix;    /* (4,4), column-major as stored by scene/cameras.py:55 */
     const float* projmatrix;    /* (4,4) full projection, scene/cameras.py:57 */
     const float* campos;        /* (3) */
+    const gsd_sh_split* sh_split; /* NULL, or the split SH operand above (then shs == NULL) */
 } gsd_raster_args;
 
 int gsd_abi_version(void);
@@ -112,7 +132,9 @@ int gsd_rasterize_forward_render(const gsd_raster_args* args, void* geom_buffer,
  * by the caller (torch::zeros upstream, rasterize_points.cu:151-159):
  * dL_dmeans2D (P,3), dL_dcolors (P,3), dL_dopacity (P,1), dL_dmeans3D (P,3),
  * dL_dcov3D (P,6), dL_dsh (P,M,3) (may be NULL if M == 0), dL_dscales (P,3),
- * dL_drotations (P,4), and the scratch dL_dconic (P,4) (float4 view of (P,2,2)). */
+ * dL_drotations (P,4), and the scratch dL_dconic (P,4) (float4 view of (P,2,2)).
+ * With args->sh_split set, dL_dsh is not used (the split sinks receive dL/dSH);
+ * dL_dcov3D may be NULL when cov3D_precomp is NULL (it is then not written). */
 int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, const void* geom_buffer,
                            const void* binning_buffer, const void* image_buffer, int64_t num_rendered,
                            const float* dL_dout_color, float* dL_dmeans2D, float* dL_dconic,
@@ -142,14 +164,16 @@ int gsd_se3_deform_backward(int32_t P, const float* twist, const float* means_in
 /* Fused render() preamble (gaussian_renderer/__init__.py:79-140, gaussian_model.py:761-797):
  *   means = xyz + dxyz, scales = exp(scaling + dscale), rotations = normalize(rotation + drot),
  *   opacities = sigmoid(opacity), shs = cat(f_dc, f_rest) + dsh.
- * Offsets (dxyz (P,3), dscale (P,3), drot (P,4), dsh (P,1+R,3)) may be NULL = zero; f_rest is (P,R,3). */
+ * Offsets (dxyz (P,3), dscale (P,3), drot (P,4), dsh (P,1+R,3)) may be NULL = zero; f_rest is (P,R,3).
+ * shs_out may be NULL: the SH stay split and go to the rasterizer as a gsd_sh_split. */
 int gsd_activate_forward(int32_t P, int32_t R, const float* xyz, const float* dxyz, const float* scaling,
                          const float* dscale, const float* rotation, const float* drot, const float* opacity,
                          const float* f_dc, const float* f_rest, const float* dsh, float* means_out,
                          float* scales_out, float* rot_out, float* opac_out, float* shs_out, void* stream);
 
 /* Backward of gsd_activate_forward.  Parameter gradients (g_xyz .. g_frest) are written, or added into the
- * existing values when accumulate != 0; offset gradients (g_dxyz .. g_dsh) are written.  Any output may be NULL. */
+ * existing values when accumulate != 0; offset gradients (g_dxyz .. g_dsh) are written.  Any output may be NULL.
+ * g_shs may be NULL (split SH: the SH gradients were written by gsd_rasterize_backward). */
 int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float* scaling, const float* dscale,
                           const float* rotation, const float* drot, const float* opacity, const float* g_means,
                           const float* g_scales, const float* g_rot, const float* g_opac, const float* g_shs,

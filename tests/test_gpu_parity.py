@@ -269,21 +269,45 @@ def test_fused_activation_matches_torch(with_offsets):
         assert rel_l2((t.grad - 1).cpu(), w.cpu()) <= 1e-5
 
 
-def test_fused_preamble_render_matches_reference_path():
-    """render(): fused HIP preamble vs the reference-literal torch preamble, same image and parameter grads."""
+class _FixedOffsets:
+    """A deformation producer with fixed non-zero offsets (dx, dscale, drot, dSH), all differentiable."""
+
+    def __init__(self, P, seed):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        mk = lambda *shape: (torch.randn(*shape, generator=g) * 0.02).to(DEV).requires_grad_(True)  # noqa: E731
+        self.t = [mk(P, 3), mk(P, 3), mk(P, 4), mk(P, 48)]
+
+    def __call__(self, pts, time, iteration):
+        return tuple(self.t)
+
+
+@pytest.mark.parametrize("offsets", [False, True])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_fused_preamble_render_matches_reference_path(offsets, inplace):
+    """render(): fused HIP preamble + split-SH rasterizer vs the reference-literal torch preamble: same image,
+    parameter grads and offset grads, with plain autograd .grad or in-place FlatGrads accumulation."""
     from gsd_amd import DeformableGaussians, default_pipe, render
     from gsd_amd.camera import synthetic_camera
+    from gsd_amd.parallel import FlatGrads
     from gsd_amd.scene import make_gaussians
-    params = make_gaussians(20_000, 320, 240, seed=9, device=DEV)
+    P = 20_000
+    params = make_gaussians(P, 320, 240, seed=9, device=DEV)
     cam = synthetic_camera(320, 240).to(DEV)
     res = []
     for fused in (True, False):
-        pc = DeformableGaussians(params, sh_degree=3)
+        offs = _FixedOffsets(P, seed=3) if offsets else None
+        pc = DeformableGaussians(params, sh_degree=3, offset_model=offs)
         pc.fused_preamble = fused
-        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
-        (out["render"] * torch.linspace(0, 1, 320, device=DEV)).sum().backward()
-        res.append((out["render"].detach(), [p.grad.clone() for p in pc.parameters()]))
+        flat = FlatGrads(pc.parameters()) if inplace else None
+        for _ in range(2 if inplace else 1):  # twice: the in-place path must accumulate, not overwrite
+            out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+            (out["render"] * torch.linspace(0, 1, 320, device=DEV)).sum().backward()
+        if flat is not None:
+            flat.collect()
+        grads = [p.grad.clone() for p in pc.parameters()] + ([t.grad.clone() for t in offs.t] if offsets else [])
+        res.append((out["render"].detach(), grads))
     assert (res[0][0] - res[1][0]).abs().max() <= 1e-5
+    assert len(res[0][1]) == len(res[1][1])
     for a, b in zip(res[0][1], res[1][1]):
         assert rel_l2(a.cpu(), b.cpu()) <= 1e-4
 
