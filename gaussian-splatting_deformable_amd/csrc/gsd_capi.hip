@@ -7,6 +7,7 @@
 // caller's stream, so one process per GPU can run views back to back.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -184,11 +185,11 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kAdam, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
-                                               "activate_bwd"};
+                                               "activate_bwd",   "l1_ssim",      "adam"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -492,6 +493,88 @@ int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float*
     p.g_drot = g_drot; p.g_dsh = g_dsh;
     hipStream_t s = as_stream(stream);
     timed(kActBwd, s, [&] { gsd::launch_activate_bwd(p, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+// ---- training loss (gsd_loss.hip) ----
+namespace {
+struct LossWs {
+    float* gmaps;    // 3 x (C,H,W)
+    float* partial;  // 2 per workgroup
+    float* out3;     // unused slot (callers pass their own out3)
+};
+size_t carve_loss(void* base, int C, int H, int W, LossWs* w) {
+    char* p = base ? align_ptr(base) : nullptr;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* r = p ? p + off : nullptr;
+        off += up(bytes);
+        return r;
+    };
+    int tx, ty;
+    gsd::ssim_tiles(H, W, &tx, &ty);
+    LossWs v;
+    v.gmaps = reinterpret_cast<float*>(take((size_t)3 * C * H * W * sizeof(float)));
+    v.partial = reinterpret_cast<float*>(take((size_t)2 * C * tx * ty * sizeof(float)));
+    v.out3 = nullptr;
+    if (w) *w = v;
+    return off + kAlign;
+}
+}  // namespace
+
+size_t gsd_l1_ssim_workspace_bytes(int32_t C, int32_t H, int32_t W) {
+    if (C <= 0 || H <= 0 || W <= 0) return kAlign;
+    return carve_loss(nullptr, C, H, W, nullptr);
+}
+
+int gsd_l1_ssim(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim, float* out3,
+                float* dL_dimg, void* workspace, void* stream) {
+    if (C <= 0 || H <= 0 || W <= 0) return fail(GSD_ERR_ARG, "image must be (C,H,W) with positive sizes");
+    if (!img || !gt || !out3 || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
+    if ((size_t)C * H * W >= (1ull << 31)) return fail(GSD_ERR_ARG, "image too large");
+    // utils/loss_utils.py:23-25: gaussian(11, 1.5), float32 exp values normalised by their float32 sum
+    float w[11], sum = 0.f;
+    for (int k = 0; k < 11; ++k) {
+        w[k] = (float)std::exp(-(double)((k - 5) * (k - 5)) / (2.0 * 1.5 * 1.5));
+        sum += w[k];
+    }
+    for (int k = 0; k < 11; ++k) w[k] = w[k] / sum;
+    LossWs ws;
+    carve_loss(workspace, C, H, W, &ws);
+    hipStream_t s = as_stream(stream);
+    timed(kLoss, s, [&] { gsd::launch_l1_ssim(C, H, W, w, lambda_dssim, img, gt, ws.gmaps, ws.partial, out3, dL_dimg, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
+                  const int64_t* group_begin, const float* group_lr, int64_t step, float beta1, float beta2, float eps,
+                  int32_t zero_grad, void* stream) {
+    if (n < 0 || n_groups < 1 || n_groups > gsd::kAdamMaxGroups || step < 1)
+        return fail(GSD_ERR_ARG, "adam: need n >= 0, 1 <= n_groups <= 16 and step >= 1");
+    if (n == 0) return GSD_OK;
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !group_begin || !group_lr)
+        return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::AdamArgs a{};
+    a.n = n;
+    a.n_groups = n_groups;
+    a.zero_grad = zero_grad != 0;
+    // torch/optim/adam.py: bias corrections and step size in double on the host, applied as float scalars
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step), bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    for (int g = 0; g < n_groups; ++g) {
+        if (group_begin[g] < (g ? group_begin[g - 1] : 0) || group_begin[g] > n || (g == 0 && group_begin[0] != 0))
+            return fail(GSD_ERR_ARG, "adam: group_begin must start at 0 and be non-decreasing");
+        a.begin[g] = group_begin[g];
+        a.step_size[g] = (float)(-(double)group_lr[g] / bc1);
+        a.bc2_sqrt[g] = (float)std::sqrt(bc2);
+    }
+    a.w1 = 1.f - beta1;
+    a.beta2 = beta2;
+    a.omb2 = 1.f - beta2;
+    a.eps = eps;
+    hipStream_t s = as_stream(stream);
+    timed(kAdam, s, [&] { gsd::launch_adam(a, param, grad, exp_avg, exp_avg_sq, s); });
     GSD_CHECK(false, s);
     return GSD_OK;
 }

@@ -172,6 +172,37 @@ __device__ __forceinline__ float wave_sum4(const float (&c)[4]) {
     return t;
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
+// release/acquire fence plus s_barrier, and the release makes every wave wait
+// for its outstanding global stores and atomics (s_waitcnt vmcnt(0)) before it
+// may arrive -- a full memory round trip after each flush of gradient atomics.
+// Here only the LDS traffic is drained (lgkmcnt(0)); global writes stay in
+// flight across the barrier (nothing in the workgroup reads them back).
+__device__ __forceinline__ void lds_barrier() {
+    // the "memory" clobber keeps the compiler from moving LDS accesses across it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// wave_sum4 in two halves, so columns 0/1 can be folded as soon as they exist
+// (fewer live registers): pair32(c0, c1) leaves lanes 0-31 with column 0 and
+// lanes 32-63 with column 1 (each over lane l and l ^ 32); fin16(pair32(c0, c1),
+// pair32(c2, c3)) returns in every lane the 64-lane total of column
+// kPair16Col[lane >> 4] = {0, 2, 1, 3}.
+__device__ __forceinline__ float pair32(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float fin16(float h01, float h23) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(h01), __float_as_uint(h23), false, false);
+    float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    t = dpp_step<0xb1, 0xf, 0xf>(t);   // quad_perm [1,0,3,2]
+    t = dpp_step<0x4e, 0xf, 0xf>(t);   // quad_perm [2,3,0,1]
+    t = dpp_step<0x141, 0xf, 0xf>(t);  // row_half_mirror
+    t = dpp_step<0x140, 0xf, 0xf>(t);  // row_mirror
+    return t;
+}
+__device__ __forceinline__ int fin16_column(int lane) { return (((lane >> 4) & 1) << 1) | (lane >> 5); }
+
 // Transposed butterfly: c[k] is this lane's value for column k (k = 0..7).
 // Returns, in every lane l, the 64-lane total of column (l >> 3).  Six
 // exchange levels serve all eight columns at once (v_permlane32_swap for lane

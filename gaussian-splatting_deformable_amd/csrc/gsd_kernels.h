@@ -185,6 +185,22 @@ void launch_tile_hist(const HistParams& p, uint32_t* tile_count, hipStream_t s);
 void launch_scatter_hist(const HistParams& p, const uint32_t* tile_base, const float* depths,
                          unsigned long long* keys, hipStream_t s);
 
+constexpr int kAdamMaxGroups = 16;
+struct AdamArgs {
+    long long n;                        // elements in the slabs
+    int n_groups;
+    int zero_grad;                      // also clear the gradient slab
+    long long begin[kAdamMaxGroups];    // first element of each group (begin[0] == 0, increasing)
+    float step_size[kAdamMaxGroups];    // -lr / (1 - beta1^t)
+    float bc2_sqrt[kAdamMaxGroups];     // sqrt(1 - beta2^t)
+    float w1, beta2, omb2, eps;         // 1 - beta1, beta2, 1 - beta2, eps
+};
+void launch_adam(const AdamArgs& a, float* param, float* grad, float* m, float* v, hipStream_t s);
+
+void ssim_tiles(int H, int W, int* tiles_x, int* tiles_y);
+void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
+                    float* gmaps, float* partial, float* out3, float* dimg, hipStream_t s);
+
 constexpr int kHistThreads = 512;       // LDS-histogram binning workgroup
 constexpr int kHistMaxTiles = 40960;    // 160 KiB of u32 bins; larger grids use global-atomic binning
 constexpr int kHistTargetBlocks = 512;  // Gaussian chunks per view

@@ -1,0 +1,216 @@
+// gsd_loss.hip -- the training loss of one view, fused: (1-l) L1 + l (1 - SSIM), value and dL/dimage.
+//
+// Reference: utils/loss_utils.py:17-63 (l1_loss, ssim with an 11x11 sigma 1.5 Gaussian window, zero
+// padding 5, C1 = 0.01^2, C2 = 0.03^2, mean over C*H*W) combined as in train.py:529 with
+// lambda_dssim = 0.2 (arguments/__init__.py:83).  torch evaluates it as 5 grouped conv2d + ~20
+// elementwise kernels forward and as many again backward.  Here:
+//
+//   k_ssim_fwd   one workgroup per (32x32 tile, channel): x, y and a 5-px halo staged in LDS, the five
+//                window sums A = w*x, B = w*y, C = w*x^2, D = w*y^2, E = w*xy by a separable
+//                11-tap pass (horizontal into LDS, then vertical), the SSIM map f, and the three
+//                per-pixel adjoints df/dA, df/dC, df/dE (scaled by -l/N) written to HBM;
+//                per-workgroup partial sums of f and |x - y| (deterministic, no float atomics).
+//   k_ssim_bwd   dL/dx = w * gA + 2x (w * gC) + y (w * gE) + (1-l)/N sign(x - y), the same
+//                separable window (it is symmetric, so the transposed correlation is itself).
+//   k_loss_sum   sums the partials in a fixed order -> loss, L1, SSIM (device scalars).
+//
+// dA/dx etc.: sigma1 = C - A^2, sigma12 = E - AB, f = (2AB + C1)(2 sigma12 + C2) /
+// ((A^2 + B^2 + C1)(sigma1 + sigma2 + C2)); with n1, n2, d1, d2 the four factors and D = d1 d2:
+//   df/dA = (2B (n2 - n1) - 2A f (d2 - d1)) / D,  df/dC = -f / d2,  df/dE = 2 n1 / D
+// (quotient-rule form: no division by n2, which can vanish).  HBM per pixel and channel: forward
+// reads 8 B and writes 12 B, backward reads 20 B and writes 4 B.
+#include "gsd_kernels.h"
+
+namespace gsd {
+
+constexpr int kSsimTile = 32;                        // output tile edge
+constexpr int kSsimHalo = 5;                         // window radius
+constexpr int kSsimIn = kSsimTile + 2 * kSsimHalo;   // 42: staged edge
+constexpr int kSsimThreads = 256;
+
+struct SsimArgs {
+    int C, H, W, tiles_x, tiles_y;
+    float w[11];        // 1-D window (the 2-D window is its outer product)
+    float coef_ssim;    // -lambda / N
+    float coef_l1;      // (1 - lambda) / N
+};
+
+// Stage a 42x42 window of one channel of `a` (and `b`) around the tile, zero outside the image.
+__device__ __forceinline__ void stage(const float* __restrict__ a, float (*sa)[kSsimIn], int H, int W, int ox,
+                                      int oy) {
+    for (int i = threadIdx.x; i < kSsimIn * kSsimIn; i += kSsimThreads) {
+        const int r = i / kSsimIn, c = i - r * kSsimIn;
+        const int gy = oy - kSsimHalo + r, gx = ox - kSsimHalo + c;
+        sa[r][c] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? a[(size_t)gy * W + gx] : 0.f;
+    }
+}
+
+__global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const float* __restrict__ img,
+                                                             const float* __restrict__ gt, float* __restrict__ gmaps,
+                                                             float* __restrict__ partial) {
+    __shared__ float sx[kSsimIn][kSsimIn], sy[kSsimIn][kSsimIn];
+    __shared__ float sh[5][kSsimIn][kSsimTile];  // horizontal sums of x, y, x^2, y^2, xy
+    __shared__ float red[2][kSsimThreads / 64];
+    const int ch = blockIdx.z;
+    const int ox = blockIdx.x * kSsimTile, oy = blockIdx.y * kSsimTile;
+    const size_t plane = (size_t)p.H * p.W;
+    stage(img + ch * plane, sx, p.H, p.W, ox, oy);
+    stage(gt + ch * plane, sy, p.H, p.W, ox, oy);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSsimIn * kSsimTile; i += kSsimThreads) {
+        const int r = i / kSsimTile, c = i - r * kSsimTile;
+        float a = 0.f, b = 0.f, cc = 0.f, d = 0.f, e = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const float x = sx[r][c + k], y = sy[r][c + k], w = p.w[k];
+            a += w * x;
+            b += w * y;
+            cc += w * (x * x);
+            d += w * (y * y);
+            e += w * (x * y);
+        }
+        sh[0][r][c] = a;
+        sh[1][r][c] = b;
+        sh[2][r][c] = cc;
+        sh[3][r][c] = d;
+        sh[4][r][c] = e;
+    }
+    __syncthreads();
+    constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    float fsum = 0.f, l1sum = 0.f;
+    for (int i = threadIdx.x; i < kSsimTile * kSsimTile; i += kSsimThreads) {
+        const int r = i / kSsimTile, c = i - r * kSsimTile;
+        const int gy = oy + r, gx = ox + c;
+        if (gy >= p.H || gx >= p.W) continue;
+        float A = 0.f, B = 0.f, Cx = 0.f, Dy = 0.f, E = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const float w = p.w[k];
+            A += w * sh[0][r + k][c];
+            B += w * sh[1][r + k][c];
+            Cx += w * sh[2][r + k][c];
+            Dy += w * sh[3][r + k][c];
+            E += w * sh[4][r + k][c];
+        }
+        const float s1 = Cx - A * A, s2 = Dy - B * B, s12 = E - A * B;
+        const float n1 = 2.f * A * B + C1, n2 = 2.f * s12 + C2;
+        const float d1 = A * A + B * B + C1, d2 = s1 + s2 + C2;
+        const float Dn = d1 * d2;
+        const float f = (n1 * n2) / Dn;
+        const float inv = 1.f / Dn;
+        const size_t o = ch * plane + (size_t)gy * p.W + gx;
+        const size_t map = (size_t)p.C * plane;  // gmaps = [dL/dA | dL/dC | dL/dE], each (C,H,W)
+        gmaps[o] = p.coef_ssim * ((2.f * B * (n2 - n1) - 2.f * A * f * (d2 - d1)) * inv);
+        gmaps[map + o] = p.coef_ssim * (-f / d2);
+        gmaps[2 * map + o] = p.coef_ssim * (2.f * n1 * inv);
+        fsum += f;
+        l1sum += fabsf(sx[r + kSsimHalo][c + kSsimHalo] - sy[r + kSsimHalo][c + kSsimHalo]);
+    }
+    fsum = wave_sum(fsum);
+    l1sum = wave_sum(l1sum);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = fsum;
+        red[1][threadIdx.x >> 6] = l1sum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int blk = (ch * p.tiles_y + blockIdx.y) * p.tiles_x + blockIdx.x;
+        partial[2 * blk] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        partial[2 * blk + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+}
+
+__global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const float* __restrict__ img,
+                                                             const float* __restrict__ gt,
+                                                             const float* __restrict__ gmaps,
+                                                             float* __restrict__ dimg) {
+    __shared__ float sg[3][kSsimIn][kSsimIn];
+    __shared__ float sh[3][kSsimIn][kSsimTile];
+    const int ch = blockIdx.z;
+    const int ox = blockIdx.x * kSsimTile, oy = blockIdx.y * kSsimTile;
+    const size_t plane = (size_t)p.H * p.W;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) stage(gmaps + ((size_t)q * p.C + ch) * plane, sg[q], p.H, p.W, ox, oy);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSsimIn * kSsimTile; i += kSsimThreads) {
+        const int r = i / kSsimTile, c = i - r * kSsimTile;
+        float a = 0.f, cc = 0.f, e = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const float w = p.w[k];
+            a += w * sg[0][r][c + k];
+            cc += w * sg[1][r][c + k];
+            e += w * sg[2][r][c + k];
+        }
+        sh[0][r][c] = a;
+        sh[1][r][c] = cc;
+        sh[2][r][c] = e;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSsimTile * kSsimTile; i += kSsimThreads) {
+        const int r = i / kSsimTile, c = i - r * kSsimTile;
+        const int gy = oy + r, gx = ox + c;
+        if (gy >= p.H || gx >= p.W) continue;
+        float a = 0.f, cc = 0.f, e = 0.f;
+#pragma unroll
+        for (int k = 0; k < 11; ++k) {
+            const float w = p.w[k];
+            a += w * sh[0][r + k][c];
+            cc += w * sh[1][r + k][c];
+            e += w * sh[2][r + k][c];
+        }
+        const size_t o = ch * plane + (size_t)gy * p.W + gx;
+        const float x = img[o], y = gt[o];
+        const float diff = x - y;
+        const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
+        dimg[o] = a + 2.f * x * cc + y * e + p.coef_l1 * sgn;
+    }
+}
+
+// Fixed-order sum of the per-workgroup partials (one workgroup): out = {loss, L1, SSIM}.
+__global__ __launch_bounds__(256) void k_loss_sum(int nblk, const float* __restrict__ partial, float inv_n,
+                                                  float lambda, float* __restrict__ out) {
+    __shared__ float red[2][4];
+    float f = 0.f, l = 0.f;
+    for (int b = threadIdx.x; b < nblk; b += 256) {
+        f += partial[2 * b];
+        l += partial[2 * b + 1];
+    }
+    f = wave_sum(f);
+    l = wave_sum(l);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = f;
+        red[1][threadIdx.x >> 6] = l;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float ssim = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) * inv_n;
+        const float l1 = ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * inv_n;
+        out[0] = (1.f - lambda) * l1 + lambda * (1.f - ssim);
+        out[1] = l1;
+        out[2] = ssim;
+    }
+}
+
+void ssim_tiles(int H, int W, int* tx, int* ty) {
+    *tx = (W + kSsimTile - 1) / kSsimTile;
+    *ty = (H + kSsimTile - 1) / kSsimTile;
+}
+
+void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
+                    float* gmaps, float* partial, float* out3, float* dimg, hipStream_t s) {
+    SsimArgs p{};
+    p.C = C; p.H = H; p.W = W;
+    ssim_tiles(H, W, &p.tiles_x, &p.tiles_y);
+    for (int k = 0; k < 11; ++k) p.w[k] = w11[k];
+    const double n = (double)C * H * W;
+    p.coef_ssim = (float)(-lambda / n);
+    p.coef_l1 = (float)((1.0 - lambda) / n);
+    const dim3 grid(p.tiles_x, p.tiles_y, C);
+    hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, partial);
+    hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, p.tiles_x * p.tiles_y * C, partial, (float)(1.0 / n),
+                       lambda, out3);
+    if (dimg) hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, dimg);
+}
+
+}  // namespace gsd

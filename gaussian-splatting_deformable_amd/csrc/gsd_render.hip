@@ -27,6 +27,16 @@
 
 namespace gsd {
 
+#ifdef GSD_EXP_PHASES
+// experiment: per-phase wave cycles of k_render_bwd, summed over waves (scripts/prof_render.py prints them)
+__device__ unsigned long long g_phase[8];
+#define PH_T() __builtin_readcyclecounter()
+#define PH_ADD(k, v) ph[k] += (v)
+#else
+#define PH_T() 0ull
+#define PH_ADD(k, v) (void)0
+#endif
+
 constexpr int kBatch = 8;     // forward: records whose alphas are evaluated together (ILP across the exps)
 constexpr int kBwdBatch = 4;  // backward: records per reduction (wave_sum4; keeps 36 partials live, not 72)
 
@@ -194,7 +204,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
+#ifdef GSD_BWD_WAVES
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_WAVES)))
+#else
+__global__ __launch_bounds__(256)
+#endif
+void k_render_bwd(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
     __shared__ float2 s_xy[kTilePix];
     __shared__ float4 s_co[kTilePix];
@@ -220,9 +235,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) wave_lc = max(wave_lc, __shfl_xor(wave_lc, off));
     if (tid == 0) s_tile_lc = 0;
-    __syncthreads();
+    lds_barrier();
     if (lane == 0) atomicMax(&s_tile_lc, wave_lc);
-    __syncthreads();
+    lds_barrier();
     const int total = min((int)(rg.y - rg.x), s_tile_lc);
     const uint32_t end = rg.x + (uint32_t)total;
     const int rounds = (total + kTilePix - 1) / kTilePix;
@@ -239,8 +254,15 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
 
+#ifdef GSD_EXP_PHASES
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long t_start = PH_T();
+#endif
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
-        __syncthreads();
+        [[maybe_unused]] const unsigned long long ta = PH_T();
+        lds_barrier();
+        [[maybe_unused]] const unsigned long long ta2 = PH_T();
+        PH_ADD(0, ta2 - ta);
         const int progress = i * kTilePix + tid;
         if (progress < total) {  // loaded back to front (backward.cu:466-478)
             const uint32_t g = p.point_list[end - progress - 1];
@@ -254,7 +276,11 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         }
 #pragma unroll
         for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;
-        __syncthreads();
+        [[maybe_unused]] const unsigned long long tb0 = PH_T();
+        lds_barrier();
+        [[maybe_unused]] const unsigned long long tb = PH_T();
+        PH_ADD(1, tb0 - ta2);
+        PH_ADD(2, tb - tb0);
         const int n = min(kTilePix, toDo);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
@@ -263,6 +289,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
 #else
         const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
 #endif
+        [[maybe_unused]] const unsigned long long tc = PH_T();
+        PH_ADD(3, tc - tb);
         for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
             // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
             float Gs[kBwdBatch], As[kBwdBatch];
@@ -278,7 +306,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             // forward at the end of each record (acc = alpha c + (1-alpha) acc) rather than at the start of
             // the next contributing one (backward.cu:516-520): the same operations on the same values, and a
             // skipped record (alpha = 0) leaves it unchanged without a select.
-            float v[9][kBwdBatch];
+            // Partials are scaled after the reduction (it is linear): v0 by -W/2, v1 by -H/2, v2..v4 by -1/2,
+            // applied once per (record, tile) in the flush below.  Records 0/1 and 2/3 are folded across the
+            // wave halves as soon as each pair exists (pair32), so at most 27 partials are live.
+            float h[2][9], v[9], prev[9];
             bool any = false;
 #pragma unroll
             for (int u = 0; u < kBwdBatch; ++u) {
@@ -299,49 +330,54 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 float dL_dalpha = (c.x - acc0) * dpix0;
                 dL_dalpha += (c.y - acc1) * dpix1;
                 dL_dalpha += (c.z - acc2) * dpix2;
-                v[6][u] = dchannel_dcolor * dpix0;
-                v[7][u] = dchannel_dcolor * dpix1;
-                v[8][u] = dchannel_dcolor * dpix2;
+                v[6] = dchannel_dcolor * dpix0;
+                v[7] = dchannel_dcolor * dpix1;
+                v[8] = dchannel_dcolor * dpix2;
                 dL_dalpha *= T;
                 dL_dalpha += (-T_final * inv1ma) * bg_dot;
-                const float dL_dG = co.w * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                const float dG_ddely = -gdy * co.z - gdx * co.y;
-                v[0][u] = dL_dG * dG_ddelx * ddelx_dx;
-                v[1][u] = dL_dG * dG_ddely * ddely_dy;
-                v[2][u] = -0.5f * gdx * dx * dL_dG;
-                v[3][u] = -0.5f * gdx * dy * dL_dG;
-                v[4][u] = -0.5f * gdy * dy * dL_dG;
-                v[5][u] = G * dL_dalpha;
+                // backward.cu:530-554 with q = G dL/dG: dL/dmean2D = q (conic . d) (-W/2, -H/2),
+                // dL/dconic = q (dx^2, dx dy, dy^2) (-1/2), dL/dopacity = G dL/dalpha
+                v[5] = G * dL_dalpha;
+                const float q = co.w * v[5];
+                v[0] = q * (dx * co.x + dy * co.y);
+                v[1] = q * (dy * co.z + dx * co.y);
+                v[2] = q * (dx * dx);
+                v[3] = q * (dx * dy);
+                v[4] = q * (dy * dy);
                 acc0 = alpha * c.x + (1.f - alpha) * acc0;
                 acc1 = alpha * c.y + (1.f - alpha) * acc1;
                 acc2 = alpha * c.z + (1.f - alpha) * acc2;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    if (u & 1)
+                        h[u >> 1][k] = pair32(prev[k], v[k]);
+                    else
+                        prev[k] = v[k];
+                }
             }
             if (__ballot(any)) {  // wave-uniform
                 // all nine reductions first (independent: their DPP chains interleave), then one masked store
                 float r[9];
 #pragma unroll
-                for (int q = 0; q < 9; ++q)
-#ifdef GSD_EXP_NORED
-                    r[q] = v[q][0] + v[q][1] + v[q][2] + v[q][3];
-#else
-                    r[q] = wave_sum4(v[q]);
-#endif
-                const int col = lane >> 4;
+                for (int k = 0; k < 9; ++k) r[k] = fin16(h[0][k], h[1][k]);
+                const int col = fin16_column(lane);
                 if ((lane & 15) == 0 && j0 + col < m) {
                     const int dst = list[j0 + col];
 #pragma unroll
-                    for (int q = 0; q < 9; ++q) atomicAdd(&s_acc[q][dst], r[q]);
+                    for (int k = 0; k < 9; ++k) atomicAdd(&s_acc[k][dst], r[k]);
                 }
             }
         }
-        __syncthreads();
+        [[maybe_unused]] const unsigned long long td = PH_T();
+        lds_barrier();
+        [[maybe_unused]] const unsigned long long te = PH_T();
+        PH_ADD(4, td - tc);
+        PH_ADD(5, te - td);
         if (tid < n) {
             const uint32_t g = s_id[tid];
-            const float a0 = s_acc[0][tid], a1 = s_acc[1][tid], a2 = s_acc[2][tid], a3 = s_acc[3][tid],
-                        a4 = s_acc[4][tid], a5 = s_acc[5][tid], a6 = s_acc[6][tid], a7 = s_acc[7][tid],
-                        a8 = s_acc[8][tid];
+            const float a0 = s_acc[0][tid] * -ddelx_dx, a1 = s_acc[1][tid] * -ddely_dy,
+                        a2 = -0.5f * s_acc[2][tid], a3 = -0.5f * s_acc[3][tid], a4 = -0.5f * s_acc[4][tid],
+                        a5 = s_acc[5][tid], a6 = s_acc[6][tid], a7 = s_acc[7][tid], a8 = s_acc[8][tid];
 #ifdef GSD_EXP_NOATOMIC
 #define atomicAdd(ptr, v) (*(ptr) = (v))
 #endif
@@ -358,7 +394,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
 #undef atomicAdd
 #endif
         }
+        PH_ADD(6, PH_T() - te);
     }
+#ifdef GSD_EXP_PHASES
+    ph[7] = PH_T() - t_start;
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], ph[k]);
+#endif
 }
 
 void launch_render_fwd(const RenderParams& p, hipStream_t s) {
@@ -369,3 +411,12 @@ void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
 }
 
 }  // namespace gsd
+
+#ifdef GSD_EXP_PHASES
+extern "C" int gsd_debug_phases(unsigned long long* out) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsd::g_phase), sizeof(unsigned long long) * 8);
+    unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gsd::g_phase), z, sizeof(z));
+    return 0;
+}
+#endif

@@ -58,6 +58,10 @@ SIGNATURES = {
     "gsd_se3_deform_backward": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_activate_forward": (_i32, [_i32, _i32] + [_vp] * 15 + [_vp]),
     "gsd_activate_backward": (_i32, [_i32, _i32, _i32] + [_vp] * 20 + [_vp]),
+    "gsd_l1_ssim_workspace_bytes": (_sz, [_i32, _i32, _i32]),
+    "gsd_l1_ssim": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32), _i64, _f32,
+                             _f32, _f32, _i32, _vp]),
     "gsd_timing_enable": (_i32, [_i32]),
     "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "gsd_timing_reset": (None, []),

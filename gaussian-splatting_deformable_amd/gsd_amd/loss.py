@@ -1,0 +1,71 @@
+"""Training loss of one view, fused in HIP (gsd_loss.hip via gsd_l1_ssim).
+
+Mirrors ``utils/loss_utils.py``: ``l1_loss`` (:17-18), ``ssim`` (:33-63: 11x11 Gaussian window,
+sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2, mean over the map) and the combination of
+``train.py:529``: ``(1 - lambda_dssim) * L1 + lambda_dssim * (1 - SSIM)`` with lambda_dssim = 0.2
+(``arguments/__init__.py:83``).  One kernel pass computes the value and d loss / d image; the gradient
+is kept for the backward, which only scales it.  Images are (C,H,W) (or (1,C,H,W)) float32 on a HIP
+device.  No CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+from ._C import _dev_f32, _ptr, _stream
+
+
+def _run(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float, want_grad: bool):
+    lib = _native.load()
+    if img.dim() == 4 and img.size(0) == 1:
+        img, gt = img[0], gt[0]
+    if img.dim() != 3 or img.shape != gt.shape:
+        raise RuntimeError(f"l1_ssim: expected two (C,H,W) images of the same shape, got {tuple(img.shape)} and "
+                           f"{tuple(gt.shape)}")
+    dev = img.device
+    if dev.type != "cuda":
+        raise RuntimeError("l1_ssim: images must be HIP device tensors (there is no CPU implementation)")
+    x = _dev_f32(img.detach(), "image", dev)
+    y = _dev_f32(gt.detach(), "gt", dev)
+    C, H, W = (int(s) for s in x.shape)
+    ws = torch.empty(lib.gsd_l1_ssim_workspace_bytes(C, H, W), dtype=torch.uint8, device=dev)
+    out3 = torch.empty(3, dtype=torch.float32, device=dev)
+    dimg = torch.empty_like(x) if want_grad else None
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_l1_ssim(C, H, W, _ptr(x), _ptr(y), ctypes.c_float(lambda_dssim), _ptr(out3), _ptr(dimg),
+                                      _ptr(ws), _stream(dev)))
+    return out3, dimg
+
+
+class _L1Ssim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, gt, lambda_dssim, which):
+        out3, dimg = _run(img, gt, lambda_dssim, img.requires_grad)
+        ctx.shape = img.shape
+        ctx.sign = -1.0 if which == 2 else 1.0  # ssim() returns SSIM = 1 - loss(lambda = 1)
+        ctx.save_for_backward(dimg if dimg is not None else torch.empty(0))
+        return out3[which]
+
+    @staticmethod
+    def backward(ctx, g):
+        (dimg,) = ctx.saved_tensors
+        return (dimg * (g * ctx.sign)).view(ctx.shape), None, None, None
+
+
+def l1_ssim_loss(image: torch.Tensor, gt: torch.Tensor, lambda_dssim: float = 0.2) -> torch.Tensor:
+    """(1 - lambda) * l1_loss + lambda * (1 - ssim)  (train.py:529), differentiable w.r.t. ``image``."""
+    return _L1Ssim.apply(image, gt, float(lambda_dssim), 0)
+
+
+def l1_loss(network_output: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    """utils/loss_utils.py:17-18 (fused kernel with lambda = 0)."""
+    return _L1Ssim.apply(network_output, gt, 0.0, 1)
+
+
+def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11, size_average: bool = True) -> torch.Tensor:
+    """utils/loss_utils.py:33-41 (window 11, size_average only), differentiable w.r.t. ``img1``."""
+    if window_size != 11 or not size_average:
+        raise NotImplementedError("ssim: only the reference's defaults (window_size=11, size_average=True)")
+    return _L1Ssim.apply(img1, img2, 1.0, 2)

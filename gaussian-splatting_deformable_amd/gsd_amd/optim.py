@@ -1,0 +1,82 @@
+"""The reference's optimizer step, fused.
+
+``FusedAdam`` keeps torch.optim.Adam's interface and semantics for the Gaussian parameter groups of
+``training_setup`` (scene/gaussian_model.py:839-856: one group per attribute, its own ``lr``, eps 1e-15,
+``update_learning_rate`` rewriting ``param_group['lr']`` each step, :875-886), but stores every
+parameter, gradient and moment in flat slabs so that one HIP launch (gsd_adam_step) updates them all.
+Construction moves each parameter's data into the parameter slab (``p.data`` becomes a view) and makes
+each ``p.grad`` a view of the gradient slab (``self.flat``, a ``FlatGrads``: the one buffer that the
+data-parallel all-reduce sums).  There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+from ._C import _ptr, _stream
+from .parallel import FlatGrads
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=0.0, betas=(0.9, 0.999), eps=1e-15):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        ps = [p for g in self.param_groups for p in g["params"]]
+        if len({id(p) for p in ps}) != len(ps):
+            raise ValueError("FusedAdam: a parameter appears in more than one group")
+        if any(g["betas"] != self.param_groups[0]["betas"] or g["eps"] != self.param_groups[0]["eps"]
+               for g in self.param_groups):
+            raise ValueError("FusedAdam: betas and eps must be the same for every group")
+        if len(self.param_groups) > 16:
+            raise ValueError("FusedAdam: at most 16 parameter groups")
+        dev = ps[0].device
+        if dev.type != "cuda" or any(p.device != dev or p.dtype != torch.float32 for p in ps):
+            raise RuntimeError("FusedAdam: parameters must be float32 HIP device tensors on one device")
+        self.flat = FlatGrads(ps, device=dev)
+        total = self.flat.slab.numel()
+        self.param_slab = torch.empty(total, dtype=torch.float32, device=dev)
+        off = 0
+        for p in ps:
+            n = p.numel()
+            view = self.param_slab[off:off + n].view_as(p)
+            view.copy_(p.detach())
+            p.data = view
+            off += n
+        self.exp_avg = torch.zeros_like(self.param_slab)
+        self.exp_avg_sq = torch.zeros_like(self.param_slab)
+        begins, off = [], 0
+        for g in self.param_groups:
+            begins.append(off)
+            off += sum(p.numel() for p in g["params"])
+        self._begin = (ctypes.c_int64 * len(begins))(*begins)
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero()
+
+    @torch.no_grad()
+    def step(self, closure=None, zero_grad: bool = False):
+        """One Adam step for every group; ``zero_grad`` also clears the gradient slab in the same pass."""
+        loss = closure() if closure is not None else None
+        self.flat.collect()
+        self.step_count += 1
+        g0 = self.param_groups[0]
+        beta1, beta2 = g0["betas"]
+        lrs = (ctypes.c_float * len(self.param_groups))(*[float(g["lr"]) for g in self.param_groups])
+        lib = _native.load()
+        dev = self.param_slab.device
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_adam_step(self.param_slab.numel(), _ptr(self.param_slab), _ptr(self.flat.slab),
+                                            _ptr(self.exp_avg), _ptr(self.exp_avg_sq), len(self.param_groups),
+                                            self._begin, lrs, self.step_count, beta1, beta2, float(g0["eps"]),
+                                            int(bool(zero_grad)), _stream(dev)))
+        if zero_grad:
+            self.flat.attach()
+        return loss
+
+    def reset_state(self):
+        """Zero the moments and the step count (as a freshly constructed torch Adam)."""
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        self.step_count = 0

@@ -180,6 +180,25 @@ int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float*
                           float* g_xyz, float* g_scaling, float* g_rotation, float* g_opacity, float* g_fdc,
                           float* g_frest, float* g_dxyz, float* g_dscale, float* g_drot, float* g_dsh, void* stream);
 
+/* Training loss of one view, fused (utils/loss_utils.py:17-63 combined as train.py:529):
+ *   loss = (1 - lambda_dssim) * mean|img - gt| + lambda_dssim * (1 - SSIM(img, gt))
+ * with the reference's 11x11 Gaussian window (sigma 1.5, zero padding 5, C1 = 0.01^2, C2 = 0.03^2).
+ * img, gt: (C,H,W) device float32.  out3 (device, 3 floats) receives {loss, L1, SSIM}; dL_dimg (C,H,W)
+ * receives d loss / d img (NULL: value only).  workspace: gsd_l1_ssim_workspace_bytes(C,H,W) bytes of
+ * device memory, owned by the caller. */
+size_t gsd_l1_ssim_workspace_bytes(int32_t C, int32_t H, int32_t W);
+int gsd_l1_ssim(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim,
+                float* out3, float* dL_dimg, void* workspace, void* stream);
+
+/* One Adam step (torch.optim.Adam semantics as configured in scene/gaussian_model.py:839-856: per-group
+ * learning rate, betas, eps 1e-15, no weight decay / amsgrad) over flat slabs of n floats: param, grad,
+ * exp_avg, exp_avg_sq.  Group g covers elements [group_begin[g], group_begin[g+1]) (group_begin[0] = 0;
+ * host arrays, n_groups <= 16) with learning rate group_lr[g]; `step` is the 1-based step count after
+ * this update (bias corrections 1 - beta^step).  zero_grad != 0 also clears the gradient slab. */
+int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
+                  const int64_t* group_begin, const float* group_lr, int64_t step, float beta1, float beta2,
+                  float eps, int32_t zero_grad, void* stream);
+
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead
  * per launch); gsd_timing_collect() synchronises on the last recorded event

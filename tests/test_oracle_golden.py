@@ -73,3 +73,14 @@ def test_product_sh_restatement_matches_reference():
     for deg in range(4):
         out = eval_sh(deg, torch.tensor(g[f"sh{deg}"]), torch.tensor(g[f"dirs{deg}"]))
         np.testing.assert_allclose(out.numpy(), g[f"out{deg}"], rtol=0, atol=1e-6)
+
+
+def test_loss_oracle_matches_reference_fixture():
+    """oracle/loss_ref.py (the fp32 restatement gsd_amd.loss is tested against) vs the values the
+    reference's utils/loss_utils.py produced for the same images (tests/golden/loss.npz)."""
+    import torch
+    from oracle import loss_ref
+    g = golden("loss.npz")
+    x, y = torch.from_numpy(g["img1"]), torch.from_numpy(g["img2"])
+    assert abs(float(loss_ref.l1_loss(x, y)) - float(g["l1"])) <= 1e-7
+    assert abs(float(loss_ref.ssim(x, y)) - float(g["ssim"])) <= 1e-6
