@@ -21,12 +21,22 @@
 // reads 8 B and writes 12 B, backward reads 20 B and writes 4 B.
 #include "gsd_kernels.h"
 
+// the loss has no bit-exact contract: multiply-adds fuse to (packed) FMA
+#pragma clang fp contract(fast)
+
 namespace gsd {
 
 constexpr int kSsimTile = 32;                        // output tile edge
 constexpr int kSsimHalo = 5;                         // window radius
 constexpr int kSsimIn = kSsimTile + 2 * kSsimHalo;   // 42: staged edge
 constexpr int kSsimThreads = 256;
+constexpr int kSsimRows = kSsimTile * kSsimTile / kSsimThreads;  // 4 output rows per thread (one column)
+
+// 1/d from v_rcp_f32 plus one Newton step (the loss has no bit-exact contract)
+__device__ __forceinline__ float fast_rcp(float d) {
+    const float r = __builtin_amdgcn_rcpf(d);
+    return fmaf(fmaf(-d, r, 1.0f), r, r);
+}
 
 struct SsimArgs {
     int C, H, W, tiles_x, tiles_y;
@@ -35,14 +45,30 @@ struct SsimArgs {
     float coef_l1;      // (1 - lambda) / N
 };
 
-// Stage a 42x42 window of one channel of `a` (and `b`) around the tile, zero outside the image.
+// Stage a 42x42 window of one channel of `a` around the tile, zero outside the image.  Fixed trip
+// counts, fully unrolled: all 12 loads of a thread are in flight before the first LDS store.
 __device__ __forceinline__ void stage(const float* __restrict__ a, float (*sa)[kSsimIn], int H, int W, int ox,
                                       int oy) {
-    for (int i = threadIdx.x; i < kSsimIn * kSsimIn; i += kSsimThreads) {
-        const int r = i / kSsimIn, c = i - r * kSsimIn;
-        const int gy = oy - kSsimHalo + r, gx = ox - kSsimHalo + c;
-        sa[r][c] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? a[(size_t)gy * W + gx] : 0.f;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    constexpr int kRowIt = (kSsimIn + 7) / 8, kColIt = 2;  // 6 x 2 slots of a 8 x 32 thread grid
+    float v[kRowIt][kColIt];
+#pragma unroll
+    for (int i = 0; i < kRowIt; ++i) {
+        const int r = ty + 8 * i, gy = oy - kSsimHalo + r;
+#pragma unroll
+        for (int j = 0; j < kColIt; ++j) {
+            const int c = tx + 32 * j, gx = ox - kSsimHalo + c;
+            const bool ok = r < kSsimIn && c < kSsimIn && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            v[i][j] = ok ? a[(size_t)gy * W + gx] : 0.f;
+        }
     }
+#pragma unroll
+    for (int i = 0; i < kRowIt; ++i)
+#pragma unroll
+        for (int j = 0; j < kColIt; ++j) {
+            const int r = ty + 8 * i, c = tx + 32 * j;
+            if (r < kSsimIn && c < kSsimIn) sa[r][c] = v[i][j];
+        }
 }
 
 __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const float* __restrict__ img,
@@ -57,8 +83,9 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
     stage(img + ch * plane, sx, p.H, p.W, ox, oy);
     stage(gt + ch * plane, sy, p.H, p.W, ox, oy);
     __syncthreads();
-    for (int i = threadIdx.x; i < kSsimIn * kSsimTile; i += kSsimThreads) {
-        const int r = i / kSsimTile, c = i - r * kSsimTile;
+    // horizontal pass: thread = (column c, row group); no integer division
+    for (int r = threadIdx.x >> 5; r < kSsimIn; r += kSsimThreads / 32) {
+        const int c = threadIdx.x & 31;
         float a = 0.f, b = 0.f, cc = 0.f, d = 0.f, e = 0.f;
 #pragma unroll
         for (int k = 0; k < 11; ++k) {
@@ -78,30 +105,37 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
     __syncthreads();
     constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
     float fsum = 0.f, l1sum = 0.f;
-    for (int i = threadIdx.x; i < kSsimTile * kSsimTile; i += kSsimThreads) {
-        const int r = i / kSsimTile, c = i - r * kSsimTile;
-        const int gy = oy + r, gx = ox + c;
-        if (gy >= p.H || gx >= p.W) continue;
-        float A = 0.f, B = 0.f, Cx = 0.f, Dy = 0.f, E = 0.f;
+    // vertical pass: thread (c, g) produces rows 4g..4g+3 of column c from 14 staged rows (register reuse)
+    const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimRows;
+    float acc[5][kSsimRows];
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const float w = p.w[k];
-            A += w * sh[0][r + k][c];
-            B += w * sh[1][r + k][c];
-            Cx += w * sh[2][r + k][c];
-            Dy += w * sh[3][r + k][c];
-            E += w * sh[4][r + k][c];
+    for (int q = 0; q < 5; ++q)
+#pragma unroll
+        for (int j = 0; j < kSsimRows; ++j) acc[q][j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < kSsimRows + 10; ++t) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const float h = sh[q][r0 + t][c];
+#pragma unroll
+            for (int j = 0; j < kSsimRows; ++j)
+                if (t - j >= 0 && t - j < 11) acc[q][j] += p.w[t - j] * h;
         }
+    }
+    const size_t map = (size_t)p.C * plane;  // gmaps = [dL/dA | dL/dC | dL/dE], each (C,H,W)
+#pragma unroll
+    for (int j = 0; j < kSsimRows; ++j) {
+        const int r = r0 + j, gy = oy + r, gx = ox + c;
+        if (gy >= p.H || gx >= p.W) continue;
+        const float A = acc[0][j], B = acc[1][j], Cx = acc[2][j], Dy = acc[3][j], E = acc[4][j];
         const float s1 = Cx - A * A, s2 = Dy - B * B, s12 = E - A * B;
         const float n1 = 2.f * A * B + C1, n2 = 2.f * s12 + C2;
         const float d1 = A * A + B * B + C1, d2 = s1 + s2 + C2;
-        const float Dn = d1 * d2;
-        const float f = (n1 * n2) / Dn;
-        const float inv = 1.f / Dn;
+        const float inv = fast_rcp(d1 * d2);
+        const float f = (n1 * n2) * inv;
         const size_t o = ch * plane + (size_t)gy * p.W + gx;
-        const size_t map = (size_t)p.C * plane;  // gmaps = [dL/dA | dL/dC | dL/dE], each (C,H,W)
         gmaps[o] = p.coef_ssim * ((2.f * B * (n2 - n1) - 2.f * A * f * (d2 - d1)) * inv);
-        gmaps[map + o] = p.coef_ssim * (-f / d2);
+        gmaps[map + o] = p.coef_ssim * (-f * fast_rcp(d2));
         gmaps[2 * map + o] = p.coef_ssim * (2.f * n1 * inv);
         fsum += f;
         l1sum += fabsf(sx[r + kSsimHalo][c + kSsimHalo] - sy[r + kSsimHalo][c + kSsimHalo]);
@@ -132,8 +166,8 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
 #pragma unroll
     for (int q = 0; q < 3; ++q) stage(gmaps + ((size_t)q * p.C + ch) * plane, sg[q], p.H, p.W, ox, oy);
     __syncthreads();
-    for (int i = threadIdx.x; i < kSsimIn * kSsimTile; i += kSsimThreads) {
-        const int r = i / kSsimTile, c = i - r * kSsimTile;
+    for (int r = threadIdx.x >> 5; r < kSsimIn; r += kSsimThreads / 32) {
+        const int c = threadIdx.x & 31;
         float a = 0.f, cc = 0.f, e = 0.f;
 #pragma unroll
         for (int k = 0; k < 11; ++k) {
@@ -147,23 +181,31 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
         sh[2][r][c] = e;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kSsimTile * kSsimTile; i += kSsimThreads) {
-        const int r = i / kSsimTile, c = i - r * kSsimTile;
-        const int gy = oy + r, gx = ox + c;
-        if (gy >= p.H || gx >= p.W) continue;
-        float a = 0.f, cc = 0.f, e = 0.f;
+    const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimRows;
+    float acc[3][kSsimRows];
 #pragma unroll
-        for (int k = 0; k < 11; ++k) {
-            const float w = p.w[k];
-            a += w * sh[0][r + k][c];
-            cc += w * sh[1][r + k][c];
-            e += w * sh[2][r + k][c];
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int j = 0; j < kSsimRows; ++j) acc[q][j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < kSsimRows + 10; ++t) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const float h = sh[q][r0 + t][c];
+#pragma unroll
+            for (int j = 0; j < kSsimRows; ++j)
+                if (t - j >= 0 && t - j < 11) acc[q][j] += p.w[t - j] * h;
         }
+    }
+#pragma unroll
+    for (int j = 0; j < kSsimRows; ++j) {
+        const int gy = oy + r0 + j, gx = ox + c;
+        if (gy >= p.H || gx >= p.W) continue;
         const size_t o = ch * plane + (size_t)gy * p.W + gx;
         const float x = img[o], y = gt[o];
         const float diff = x - y;
         const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
-        dimg[o] = a + 2.f * x * cc + y * e + p.coef_l1 * sgn;
+        dimg[o] = acc[0][j] + 2.f * x * acc[1][j] + y * acc[2][j] + p.coef_l1 * sgn;
     }
 }
 

@@ -9,7 +9,7 @@ IFS=';' read -ra PASSES <<< "${PMC_PASSES}"
 for pass in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $pass --kernel-include-regex "${KREGEX:-gsd}" --output-format csv \
-      -d "$R/gpurun_out/pmc/p$i" -o pmc -- python "$R/scripts/prof_render.py" --iters 3 > gpurun_out/pmc/p$i.log 2>&1
+      -d "$R/gpurun_out/pmc/p$i" -o pmc -- python "$R/${PROF_SCRIPT:-scripts/prof_render.py}" ${PROF_ARGS:---iters 3} > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($pass) rc=$rc"
   [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc/p$i.log; exit $rc; }
 done
