@@ -27,15 +27,6 @@
 
 namespace gsd {
 
-#ifdef GSD_EXP_PHASES
-// experiment: per-phase wave cycles of k_render_bwd, summed over waves (scripts/prof_render.py prints them)
-__device__ unsigned long long g_phase[8];
-#define PH_T() __builtin_readcyclecounter()
-#define PH_ADD(k, v) ph[k] += (v)
-#else
-#define PH_T() 0ull
-#define PH_ADD(k, v) (void)0
-#endif
 
 constexpr int kBatch = 8;     // forward: records whose alphas are evaluated together (ILP across the exps)
 constexpr int kBwdBatch = 4;  // backward: records per reduction (wave_sum4; keeps 36 partials live, not 72)
@@ -55,11 +46,33 @@ __device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
     return make_float4(xy.x - ex, xy.x + ex, xy.y - ey, xy.y + ey);
 }
 
+// Does the ellipse {d : Q(d) <= t} around (mx, my) meet the rectangle [x0, x1] x [y0, y1]?
+// Q(d) = a dx^2 + 2 b dx dy + c dy^2 (positive definite: a, c > 0, det > 0).  Q is convex, so its minimum
+// over the rectangle is 0 when the centre is inside, else it lies on an edge; on an edge x = const the
+// minimiser is dy* = -b dx / c clamped to the edge (and symmetrically).  Conservative by `slack`.
+__device__ __forceinline__ float edge_min_x(float a, float b, float c, float dx, float dy0, float dy1) {
+    const float dy = fminf(fmaxf(-b * dx / c, dy0), dy1);
+    return a * dx * dx + 2.f * b * dx * dy + c * dy * dy;
+}
+__device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t, float x0, float x1, float y0,
+                                                   float y1) {
+    const float dx0 = x0 - xy.x, dx1 = x1 - xy.x, dy0 = y0 - xy.y, dy1 = y1 - xy.y;
+    if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // centre inside
+    const float a = co.x, b = co.y, c = co.z;
+    float q = fminf(edge_min_x(a, b, c, dx0, dy0, dy1), edge_min_x(a, b, c, dx1, dy0, dy1));
+    q = fminf(q, fminf(edge_min_x(c, b, a, dy0, dx0, dx1), edge_min_x(c, b, a, dy1, dx0, dx1)));
+    return !(q > t);  // NaN-safe: keeps the record
+}
+
 // Per-wave compaction of the batch: s_list receives, in increasing slot order,
-// the slots whose alpha box meets [qx0, qx0+7] x [qy0, qy0+7].  Returns the count.
+// the slots whose alpha box meets [qx0, qx0+7] x [qy0, qy0+7] -- and, with kExact,
+// whose alpha ellipse meets it too (-11 % of the backward's record iterations on the
+// bench scene; the forward, cheaper per record and early-terminating, loses more to
+// the extra test than it saves).  Returns the count.
 // Slots below t_min are skipped too (the backward's last-contributor bound).
-template <int RW = 8, int RH = 8>
-__device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, uint8_t* __restrict__ s_list, int n,
+template <bool kExact, int RW = 8, int RH = 8>
+__device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, const float2* __restrict__ s_xy,
+                                            const float4* __restrict__ s_co, uint8_t* __restrict__ s_list, int n,
                                             float qx0, float qy0, int lane, int t_min = 0) {
     int m = 0;
 #pragma unroll
@@ -69,6 +82,15 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, ui
         if (t < n && t >= t_min) {
             const float4 bx = s_box[t];
             hit = bx.y >= qx0 && bx.x <= qx0 + (float)(RW - 1) && bx.w >= qy0 && bx.z <= qy0 + (float)(RH - 1);
+            if (kExact && hit) {
+                const float4 co = s_co[t];
+                const float det = co.x * co.z - co.y * co.y;
+                // alpha >= 1/255  <=>  Q <= 2 ln(255 o); slack: 0.1 % + 0.05 (v_exp / v_log rounding)
+                const float tq = 2.0f * 0.69314718f * __builtin_amdgcn_logf(255.0f * co.w) * 1.001f + 0.05f;
+                if (co.x > 0.f && co.z > 0.f && det > 0.f)
+                    hit = ellipse_meets_rect(s_xy[t], co, tq, qx0, qx0 + (float)(RW - 1), qy0,
+                                             qy0 + (float)(RH - 1));
+            }
         }
         const unsigned long long mask = __ballot(hit);
         if (hit) {
@@ -161,7 +183,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, tg.lane);
+        const int m = wave_compact<false>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, tg.lane);
         for (int j0 = 0; j0 < m; j0 += kBatch) {
             if (!__ballot(!done)) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
@@ -204,12 +226,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     }
 }
 
-#ifdef GSD_BWD_WAVES
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_WAVES)))
-#else
-__global__ __launch_bounds__(256)
-#endif
-void k_render_bwd(RenderBwdParams p) {
+__global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
     __shared__ float2 s_xy[kTilePix];
     __shared__ float4 s_co[kTilePix];
@@ -254,15 +271,8 @@ void k_render_bwd(RenderBwdParams p) {
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
 
-#ifdef GSD_EXP_PHASES
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const unsigned long long t_start = PH_T();
-#endif
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
-        [[maybe_unused]] const unsigned long long ta = PH_T();
         lds_barrier();
-        [[maybe_unused]] const unsigned long long ta2 = PH_T();
-        PH_ADD(0, ta2 - ta);
         const int progress = i * kTilePix + tid;
         if (progress < total) {  // loaded back to front (backward.cu:466-478)
             const uint32_t g = p.point_list[end - progress - 1];
@@ -276,21 +286,11 @@ void k_render_bwd(RenderBwdParams p) {
         }
 #pragma unroll
         for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;
-        [[maybe_unused]] const unsigned long long tb0 = PH_T();
         lds_barrier();
-        [[maybe_unused]] const unsigned long long tb = PH_T();
-        PH_ADD(1, tb0 - ta2);
-        PH_ADD(2, tb - tb0);
         const int n = min(kTilePix, toDo);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
-#ifdef GSD_EXP_NOCOMPUTE
-        const int m = 0 * wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
-#else
-        const int m = wave_compact(s_box, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
-#endif
-        [[maybe_unused]] const unsigned long long tc = PH_T();
-        PH_ADD(3, tc - tb);
+        const int m = wave_compact<true>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
         for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
             // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
             float Gs[kBwdBatch], As[kBwdBatch];
@@ -368,19 +368,12 @@ void k_render_bwd(RenderBwdParams p) {
                 }
             }
         }
-        [[maybe_unused]] const unsigned long long td = PH_T();
         lds_barrier();
-        [[maybe_unused]] const unsigned long long te = PH_T();
-        PH_ADD(4, td - tc);
-        PH_ADD(5, te - td);
         if (tid < n) {
             const uint32_t g = s_id[tid];
             const float a0 = s_acc[0][tid] * -ddelx_dx, a1 = s_acc[1][tid] * -ddely_dy,
                         a2 = -0.5f * s_acc[2][tid], a3 = -0.5f * s_acc[3][tid], a4 = -0.5f * s_acc[4][tid],
                         a5 = s_acc[5][tid], a6 = s_acc[6][tid], a7 = s_acc[7][tid], a8 = s_acc[8][tid];
-#ifdef GSD_EXP_NOATOMIC
-#define atomicAdd(ptr, v) (*(ptr) = (v))
-#endif
             if (a0 != 0.f) atomicAdd(p.dL_dmean2D + 3 * g, a0);
             if (a1 != 0.f) atomicAdd(p.dL_dmean2D + 3 * g + 1, a1);
             if (a2 != 0.f) atomicAdd(p.dL_dconic + 4 * g, a2);
@@ -390,17 +383,8 @@ void k_render_bwd(RenderBwdParams p) {
             if (a6 != 0.f) atomicAdd(p.dL_dcolors + 3 * g, a6);
             if (a7 != 0.f) atomicAdd(p.dL_dcolors + 3 * g + 1, a7);
             if (a8 != 0.f) atomicAdd(p.dL_dcolors + 3 * g + 2, a8);
-#ifdef GSD_EXP_NOATOMIC
-#undef atomicAdd
-#endif
         }
-        PH_ADD(6, PH_T() - te);
     }
-#ifdef GSD_EXP_PHASES
-    ph[7] = PH_T() - t_start;
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], ph[k]);
-#endif
 }
 
 void launch_render_fwd(const RenderParams& p, hipStream_t s) {
@@ -412,11 +396,3 @@ void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
 
 }  // namespace gsd
 
-#ifdef GSD_EXP_PHASES
-extern "C" int gsd_debug_phases(unsigned long long* out) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(gsd::g_phase), sizeof(unsigned long long) * 8);
-    unsigned long long z[8] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(gsd::g_phase), z, sizeof(z));
-    return 0;
-}
-#endif

@@ -51,14 +51,6 @@ def main():
     if a.timing:
         for k, (tot, n) in kernel_times(enable=False).items():
             print("%-16s %8.4f ms/launch (%d launches)" % (k, tot / n, n))
-    lib = __import__("gsd_amd._native", fromlist=["load"]).load()
-    if hasattr(lib, "gsd_debug_phases"):  # GSD_EXP_PHASES builds: per-phase wave cycles of render_bwd
-        import ctypes
-        buf = (ctypes.c_ulonglong * 8)()
-        lib.gsd_debug_phases(buf)
-        names = ["bar1", "stage", "bar2", "compact", "compute", "bar3", "flush", "total"]
-        tot = buf[7] or 1
-        print("render_bwd phases (% of wave cycles):", {n: round(100.0 * buf[k] / tot, 1) for k, n in enumerate(names)})
     print("done K=%d" % K)
 
 
