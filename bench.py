@@ -60,6 +60,21 @@ def algorithmic_bytes(P, V, K, W, H, C):
     }
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*/pmc_traffic.json,
+    written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return {"hbm_bytes": d[kernel]["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def make_optimizer(pc):
     """training_setup (scene/gaussian_model.py:834-864) param groups, spatial_lr_scale = 1, eps 1e-15, as one
     fused HIP Adam over flat slabs (gsd_amd.optim.FusedAdam; torch.optim.Adam semantics)."""
@@ -219,6 +234,10 @@ def main():
                 roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                         "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(per_kernel[dom], 4)}
+                tr = pmc_traffic(dom)
+                if tr is not None:
+                    roof["traffic"] = tr["hbm_bytes"]
+                    roof["traffic_source"] = tr["source"]
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             cpu = cpu_baseline(cfg, args.config)

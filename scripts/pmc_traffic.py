@@ -1,0 +1,41 @@
+#!/usr/bin/env python
+"""HBM traffic per launch from rocprofv3 PMC passes (scripts/gpu_pmc.sh with FETCH_SIZE and WRITE_SIZE in
+separate passes), corrected as /opt/skills/guides/MI355X_MICROARCH.md (HBM section) prescribes for gfx950:
+FETCH_SIZE (KB) reports half the bytes of wide coalesced reads -> doubled; WRITE_SIZE (KB) is taken as is.
+Writes a JSON {kernel: {fetch_kb, write_kb, hbm_bytes}} that bench.py reads for roofline.traffic.
+
+    python scripts/pmc_traffic.py gpurun_out/pmc profiles/round1/pmc_traffic.json
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import summarise  # noqa: E402
+
+
+def short(name):
+    n = name.split("::")[-1]
+    n = n.split("<")[0]
+    return n[2:] if n.startswith("k_") else n
+
+
+def main(src, dst):
+    s = summarise(src)
+    out = {}
+    for k, cs in s.items():
+        if "FETCH_SIZE" not in cs and "WRITE_SIZE" not in cs:
+            continue
+        f, w = cs.get("FETCH_SIZE", 0.0), cs.get("WRITE_SIZE", 0.0)
+        out[short(k)] = {"kernel": k, "fetch_kb": round(f, 1), "write_kb": round(w, 1),
+                         "hbm_bytes": int(round((2.0 * f + w) * 1024.0))}
+    out["_note"] = ("per-launch means over the profiled launches (scripts/prof_render.py, cfg 4); FETCH_SIZE x2 "
+                    "per the gfx950 calibration, WRITE_SIZE as is; gathers and atomics are uncalibrated widths")
+    with open(dst, "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc",
+         sys.argv[2] if len(sys.argv) > 2 else "profiles/round1/pmc_traffic.json")
