@@ -185,11 +185,11 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kAdam, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kAdam, kDensify, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
-                                               "activate_bwd",   "l1_ssim",      "adam"};
+                                               "activate_bwd",   "l1_ssim",      "adam",         "densify_stats"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -575,6 +575,20 @@ int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* e
     a.eps = eps;
     hipStream_t s = as_stream(stream);
     timed(kAdam, s, [&] { gsd::launch_adam(a, param, grad, exp_avg, exp_avg_sq, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int gsd_densify_stats(int32_t P, const float* viewspace_grad, const int32_t* radii, float* grad_accum,
+                      float* grad_accum_3vec, float* denom, float* max_radii2D, void* stream) {
+    if (P < 0) return fail(GSD_ERR_ARG, "invalid P");
+    if (P == 0) return GSD_OK;
+    if (!viewspace_grad || !radii || !grad_accum || !grad_accum_3vec || !denom || !max_radii2D)
+        return fail(GSD_ERR_ARG, "null pointer argument");
+    hipStream_t s = as_stream(stream);
+    timed(kDensify, s, [&] {
+        gsd::launch_densify_stats(P, viewspace_grad, radii, grad_accum, grad_accum_3vec, denom, max_radii2D, s);
+    });
     GSD_CHECK(false, s);
     return GSD_OK;
 }

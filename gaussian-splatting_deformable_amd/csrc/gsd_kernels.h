@@ -185,6 +185,9 @@ void launch_tile_hist(const HistParams& p, uint32_t* tile_count, hipStream_t s);
 void launch_scatter_hist(const HistParams& p, const uint32_t* tile_base, const float* depths,
                          unsigned long long* keys, hipStream_t s);
 
+void launch_densify_stats(int P, const float* vgrad, const int* radii, float* accum, float* accum3, float* denom,
+                          float* max_radii, hipStream_t s);
+
 constexpr int kAdamMaxGroups = 16;
 struct AdamArgs {
     long long n;                        // elements in the slabs

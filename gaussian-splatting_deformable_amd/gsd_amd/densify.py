@@ -1,0 +1,142 @@
+"""Densification and pruning (cfg 5 runs it every 100 views).
+
+Mirrors scene/gaussian_model.py:960-1257 and its call site train.py:610-648 for a ``DeformableGaussians``
+trained by ``gsd_amd.optim.FusedAdam``:
+
+- ``add_densification_stats`` / the max-radii update (train.py:613-616, :1252-1257) run as one fused HIP
+  pass (``gsd_densify_stats``) instead of ~8 boolean-mask torch kernels per view.
+- ``densify_and_clone`` (:1186-1200), ``densify_and_split`` (:1129-1152), ``prune_points`` (:1064-1079),
+  ``densify_and_prune`` (:1219-1233) and ``reset_opacity`` (:960-963) keep the reference's selection rules,
+  sampling (``torch.normal`` around the parent with its scale, rotated), ordering and optimizer-state
+  semantics: new points get zero moments, pruned points drop theirs, a replaced tensor gets zero moments.
+  They run every ``densification_interval`` (100) views, so they stay torch ops on the GPU; the flat
+  parameter / moment / gradient slabs are rebuilt once per call (``FusedAdam.rebuild``).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native
+from ._C import _ptr, _stream
+from .renderer import build_rotation, inverse_sigmoid
+
+_NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+
+
+class GaussianDensifier:
+    def __init__(self, pc, optimizer, percent_dense: float = 0.01):
+        self.pc = pc
+        self.opt = optimizer
+        self.percent_dense = percent_dense
+        self._reset_stats()
+
+    # ---- statistics (one fused kernel per view) ----
+    def _reset_stats(self):
+        P, dev = self.pc._xyz.shape[0], self.pc._xyz.device
+        self.xyz_gradient_accum = torch.zeros((P, 1), device=dev)
+        self.xyz_gradient_accum_3vec = torch.zeros((P, 3), device=dev)
+        self.denom = torch.zeros((P, 1), device=dev)
+        self.max_radii2D = torch.zeros((P,), device=dev)
+
+    def add_densification_stats(self, viewspace_point_tensor, radii):
+        """train.py:613-616: max_radii2D / gradient accumulators for the Gaussians with radii > 0
+        (``visibility_filter``); ``viewspace_point_tensor`` is render()'s ``viewspace_points``."""
+        g = viewspace_point_tensor.grad
+        if g is None:
+            raise RuntimeError("add_densification_stats: viewspace_points has no gradient (call backward first)")
+        lib = _native.load()
+        P = int(radii.shape[0])
+        g = g.contiguous()
+        r = radii.to(torch.int32).contiguous()
+        with torch.cuda.device(g.device):
+            _native.check(lib.gsd_densify_stats(P, _ptr(g), _ptr(r), _ptr(self.xyz_gradient_accum),
+                                                _ptr(self.xyz_gradient_accum_3vec), _ptr(self.denom),
+                                                _ptr(self.max_radii2D), _stream(g.device)))
+
+    # ---- optimizer-state surgery ----
+    def _params(self):
+        pc = self.pc
+        return [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+
+    def _apply(self, fn):
+        """fn(name, data, exp_avg, exp_avg_sq) -> (data, exp_avg, exp_avg_sq) for every Gaussian attribute;
+        any other optimizer parameter (e.g. a twist or an offset network) must not change shape."""
+        datas, ms, vs = [], [], []
+        gauss = {id(p): n for p, n in zip(self._params(), _NAMES)}
+        for g in self.opt.param_groups:
+            for p in g["params"]:
+                m, v = self.opt.moments(p)
+                if id(p) in gauss:
+                    d, m, v = fn(gauss[id(p)], p.detach(), m, v)
+                else:
+                    d = p.detach()
+                datas.append(d)
+                ms.append(m)
+                vs.append(v)
+        self.opt.rebuild(datas, ms, vs)
+
+    def densification_postfix(self, new):
+        """:1107-1127 -- append points (zero moments) and reset the statistics."""
+        self._apply(lambda n, d, m, v: (torch.cat((d, new[n]), 0), torch.cat((m, torch.zeros_like(new[n])), 0),
+                                        torch.cat((v, torch.zeros_like(new[n])), 0)))
+        self._reset_stats()
+
+    def prune_points(self, mask):
+        """:1064-1079 -- drop the points where ``mask`` is True (with their moments and statistics)."""
+        keep = ~mask
+        self._apply(lambda n, d, m, v: (d[keep], m[keep], v[keep]))
+        self.xyz_gradient_accum = self.xyz_gradient_accum[keep]
+        self.xyz_gradient_accum_3vec = self.xyz_gradient_accum_3vec[keep]
+        self.denom = self.denom[keep]
+        self.max_radii2D = self.max_radii2D[keep]
+
+    # ---- the reference's operations ----
+    def densify_and_clone(self, grads, grad_threshold, scene_extent):
+        pc = self.pc
+        sel = torch.where(torch.norm(grads, dim=-1) >= grad_threshold, True, False)
+        sel = torch.logical_and(sel, torch.max(pc.get_scaling, dim=1).values <= self.percent_dense * scene_extent)
+        new = {"xyz": pc._xyz[sel], "f_dc": pc._features_dc[sel], "f_rest": pc._features_rest[sel],
+               "opacity": pc._opacity[sel], "scaling": pc._scaling[sel], "rotation": pc._rotation[sel]}
+        self.densification_postfix({k: v.detach() for k, v in new.items()})
+
+    def densify_and_split(self, grads, grad_threshold, scene_extent, N=2):
+        pc = self.pc
+        n_init = pc._xyz.shape[0]
+        padded = torch.zeros((n_init), device=pc._xyz.device)
+        padded[:grads.shape[0]] = grads.squeeze()
+        sel = torch.where(padded >= grad_threshold, True, False)
+        sel = torch.logical_and(sel, torch.max(pc.get_scaling, dim=1).values > self.percent_dense * scene_extent)
+        with torch.no_grad():
+            stds = pc.get_scaling[sel].repeat(N, 1)
+            means = torch.zeros((stds.size(0), 3), device=pc._xyz.device)
+            samples = torch.normal(mean=means, std=stds)
+            rots = build_rotation(pc._rotation[sel]).repeat(N, 1, 1)
+            new = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + pc._xyz[sel].repeat(N, 1),
+                   "scaling": torch.log(pc.get_scaling[sel].repeat(N, 1) / (0.8 * N)),
+                   "rotation": pc._rotation[sel].repeat(N, 1), "f_dc": pc._features_dc[sel].repeat(N, 1, 1),
+                   "f_rest": pc._features_rest[sel].repeat(N, 1, 1), "opacity": pc._opacity[sel].repeat(N, 1)}
+        self.densification_postfix(new)
+        prune = torch.cat((sel, torch.zeros(N * int(sel.sum()), device=sel.device, dtype=torch.bool)))
+        self.prune_points(prune)
+
+    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size):
+        """:1219-1233."""
+        grads = self.xyz_gradient_accum / self.denom
+        grads[grads.isnan()] = 0.0
+        self.densify_and_clone(grads, max_grad, extent)
+        self.densify_and_split(grads, max_grad, extent)
+        pc = self.pc
+        with torch.no_grad():
+            prune = (pc.get_opacity < min_opacity).squeeze()
+            if max_screen_size:
+                big_vs = self.max_radii2D > max_screen_size
+                big_ws = pc.get_scaling.max(dim=1).values > 0.1 * extent
+                prune = torch.logical_or(torch.logical_or(prune, big_vs), big_ws)
+        self.prune_points(prune)
+
+    def reset_opacity(self):
+        """:960-963 -- opacities to min(sigmoid(o), 0.01), with zero moments for that group."""
+        with torch.no_grad():
+            new = inverse_sigmoid(torch.min(self.pc.get_opacity, torch.ones_like(self.pc.get_opacity) * 0.01))
+        self._apply(lambda n, d, m, v: (new, torch.zeros_like(new), torch.zeros_like(new)) if n == "opacity"
+                    else (d, m, v))

@@ -75,6 +75,50 @@ class FusedAdam(torch.optim.Optimizer):
             self.flat.attach()
         return loss
 
+    def moments(self, p: torch.Tensor):
+        """(exp_avg, exp_avg_sq) views of parameter ``p`` (shaped like ``p``)."""
+        off = 0
+        for q in (q for g in self.param_groups for q in g["params"]):
+            n = q.numel()
+            if q is p:
+                return self.exp_avg[off:off + n].view_as(q), self.exp_avg_sq[off:off + n].view_as(q)
+            off += n
+        raise KeyError("parameter not managed by this optimizer")
+
+    @torch.no_grad()
+    def rebuild(self, new_data, new_exp_avg, new_exp_avg_sq):
+        """Give every parameter (in group order) new data and moments, whose shapes may differ from the old
+        ones -- the optimizer-state surgery of densification (scene/gaussian_model.py:1027-1105:
+        replace / prune / concatenate).  Parameter objects stay the same; their ``.data`` and ``.grad``
+        become views of freshly allocated slabs; the gradient slab is zero."""
+        ps = [p for g in self.param_groups for p in g["params"]]
+        if not (len(new_data) == len(new_exp_avg) == len(new_exp_avg_sq) == len(ps)):
+            raise ValueError("rebuild: one tensor per parameter expected")
+        dev = self.param_slab.device
+        total = sum(t.numel() for t in new_data)
+        param_slab = torch.empty(total, dtype=torch.float32, device=dev)
+        exp_avg = torch.empty_like(param_slab)
+        exp_avg_sq = torch.empty_like(param_slab)
+        off = 0
+        for p, d, a, b in zip(ps, new_data, new_exp_avg, new_exp_avg_sq):
+            n = d.numel()
+            if a.numel() != n or b.numel() != n:
+                raise ValueError("rebuild: moments must match their parameter")
+            view = param_slab[off:off + n].view_as(d)
+            view.copy_(d)
+            exp_avg[off:off + n].copy_(a.reshape(-1))
+            exp_avg_sq[off:off + n].copy_(b.reshape(-1))
+            p.grad = None
+            p.data = view
+            off += n
+        self.param_slab, self.exp_avg, self.exp_avg_sq = param_slab, exp_avg, exp_avg_sq
+        self.flat = FlatGrads(ps, device=dev)
+        begins, off = [], 0
+        for g in self.param_groups:
+            begins.append(off)
+            off += sum(p.numel() for p in g["params"])
+        self._begin = (ctypes.c_int64 * len(begins))(*begins)
+
     def reset_state(self):
         """Zero the moments and the step count (as a freshly constructed torch Adam)."""
         self.exp_avg.zero_()

@@ -199,6 +199,12 @@ int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* e
                   const int64_t* group_begin, const float* group_lr, int64_t step, float beta1, float beta2,
                   float eps, int32_t zero_grad, void* stream);
 
+/* Per-view densification statistics (train.py:613-616, scene/gaussian_model.py:1252-1257): for every
+ * Gaussian with radii > 0, max_radii2D = max(max_radii2D, radii); grad_accum_3vec += viewspace_grad;
+ * grad_accum += ||viewspace_grad[:2]||; denom += 1.  viewspace_grad (P,3) is dL/d means2D of the view. */
+int gsd_densify_stats(int32_t P, const float* viewspace_grad, const int32_t* radii, float* grad_accum,
+                      float* grad_accum_3vec, float* denom, float* max_radii2D, void* stream);
+
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead
  * per launch); gsd_timing_collect() synchronises on the last recorded event

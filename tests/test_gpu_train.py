@@ -88,3 +88,69 @@ def test_fused_adam_matches_torch_adam():
         assert pa.data_ptr() >= opt_a.param_slab.data_ptr()
         assert rel_l2(pa.detach(), pb.detach()) <= 1e-6
         assert float((pa - pb).abs().max()) <= 1e-6
+
+
+def test_densify_and_prune_matches_reference():
+    """gsd_amd.densify (fused statistics kernel + FusedAdam slab surgery) vs the line-by-line restatement of
+    scene/gaussian_model.py's densification on torch.optim.Adam (oracle/densify_ref.py): statistics after three
+    views, then densify_and_prune (clone + split with the same torch.normal draws + prune), reset_opacity and
+    one more optimizer step -- same point count, parameters, moments and statistics."""
+    from gsd_amd import DeformableGaussians
+    from gsd_amd.densify import GaussianDensifier
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    from oracle.densify_ref import RefGaussians
+    P = 4000
+    prm = make_gaussians(P, 320, 240, seed=21, device=DEV)
+    lrs = [0.00016, 0.0025, 0.0025 / 20.0, 0.05, 0.005, 0.001]
+    pc = DeformableGaussians(prm, sh_degree=3)
+    ps = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+    opt = FusedAdam([{"params": [p], "lr": lr, "name": n} for p, lr, n in
+                     zip(ps, lrs, ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"])], lr=0.0, eps=1e-15)
+    dens = GaussianDensifier(pc, opt)
+    ref = RefGaussians(*(p.detach() for p in ps), lrs=lrs)
+    gen = torch.Generator().manual_seed(3)
+    extent = float(torch.exp(prm.scaling).max(dim=1).values.median()) / 0.01  # ~half the points split, half clone
+
+    def both_step():
+        gs = [torch.randn(p.shape, generator=gen).to(DEV) * 1e-3 for p in ps]
+        for p, g in zip(ps, gs):
+            p.grad.copy_(g)
+        for p, g in zip(ref.params(), gs):
+            p.grad = g.clone()
+        opt.step()
+        ref.optimizer.step()
+
+    def compare(tag):
+        assert pc._xyz.shape == ref._xyz.shape, tag
+        for a, b in zip(ps, ref.params()):
+            assert float((a.detach() - b.detach()).abs().max()) <= 1e-5, tag
+        for a, b in zip(ps, ref.params()):
+            m, v = opt.moments(a)
+            st = ref.optimizer.state[b]
+            assert float((m - st["exp_avg"]).abs().max()) <= 1e-6, tag
+            assert float((v - st["exp_avg_sq"]).abs().max()) <= 1e-9, tag
+        for n in ("xyz_gradient_accum", "xyz_gradient_accum_3vec", "denom", "max_radii2D"):
+            assert float((getattr(dens, n) - getattr(ref, n)).abs().max()) <= 1e-6, (tag, n)
+
+    both_step()
+    for _ in range(3):
+        vg = torch.randn(P, 3, generator=gen).to(DEV) * 2e-4
+        radii = torch.randint(0, 30, (P,), generator=gen, dtype=torch.int32).to(DEV)
+        holder = torch.zeros(P, 3, device=DEV, requires_grad=True)
+        holder.grad = vg
+        dens.add_densification_stats(holder, radii)
+        ref.add_stats(vg, radii)
+    compare("stats")
+    torch.cuda.manual_seed(11)
+    dens.densify_and_prune(2e-4, 0.05, extent, 20)
+    torch.cuda.manual_seed(11)
+    ref.densify_and_prune(2e-4, 0.05, extent, 20)
+    assert pc._xyz.shape[0] != P  # something was cloned / split / pruned
+    compare("densify_and_prune")
+    dens.reset_opacity()
+    ref.reset_opacity()
+    compare("reset_opacity")
+    ps[:] = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+    both_step()
+    compare("step after surgery")
