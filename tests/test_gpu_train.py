@@ -154,3 +154,46 @@ def test_densify_and_prune_matches_reference():
     ps[:] = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
     both_step()
     compare("step after surgery")
+
+
+def test_checkpoint_capture_restore_roundtrip(tmp_path):
+    """gsd_amd.io.capture / restore (gaussian_model.py:686-730): the tuple survives torch.save /
+    torch.load(weights_only=True), restores parameters, statistics and Adam moments into a fresh model, and
+    its optimizer state_dict loads into a torch.optim.Adam built with the reference's groups."""
+    from gsd_amd import DeformableGaussians
+    from gsd_amd.densify import GaussianDensifier
+    from gsd_amd.io import capture, restore
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    names = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
+    lrs = [0.00016, 0.0025, 0.0025 / 20.0, 0.05, 0.005, 0.001]
+
+    def model(seed):
+        pc = DeformableGaussians(make_gaussians(999, 64, 48, seed=seed, device=DEV), sh_degree=3)
+        ps = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+        opt = FusedAdam([{"params": [p], "lr": lr, "name": n} for p, lr, n in zip(ps, lrs, names)], eps=1e-15)
+        return pc, ps, opt, GaussianDensifier(pc, opt)
+
+    pc, ps, opt, dens = model(1)
+    gen = torch.Generator().manual_seed(2)
+    for _ in range(2):
+        for p in ps:
+            p.grad.copy_(torch.randn(p.shape, generator=gen).to(DEV))
+        opt.step()
+    dens.max_radii2D.fill_(3.0)
+    path = str(tmp_path / "chkpnt_2.pth")
+    torch.save((capture(pc, opt, dens, 1.5), 2), path)
+    model_args, it = torch.load(path, weights_only=True)
+    assert it == 2 and len(model_args) == 12
+    pc2, ps2, opt2, dens2 = model(9)
+    assert restore(model_args, pc2, opt2, dens2) == 1.5
+    for a, b in zip(ps, ps2):
+        assert torch.equal(a.detach(), b.detach())
+        for x, y in zip(opt.moments(a), opt2.moments(b)):
+            assert torch.equal(x, y)
+    assert opt2.step_count == 2 and torch.equal(dens2.max_radii2D, dens.max_radii2D)
+    ref_ps = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    ref = torch.optim.Adam([{"params": [p], "lr": lr, "name": n} for p, lr, n in zip(ref_ps, lrs, names)],
+                           lr=0.0, eps=1e-15)
+    ref.load_state_dict(model_args[10])
+    assert torch.equal(ref.state[ref_ps[2]]["exp_avg"], opt.moments(ps[2])[0])
