@@ -197,3 +197,32 @@ def test_checkpoint_capture_restore_roundtrip(tmp_path):
                            lr=0.0, eps=1e-15)
     ref.load_state_dict(model_args[10])
     assert torch.equal(ref.state[ref_ps[2]]["exp_avg"], opt.moments(ps[2])[0])
+
+
+def test_render_with_deformation_mlp():
+    """render() with the reference's deformation network as the offset producer (past its 3000-iteration
+    zero phase): the fused preamble + split-SH rasterizer and the reference-literal preamble give the same
+    image and the same gradients for the network's weights and the Gaussians."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    from gsd_amd.scene import make_gaussians
+    torch.manual_seed(0)
+    net = DirectTemporalNeRF().to(DEV)
+    with torch.no_grad():
+        for h in (net._time_out, net._time_out_scale, net._time_out_rot, net._time_out_shs):
+            h.weight.mul_(0.01)  # small offsets, like a trained network
+    params = make_gaussians(8000, 256, 192, seed=5, device=DEV)
+    cam = synthetic_camera(256, 192).to(DEV)
+    res = []
+    for fused in (True, False):
+        net.zero_grad(set_to_none=True)
+        pc = DeformableGaussians(params, sh_degree=3, offset_model=net)
+        pc.fused_preamble = fused
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV), iteration=5000)
+        (out["render"] * torch.linspace(0, 1, 256, device=DEV)).sum().backward()
+        res.append((out["render"].detach(), [p.grad.clone() for p in pc.parameters()],
+                    [p.grad.clone() for p in net.parameters()]))
+    assert (res[0][0] - res[1][0]).abs().max() <= 1e-5
+    for a, b in zip(res[0][1] + res[0][2], res[1][1] + res[1][2]):
+        assert rel_l2(a, b) <= 1e-4
