@@ -185,11 +185,12 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kAdam, kDensify, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kAdam, kDensify, kKnn, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
-                                               "activate_bwd",   "l1_ssim",      "adam",         "densify_stats"};
+                                               "activate_bwd",   "l1_ssim",      "adam",         "densify_stats",
+                                               "knn"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -589,6 +590,20 @@ int gsd_densify_stats(int32_t P, const float* viewspace_grad, const int32_t* rad
     timed(kDensify, s, [&] {
         gsd::launch_densify_stats(P, viewspace_grad, radii, grad_accum, grad_accum_3vec, denom, max_radii2D, s);
     });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+size_t gsd_knn_workspace_bytes(int32_t P) { return P > 0 ? gsd::knn_workspace(P, nullptr) : kAlign; }
+
+int gsd_knn_mean_dist2(int32_t P, const float* points, float* mean_dist2, void* workspace, void* stream) {
+    if (P < 0) return fail(GSD_ERR_ARG, "invalid P");
+    if (P == 0) return GSD_OK;
+    if (!points || !mean_dist2 || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
+    hipStream_t s = as_stream(stream);
+    int e = 0;
+    timed(kKnn, s, [&] { e = gsd::launch_knn(P, points, mean_dist2, workspace, s); });
+    if (e) return fail(GSD_ERR_HIP, std::string("knn sort: ") + hipGetErrorString((hipError_t)e));
     GSD_CHECK(false, s);
     return GSD_OK;
 }

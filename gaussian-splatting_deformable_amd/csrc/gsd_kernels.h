@@ -188,6 +188,9 @@ void launch_scatter_hist(const HistParams& p, const uint32_t* tile_base, const f
 void launch_densify_stats(int P, const float* vgrad, const int* radii, float* accum, float* accum3, float* denom,
                           float* max_radii, hipStream_t s);
 
+size_t knn_workspace(int P, size_t* sort_bytes);
+int launch_knn(int P, const float* pts, float* out, void* ws, hipStream_t s);
+
 constexpr int kAdamMaxGroups = 16;
 struct AdamArgs {
     long long n;                        // elements in the slabs

@@ -63,6 +63,8 @@ SIGNATURES = {
     "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32), _i64, _f32,
                              _f32, _f32, _i32, _vp]),
     "gsd_densify_stats": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_knn_workspace_bytes": (_sz, [_i32]),
+    "gsd_knn_mean_dist2": (_i32, [_i32, _vp, _vp, _vp, _vp]),
     "gsd_timing_enable": (_i32, [_i32]),
     "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "gsd_timing_reset": (None, []),

@@ -205,6 +205,13 @@ int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* e
 int gsd_densify_stats(int32_t P, const float* viewspace_grad, const int32_t* radii, float* grad_accum,
                       float* grad_accum_3vec, float* denom, float* max_radii2D, void* stream);
 
+/* Initial scales (simple-knn distCUDA2, submodules/simple-knn/simple_knn.cu:165-219, used by
+ * create_from_pcd, scene/gaussian_model.py:817): mean_dist2[i] = mean of the squared distances from point i
+ * to its 3 nearest other points.  points (P,3); workspace: gsd_knn_workspace_bytes(P) bytes of device memory
+ * (256-B aligned). */
+size_t gsd_knn_workspace_bytes(int32_t P);
+int gsd_knn_mean_dist2(int32_t P, const float* points, float* mean_dist2, void* workspace, void* stream);
+
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead
  * per launch); gsd_timing_collect() synchronises on the last recorded event

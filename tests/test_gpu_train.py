@@ -226,3 +226,23 @@ def test_render_with_deformation_mlp():
     assert (res[0][0] - res[1][0]).abs().max() <= 1e-5
     for a, b in zip(res[0][1] + res[0][2], res[1][1] + res[1][2]):
         assert rel_l2(a, b) <= 1e-4
+
+
+@pytest.mark.parametrize("P,dup", [(2, False), (5, False), (3000, False), (5000, True)])
+def test_knn_init_matches_bruteforce(P, dup):
+    """gsd_knn (simple-knn's Morton-box 3-NN, distCUDA2) bit-exact against the brute-force float32 restatement
+    (oracle/knn_ref.py), several boxes of 1024, duplicated points, fewer than 4 points; create_from_pcd."""
+    from gsd_amd.init import create_from_pcd, dist_cuda2
+    from oracle.knn_ref import mean_dist2
+    gen = torch.Generator().manual_seed(P)
+    pts = torch.randn(P, 3, generator=gen) * torch.tensor([3.0, 1.0, 0.5]) + 2.0
+    if dup:
+        pts[100:200] = pts[0:100]
+    got = dist_cuda2(pts.to(DEV)).cpu().numpy()
+    ref = mean_dist2(pts.numpy())
+    assert np.array_equal(got, ref) or (np.isinf(ref).any() and np.array_equal(np.isinf(got), np.isinf(ref)))
+    if P >= 4:
+        g = create_from_pcd(pts.to(DEV), torch.rand(P, 3, generator=gen).to(DEV))
+        assert g.features_dc.shape == (P, 1, 3) and g.features_rest.shape == (P, 15, 3)
+        assert torch.allclose(g.scaling[:, 0].cpu(), torch.log(torch.sqrt(torch.clamp_min(torch.from_numpy(ref),
+                                                                                            1e-7))))

@@ -84,3 +84,17 @@ def test_loss_oracle_matches_reference_fixture():
     x, y = torch.from_numpy(g["img1"]), torch.from_numpy(g["img2"])
     assert abs(float(loss_ref.l1_loss(x, y)) - float(g["l1"])) <= 1e-7
     assert abs(float(loss_ref.ssim(x, y)) - float(g["ssim"])) <= 1e-6
+
+
+def test_knn_oracle_against_scipy():
+    """oracle/knn_ref.py (distCUDA2 restatement) vs scipy's KD-tree 3-NN on a small cloud (float64 within
+    float32 rounding), plus the FLT_MAX padding below four points."""
+    import numpy as np
+    from scipy.spatial import cKDTree
+    from oracle.knn_ref import mean_dist2
+    rng = np.random.default_rng(0)
+    pts = rng.normal(size=(400, 3)).astype(np.float32)
+    d, _ = cKDTree(pts.astype(np.float64)).query(pts.astype(np.float64), k=4)
+    np.testing.assert_allclose(mean_dist2(pts), (d[:, 1:] ** 2).mean(1), rtol=1e-5)
+    assert np.isinf(mean_dist2(pts[:2])).all()
+    np.testing.assert_allclose(mean_dist2(pts[:3]), np.finfo(np.float32).max / 3, rtol=1e-6)
