@@ -55,7 +55,8 @@ def algorithmic_bytes(P, V, K, W, H, C):
         "render_fwd": 8 * T + 44 * K + 20 * npix,
         "render_bwd": 8 * T + 44 * K + 20 * npix + 44 * V,
         "preprocess_bwd": 4 * P + (85 + 12 * C) * V + (64 + 12 * C) * V,
-        "l1_ssim": 3 * npix * (8 + 12 + 20 + 4),
+        "l1_ssim": 3 * npix * (8 + 12),         # img, gt in; window adjoints out
+        "l1_ssim_bwd": 3 * npix * (12 + 8 + 4),  # adjoints, img, gt in; dL/dimg out
         "adam": 32 * P * (3 + 3 + 45 + 1 + 3 + 4),
     }
 

@@ -185,11 +185,11 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kAdam, kDensify, kKnn, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kAdam, kDensify, kKnn, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
-                                               "activate_bwd",   "l1_ssim",      "adam",         "densify_stats",
+                                               "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "adam",         "densify_stats",
                                                "knn"};
 struct TimingState {
     bool on = false;
@@ -286,7 +286,9 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
     const bool use_hist = hist_binning(T);
     if (!use_hist) GSD_HIP(hipMemsetAsync(im.tile_count, 0, sizeof(uint32_t) * T, s));
-    GSD_HIP(hipMemsetAsync(im.counters, 0, 16, s));
+    // counters[1] collects the prefiltered-culling error flag (set only when prefiltered, forward.cu:174-175);
+    // counters[0] is written by the tile scan
+    if (a->prefiltered) GSD_HIP(hipMemsetAsync(im.counters, 0, 16, s));
 
     gsd::PreprocessParams p{};
     p.P = a->P; p.D = a->D; p.M = a->M; p.W = a->width; p.H = a->height; p.grid_x = gx; p.grid_y = gy;
@@ -316,7 +318,7 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     if (!g_pinned) GSD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_pinned), 16, hipHostMallocDefault));
     GSD_HIP(hipMemcpyAsync(g_pinned, im.counters, 8, hipMemcpyDeviceToHost, s));
     GSD_HIP(hipStreamSynchronize(s));
-    if (g_pinned[1] & gsd::kErrPrefiltered)
+    if (a->prefiltered && (g_pinned[1] & gsd::kErrPrefiltered))
         return fail(GSD_ERR_ARG, "Point is filtered although prefiltered is set. This shouldn't happen!");
     *num_rendered = (int64_t)g_pinned[0];
     return GSD_OK;
@@ -529,22 +531,44 @@ size_t gsd_l1_ssim_workspace_bytes(int32_t C, int32_t H, int32_t W) {
     return carve_loss(nullptr, C, H, W, nullptr);
 }
 
-int gsd_l1_ssim(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim, float* out3,
-                float* dL_dimg, void* workspace, void* stream) {
-    if (C <= 0 || H <= 0 || W <= 0) return fail(GSD_ERR_ARG, "image must be (C,H,W) with positive sizes");
-    if (!img || !gt || !out3 || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
-    if ((size_t)C * H * W >= (1ull << 31)) return fail(GSD_ERR_ARG, "image too large");
+static void ssim_window(float (&w)[11]) {
     // utils/loss_utils.py:23-25: gaussian(11, 1.5), float32 exp values normalised by their float32 sum
-    float w[11], sum = 0.f;
+    float sum = 0.f;
     for (int k = 0; k < 11; ++k) {
         w[k] = (float)std::exp(-(double)((k - 5) * (k - 5)) / (2.0 * 1.5 * 1.5));
         sum += w[k];
     }
     for (int k = 0; k < 11; ++k) w[k] = w[k] / sum;
+}
+
+int gsd_l1_ssim(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim, float* out3,
+                float* dL_dimg, void* workspace, void* stream) {
+    if (C <= 0 || H <= 0 || W <= 0) return fail(GSD_ERR_ARG, "image must be (C,H,W) with positive sizes");
+    if (!img || !gt || !out3 || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
+    if ((size_t)C * H * W >= (1ull << 31)) return fail(GSD_ERR_ARG, "image too large");
+    float w[11];
+    ssim_window(w);
     LossWs ws;
     carve_loss(workspace, C, H, W, &ws);
     hipStream_t s = as_stream(stream);
     timed(kLoss, s, [&] { gsd::launch_l1_ssim(C, H, W, w, lambda_dssim, img, gt, ws.gmaps, ws.partial, out3, dL_dimg, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim,
+                         const float* grad_out, float sign, float* dL_dimg, const void* workspace, void* stream) {
+    if (C <= 0 || H <= 0 || W <= 0) return fail(GSD_ERR_ARG, "image must be (C,H,W) with positive sizes");
+    if (!img || !gt || !dL_dimg || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
+    if ((size_t)C * H * W >= (1ull << 31)) return fail(GSD_ERR_ARG, "image too large");
+    float w[11];
+    ssim_window(w);
+    LossWs ws;
+    carve_loss(const_cast<void*>(workspace), C, H, W, &ws);
+    hipStream_t s = as_stream(stream);
+    timed(kLossBwd, s, [&] {
+        gsd::launch_l1_ssim_bwd(C, H, W, w, lambda_dssim, img, gt, ws.gmaps, grad_out, sign, dL_dimg, s);
+    });
     GSD_CHECK(false, s);
     return GSD_OK;
 }

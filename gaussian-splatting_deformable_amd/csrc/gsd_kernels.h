@@ -206,6 +206,8 @@ void launch_adam(const AdamArgs& a, float* param, float* grad, float* m, float* 
 void ssim_tiles(int H, int W, int* tiles_x, int* tiles_y);
 void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
                     float* gmaps, float* partial, float* out3, float* dimg, hipStream_t s);
+void launch_l1_ssim_bwd(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
+                        const float* gmaps, const float* gscale, float sign, float* dimg, hipStream_t s);
 
 constexpr int kHistThreads = 512;       // LDS-histogram binning workgroup
 constexpr int kHistMaxTiles = 40960;    // 160 KiB of u32 bins; larger grids use global-atomic binning

@@ -157,6 +157,7 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
 __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const float* __restrict__ img,
                                                              const float* __restrict__ gt,
                                                              const float* __restrict__ gmaps,
+                                                             const float* __restrict__ gscale, float sign,
                                                              float* __restrict__ dimg) {
     __shared__ float sg[3][kSsimIn][kSsimIn];
     __shared__ float sh[3][kSsimIn][kSsimTile];
@@ -182,6 +183,7 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
     }
     __syncthreads();
     const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimRows;
+    const float g = gscale ? sign * gscale[0] : sign;  // d out / d loss (autograd's incoming gradient)
     float acc[3][kSsimRows];
 #pragma unroll
     for (int q = 0; q < 3; ++q)
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
         const float x = img[o], y = gt[o];
         const float diff = x - y;
         const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
-        dimg[o] = acc[0][j] + 2.f * x * acc[1][j] + y * acc[2][j] + p.coef_l1 * sgn;
+        dimg[o] = g * (acc[0][j] + 2.f * x * acc[1][j] + y * acc[2][j] + p.coef_l1 * sgn);
     }
 }
 
@@ -239,8 +241,7 @@ void ssim_tiles(int H, int W, int* tx, int* ty) {
     *ty = (H + kSsimTile - 1) / kSsimTile;
 }
 
-void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
-                    float* gmaps, float* partial, float* out3, float* dimg, hipStream_t s) {
+static SsimArgs ssim_args(int C, int H, int W, const float* w11, float lambda) {
     SsimArgs p{};
     p.C = C; p.H = H; p.W = W;
     ssim_tiles(H, W, &p.tiles_x, &p.tiles_y);
@@ -248,11 +249,27 @@ void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const f
     const double n = (double)C * H * W;
     p.coef_ssim = (float)(-lambda / n);
     p.coef_l1 = (float)((1.0 - lambda) / n);
+    return p;
+}
+
+void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
+                    float* gmaps, float* partial, float* out3, float* dimg, hipStream_t s) {
+    const SsimArgs p = ssim_args(C, H, W, w11, lambda);
+    const double n = (double)C * H * W;
     const dim3 grid(p.tiles_x, p.tiles_y, C);
     hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, partial);
     hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, p.tiles_x * p.tiles_y * C, partial, (float)(1.0 / n),
                        lambda, out3);
-    if (dimg) hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, dimg);
+    if (dimg)
+        hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, (const float*)nullptr, 1.0f,
+                           dimg);
+}
+
+void launch_l1_ssim_bwd(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
+                        const float* gmaps, const float* gscale, float sign, float* dimg, hipStream_t s) {
+    const SsimArgs p = ssim_args(C, H, W, w11, lambda);
+    const dim3 grid(p.tiles_x, p.tiles_y, C);
+    hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, gscale, sign, dimg);
 }
 
 }  // namespace gsd

@@ -336,10 +336,51 @@ __device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&d
     for (int k = K0; k < K1; ++k) dst[k - K0] = old[k - K0] + ds[k];
 }
 
+// SH gradient entries [from, M) x 3 of one Gaussian: the coefficients above the active degree get zero
+// gradients (and all of them for a skipped Gaussian), as in the reference's zero-initialised dL_dsh.
+// Accumulating split sinks are left untouched.
+__device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int idx, int from) {
+    if (p.dL_dsh) {
+        for (int k = 3 * from; k < p.M * 3; ++k) p.dL_dsh[(size_t)idx * p.M * 3 + k] = 0.f;
+    } else if (!p.sh_accumulate) {
+        if (p.dsh_dc && from == 0)
+            for (int k = 0; k < 3; ++k) p.dsh_dc[(size_t)idx * 3 + k] = 0.f;
+        if (p.dsh_rest)
+            for (int k = 3 * (from > 1 ? from - 1 : 0); k < (p.M - 1) * 3; ++k)
+                p.dsh_rest[(size_t)idx * (p.M - 1) * 3 + k] = 0.f;
+        if (p.dsh_off)
+            for (int k = 3 * from; k < p.M * 3; ++k) p.dsh_off[(size_t)idx * p.M * 3 + k] = 0.f;
+    }
+}
+
+// Gradients of a Gaussian the backward skips (radii == 0): every per-Gaussian output is written, so callers need
+// not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  Accumulating SH
+// sinks are left untouched.
+__device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx) {
+    p.dL_dmeans3D[3 * idx] = 0.f;
+    p.dL_dmeans3D[3 * idx + 1] = 0.f;
+    p.dL_dmeans3D[3 * idx + 2] = 0.f;
+    if (p.dL_dcov3D) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = 0.f;
+    }
+    if (p.dL_dscales) {
+        p.dL_dscales[3 * idx] = 0.f;
+        p.dL_dscales[3 * idx + 1] = 0.f;
+        p.dL_dscales[3 * idx + 2] = 0.f;
+    }
+    if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0);
+}
+
 template <int DEG>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= p.P || !(p.radii[idx] > 0)) return;
+    if (idx >= p.P) return;
+    if (!(p.radii[idx] > 0)) {  // backward.cu:359-360 skips it; its gradients are the zeros torch::zeros holds
+        zero_outputs(p, idx);
+        return;
+    }
     const Mat4 Vm = load_mat4(p.view);
     const Mat4 Pm = load_mat4(p.proj);
     const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
@@ -407,6 +448,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
             if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + (size_t)idx * (p.M - 1) * 3, ds, acc);
             if (p.dsh_off) sink_sh<0, nc * 3>(p.dsh_off + (size_t)idx * p.M * 3, ds, acc);
         }
+        if (p.M > nc) zero_sh_tail(p, idx, nc);
         // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
         const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
                                         gx.z * dc.x + gy.z * dc.y + gz.z * dc.z);
@@ -417,15 +459,15 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     p.dL_dmeans3D[3 * idx + 1] = dmean.y;
     p.dL_dmeans3D[3 * idx + 2] = dmean.z;
 
-    if (p.scales) {
-        float3 dscale;
-        float4 drot;
-        cov3d_bwd(scale, p.scale_modifier, q, dcov, dscale, drot);
+    float3 dscale = make_float3(0.f, 0.f, 0.f);
+    float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.scales) cov3d_bwd(scale, p.scale_modifier, q, dcov, dscale, drot);
+    if (p.dL_dscales) {
         p.dL_dscales[3 * idx] = dscale.x;
         p.dL_dscales[3 * idx + 1] = dscale.y;
         p.dL_dscales[3 * idx + 2] = dscale.z;
-        reinterpret_cast<float4*>(p.dL_drotations)[idx] = drot;
     }
+    if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = drot;
 }
 
 }  // namespace gsd

@@ -38,6 +38,25 @@ def _dev_f32(t: torch.Tensor, name: str, dev: torch.device) -> torch.Tensor:
     return t.contiguous()
 
 
+_MATS = {}
+
+
+def _dev_mat(t: torch.Tensor, name: str, dev: torch.device) -> torch.Tensor:
+    """_dev_f32 for the small per-camera tensors (view / projection matrices, camera centre).  The reference's
+    Camera stores its matrices transposed (non-contiguous, scene/cameras.py), so the contiguous copy is cached per
+    tensor object and version instead of being remade (one copy kernel each) at every call."""
+    if t.is_contiguous():
+        return _dev_f32(t, name, dev)
+    e = _MATS.get(id(t))
+    if e is not None and e[0] is t and e[1] == t._version:
+        return e[2]
+    c = _dev_f32(t, name, dev)
+    if len(_MATS) >= 64:
+        _MATS.clear()
+    _MATS[id(t)] = (t, t._version, c)   # holds t, so its id is not reused while cached
+    return c
+
+
 def _ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
@@ -81,9 +100,9 @@ class _Args:
         self.scales = None if _absent(scales) else _dev_f32(scales, "scales", dev)
         self.rotations = None if _absent(rotations) else _dev_f32(rotations, "rotations", dev)
         self.cov3D = None if _absent(cov3D_precomp) else _dev_f32(cov3D_precomp, "cov3D_precomp", dev)
-        self.view = _dev_f32(viewmatrix, "viewmatrix", dev)
-        self.proj = _dev_f32(projmatrix, "projmatrix", dev)
-        self.campos = _dev_f32(campos, "campos", dev)
+        self.view = _dev_mat(viewmatrix, "viewmatrix", dev)
+        self.proj = _dev_mat(projmatrix, "projmatrix", dev)
+        self.campos = _dev_mat(campos, "campos", dev)
         self.M = 0 if self.sh is None else int(self.sh.size(1))  # rasterize_points.cu:83-87
         self.sh_split = sh_split
         if sh_split is not None:
@@ -114,7 +133,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
               projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
               sh_split)
     dev, P, H, W = a.dev, a.P, a.H, a.W
-    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)   # preprocess writes every entry (forward.cu:174)
     byte = dict(dtype=torch.uint8, device=dev)
     if P == 0:
         empty = torch.empty(0, **byte)
@@ -149,15 +168,19 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dev, P, M = a.dev, a.P, a.M
     split = sh_split is not None
     want_cov = not split or a.cov3D is not None
-    # one zero-filled slab for every gradient (a single memset instead of nine);
-    # the float4-accessed arrays (conic, rotation) first so they stay 16-B aligned
-    widths = [4, 4, 3, 3, 1, 3, 6 if want_cov else 0, 0 if split else M * 3, 3]
-    slab = torch.zeros(P * sum(widths), dtype=torch.float32, device=dev)
-    views, off = [], 0
-    for w in widths:
-        views.append(slab[off:off + P * w].view(P, w) if w else None)
-        off += P * w
-    dconic, drot, dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales = views
+    # two slabs: the per-pixel atomic accumulation targets, zero-filled with a single memset, and the per-Gaussian
+    # outputs the backward writes for every Gaussian (zeros where radii == 0), left unfilled; the float4-accessed
+    # arrays (conic, rotation) come first so they stay 16-B aligned
+    acc_w = [4, 3, 3, 1]
+    out_w = [4, 3, 6 if want_cov else 0, 0 if split else M * 3, 3]
+    views = []
+    for fill, widths in ((torch.zeros, acc_w), (torch.empty, out_w)):
+        slab = fill(P * sum(widths), dtype=torch.float32, device=dev)
+        off = 0
+        for w in widths:
+            views.append(slab[off:off + P * w].view(P, w) if w else None)
+            off += P * w
+    dconic, dmeans2D, dcolors, dopacity, drot, dmeans3D, dcov3D, dsh, dscales = views
     if dsh is not None:
         dsh = dsh.view(P, M, 3)
     if P != 0:

@@ -60,6 +60,7 @@ SIGNATURES = {
     "gsd_activate_backward": (_i32, [_i32, _i32, _i32] + [_vp] * 20 + [_vp]),
     "gsd_l1_ssim_workspace_bytes": (_sz, [_i32, _i32, _i32]),
     "gsd_l1_ssim": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gsd_l1_ssim_backward": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _f32, _vp, _vp, _vp]),
     "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32), _i64, _f32,
                              _f32, _f32, _i32, _vp]),
     "gsd_densify_stats": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

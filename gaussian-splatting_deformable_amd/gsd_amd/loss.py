@@ -3,8 +3,8 @@
 Mirrors ``utils/loss_utils.py``: ``l1_loss`` (:17-18), ``ssim`` (:33-63: 11x11 Gaussian window,
 sigma 1.5, zero padding, C1 = 0.01^2, C2 = 0.03^2, mean over the map) and the combination of
 ``train.py:529``: ``(1 - lambda_dssim) * L1 + lambda_dssim * (1 - SSIM)`` with lambda_dssim = 0.2
-(``arguments/__init__.py:83``).  One kernel pass computes the value and d loss / d image; the gradient
-is kept for the backward, which only scales it.  Images are (C,H,W) (or (1,C,H,W)) float32 on a HIP
+(``arguments/__init__.py:83``).  The forward computes the value and keeps the SSIM window adjoints; the
+backward (gsd_l1_ssim_backward) turns them into d loss / d image, scaled by autograd's incoming gradient.  Images are (C,H,W) (or (1,C,H,W)) float32 on a HIP
 device.  No CPU path.
 """
 from __future__ import annotations
@@ -17,8 +17,7 @@ from . import _native
 from ._C import _dev_f32, _ptr, _stream
 
 
-def _run(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float, want_grad: bool):
-    lib = _native.load()
+def _check(img: torch.Tensor, gt: torch.Tensor):
     if img.dim() == 4 and img.size(0) == 1:
         img, gt = img[0], gt[0]
     if img.dim() != 3 or img.shape != gt.shape:
@@ -27,31 +26,47 @@ def _run(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float, want_grad: bo
     dev = img.device
     if dev.type != "cuda":
         raise RuntimeError("l1_ssim: images must be HIP device tensors (there is no CPU implementation)")
-    x = _dev_f32(img.detach(), "image", dev)
-    y = _dev_f32(gt.detach(), "gt", dev)
+    return _dev_f32(img.detach(), "image", dev), _dev_f32(gt.detach(), "gt", dev)
+
+
+def _run(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float):
+    """Forward: {loss, L1, SSIM} (device) and the workspace holding the window adjoints the backward reads."""
+    lib = _native.load()
+    x, y = _check(img, gt)
+    dev = x.device
     C, H, W = (int(s) for s in x.shape)
     ws = torch.empty(lib.gsd_l1_ssim_workspace_bytes(C, H, W), dtype=torch.uint8, device=dev)
     out3 = torch.empty(3, dtype=torch.float32, device=dev)
-    dimg = torch.empty_like(x) if want_grad else None
     with torch.cuda.device(dev):
-        _native.check(lib.gsd_l1_ssim(C, H, W, _ptr(x), _ptr(y), ctypes.c_float(lambda_dssim), _ptr(out3), _ptr(dimg),
+        _native.check(lib.gsd_l1_ssim(C, H, W, _ptr(x), _ptr(y), ctypes.c_float(lambda_dssim), _ptr(out3), None,
                                       _ptr(ws), _stream(dev)))
-    return out3, dimg
+    return out3, x, y, ws
 
 
 class _L1Ssim(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, gt, lambda_dssim, which):
-        out3, dimg = _run(img, gt, lambda_dssim, img.requires_grad)
+        out3, x, y, ws = _run(img, gt, lambda_dssim)
         ctx.shape = img.shape
+        ctx.lambda_dssim = lambda_dssim
         ctx.sign = -1.0 if which == 2 else 1.0  # ssim() returns SSIM = 1 - loss(lambda = 1)
-        ctx.save_for_backward(dimg if dimg is not None else torch.empty(0))
+        ctx.save_for_backward(x, y, ws)
         return out3[which]
 
     @staticmethod
     def backward(ctx, g):
-        (dimg,) = ctx.saved_tensors
-        return (dimg * (g * ctx.sign)).view(ctx.shape), None, None, None
+        # the incoming gradient scales d loss / d img inside the kernel (no separate multiply)
+        x, y, ws = ctx.saved_tensors
+        lib = _native.load()
+        dev = x.device
+        C, H, W = (int(s) for s in x.shape)
+        gs = _dev_f32(g.reshape(1), "grad", dev)
+        dimg = torch.empty_like(x)
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_l1_ssim_backward(C, H, W, _ptr(x), _ptr(y), ctypes.c_float(ctx.lambda_dssim),
+                                                   _ptr(gs), ctypes.c_float(ctx.sign), _ptr(dimg), _ptr(ws),
+                                                   _stream(dev)))
+        return dimg.view(ctx.shape), None, None, None
 
 
 def l1_ssim_loss(image: torch.Tensor, gt: torch.Tensor, lambda_dssim: float = 0.2) -> torch.Tensor:

@@ -104,6 +104,8 @@ class _RasterizeSplitSH(torch.autograd.Function):
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.has_offset = sh_offset is not None
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)   # no zero-filled int32 gradient for radii
         ctx.params = (f_dc, f_rest)
         ctx.save_for_backward(means3D, scales, rotations, radii, f_dc, f_rest,
                               sh_offset if sh_offset is not None else torch.empty(0), geomBuffer, binningBuffer,
@@ -113,6 +115,8 @@ class _RasterizeSplitSH(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, _):
         from .activate import _sinks
+        if grad_out_color is None:
+            return (None,) * 9
         rs = ctx.raster_settings
         means3D, scales, rotations, radii, f_dc, f_rest, sh_offset, geomBuffer, binningBuffer, imgBuffer = \
             ctx.saved_tensors

@@ -159,15 +159,58 @@ def se3_rot_or(pc, rot_offset, se3_rotations):
     return pc.rotation_activation(pc._rotation + rot_offset)
 
 
+_ZEROS = {}
+
+
+def _zeros(P, w, like):
+    """A cached all-zero (P, w) float32 buffer on like's device, never written by this package."""
+    key = (like.device, P, w)
+    z = _ZEROS.get(key)
+    if z is None:
+        if len(_ZEROS) > 16:
+            _ZEROS.clear()
+        z = _ZEROS[key] = torch.zeros(P, w, dtype=torch.float32, device=like.device)
+    return z
+
+
+class RenderPackage(dict):
+    """render()'s returned dict; "visibility_filter" (radii > 0) is computed the first time it is read."""
+
+    def __missing__(self, key):
+        if key == "visibility_filter":
+            v = self["radii"] > 0
+            self[key] = v
+            return v
+        raise KeyError(key)
+
+    def __contains__(self, key):
+        return key == "visibility_filter" or dict.__contains__(self, key)
+
+
+class _Time:
+    """The (P, 1) time tensor of gaussian_renderer/__init__.py:87, built only if a deformation model reads it."""
+
+    def __init__(self, P, t, dev):
+        self.P, self.t, self.dev, self.v = P, t, dev, None
+
+    def get(self):
+        if self.v is None:
+            self.v = torch.full((self.P, 1), self.t, device=self.dev)
+        return self.v
+
+
+def _time_for(model, tm):
+    return None if model is None or isinstance(model, ZeroOffsets) else tm.get()
+
+
 def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1.0, override_color=None,
            save_ply=False, control_time=None):
     """gaussian_renderer/__init__.py:20-195."""
     dev = pc.get_xyz.device
-    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True, device=dev) + 0
-    try:
-        screenspace_points.retain_grad()
-    except Exception:
-        pass
+    # the reference's zeros_like(xyz, requires_grad=True) + 0 with retain_grad(): a zero tensor whose .grad
+    # receives dL/d means2D.  The rasterizer never reads its values, so it is a fresh leaf on a cached zero
+    # buffer (no fill, no add, and autograd stores the gradient without the retain_grad copy).
+    screenspace_points = _zeros(pc.get_xyz.shape[0], 3, pc.get_xyz).detach().requires_grad_(True)
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
     raster_settings = GaussianRasterizationSettings(
@@ -179,7 +222,7 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     means3D = pc.get_xyz
     t = control_time if control_time is not None else viewpoint_camera.time
-    time = torch.full((means3D.size(0), 1), t, device=means3D.device)
+    tm = _Time(means3D.size(0), t, means3D.device)
     means2D = screenspace_points
     python_modes = (getattr(pipe, "compute_cov3D_python", False) or getattr(pipe, "convert_SHs_python", False)
                     or override_color is not None)
@@ -187,35 +230,37 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
         # fused preamble: offsets + activations in one HIP pass (gsd_amd.activate); the SH are not
         # concatenated -- the rasterizer reads features_dc / features_rest / the SH offset in place
         P = means3D.size(0)
-        dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, time, iteration)
+        dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, _time_for(pc.offset_model, tm), iteration)
         dsh = None if mlp_shs is None else mlp_shs.reshape(P, -1, 3)
         means3D, scales, rotations, opacity = activate_split_sh(pc._xyz, pc._scaling, pc._rotation, pc._opacity, dx,
                                                                 scale_offset, rot_offset)
         if getattr(pc, "deform", "additive") == "se3":
             # one fused kernel moves means AND rotations by the same rigid motion
-            means3D, rotations = se3_deform(pc.get_twist(pc.get_xyz, time, iteration), means3D, rotations)
+            means3D, rotations = se3_deform(pc.get_twist(pc.get_xyz, _time_for(pc.twist_model, tm), iteration),
+                                            means3D, rotations)
         means3D_ori = pc._xyz
         moved = dx is not None or getattr(pc, "deform", "additive") == "se3"
-        means3D_offset = means3D - means3D_ori if moved else torch.zeros_like(means3D_ori)
-        rot_offset = rot_offset if rot_offset is not None else means3D.new_zeros(P, 4)
+        # zero offsets are read-only expanded views of a cached zero row (in-place writes raise)
+        means3D_offset = means3D - means3D_ori if moved else _zeros(1, 3, means3D).expand(P, 3)
+        rot_offset = rot_offset if rot_offset is not None else _zeros(1, 4, means3D).expand(P, 4)
         rendered_image, radii = rasterize_gaussians_split_sh(means3D, means2D, pc._features_dc, pc._features_rest,
                                                              dsh, opacity, scales, rotations, raster_settings)
-        return {"render": rendered_image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
-                "radii": radii, "means3D": means3D, "means3D_ori": means3D_ori, "rotations": rotations,
-                "means3D_offset": means3D_offset, "opacities": opacity, "rot_offset": rot_offset}
+        return RenderPackage(render=rendered_image, viewspace_points=screenspace_points, radii=radii,
+                             means3D=means3D, means3D_ori=means3D_ori, rotations=rotations,
+                             means3D_offset=means3D_offset, opacities=opacity, rot_offset=rot_offset)
     # reference-literal path (Python covariance / SH modes, override colours)
     se3_rot = getattr(pc, "deform", "additive") == "se3" and not getattr(pipe, "compute_cov3D_python", False)
     if se3_rot:
-        dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, time, iteration)
+        dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, tm.get(), iteration)
         P = means3D.size(0)
         dx, scale_offset = _zeros_if_none(dx, P, 3, pc._xyz), _zeros_if_none(scale_offset, P, 3, pc._xyz)
         rot_offset, mlp_shs = _zeros_if_none(rot_offset, P, 4, pc._xyz), _zeros_if_none(mlp_shs, P, 48, pc._xyz)
-        twist = pc.get_twist(means3D, time, iteration)
+        twist = pc.get_twist(means3D, tm.get(), iteration)
         means3D_ori = pc._xyz
         means3D, se3_rotations = se3_deform(twist, pc._xyz + dx, pc.rotation_activation(pc._rotation + rot_offset))
         means3D_offset = means3D - means3D_ori
     else:
-        means3D, means3D_ori, means3D_offset, scale_offset, rot_offset, mlp_shs = pc.get_xyz_all(means3D, time,
+        means3D, means3D_ori, means3D_offset, scale_offset, rot_offset, mlp_shs = pc.get_xyz_all(means3D, tm.get(),
                                                                                                  iteration)
     opacity = pc.get_opacity
     scales = rotations = cov3D_precomp = None

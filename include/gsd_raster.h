@@ -128,12 +128,15 @@ int gsd_rasterize_forward_render(const gsd_raster_args* args, void* geom_buffer,
                                  void* binning_buffer, int64_t num_rendered, const int32_t* radii,
                                  float* out_color, void* stream);
 
-/* Backward (rasterizer_impl.cu:340-434).  Output arrays must be zero-filled
- * by the caller (torch::zeros upstream, rasterize_points.cu:151-159):
- * dL_dmeans2D (P,3), dL_dcolors (P,3), dL_dopacity (P,1), dL_dmeans3D (P,3),
- * dL_dcov3D (P,6), dL_dsh (P,M,3) (may be NULL if M == 0), dL_dscales (P,3),
- * dL_drotations (P,4), and the scratch dL_dconic (P,4) (float4 view of (P,2,2)).
- * With args->sh_split set, dL_dsh is not used (the split sinks receive dL/dSH);
+/* Backward (rasterizer_impl.cu:340-434).  The per-pixel accumulation targets
+ * dL_dmeans2D (P,3), dL_dcolors (P,3), dL_dopacity (P,1) and the scratch
+ * dL_dconic (P,4) (float4 view of (P,2,2)) must be zero-filled by the caller
+ * (torch::zeros upstream, rasterize_points.cu:151-159).  The per-Gaussian
+ * outputs dL_dmeans3D (P,3), dL_dcov3D (P,6), dL_dsh (P,M,3) (may be NULL if
+ * M == 0), dL_dscales (P,3) and dL_drotations (P,4) are written for every
+ * Gaussian (zeros where radii == 0 and above the active SH degree), so they
+ * need no fill.  With args->sh_split set, dL_dsh is not used (the split sinks
+ * receive dL/dSH; with accumulate != 0 only visible Gaussians' entries change);
  * dL_dcov3D may be NULL when cov3D_precomp is NULL (it is then not written). */
 int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, const void* geom_buffer,
                            const void* binning_buffer, const void* image_buffer, int64_t num_rendered,
@@ -189,6 +192,13 @@ int gsd_activate_backward(int32_t P, int32_t R, int32_t accumulate, const float*
 size_t gsd_l1_ssim_workspace_bytes(int32_t C, int32_t H, int32_t W);
 int gsd_l1_ssim(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim,
                 float* out3, float* dL_dimg, void* workspace, void* stream);
+
+/* Backward of gsd_l1_ssim, split from it so the incoming autograd gradient scales d loss / d img inside the
+ * kernel: dL_dimg = sign * grad_out[0] * d out3[0] / d img (grad_out: one device float, NULL => 1).  workspace
+ * must hold what gsd_l1_ssim wrote for the same (img, gt, lambda_dssim) (its window adjoints).  sign = -1 turns
+ * the loss gradient at lambda_dssim = 1 into the gradient of SSIM itself (utils/loss_utils.py:33 ssim). */
+int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim,
+                         const float* grad_out, float sign, float* dL_dimg, const void* workspace, void* stream);
 
 /* One Adam step (torch.optim.Adam semantics as configured in scene/gaussian_model.py:839-856: per-group
  * learning rate, betas, eps 1e-15, no weight decay / amsgrad) over flat slabs of n floats: param, grad,

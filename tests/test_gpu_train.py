@@ -44,6 +44,22 @@ def test_l1_ssim_value_and_grad(C, H, W, lam):
     assert rel_l2(x1.grad, x2.grad) <= 1e-4
 
 
+def test_loss_backward_scaled_and_composed():
+    """The backward scales d loss / d img by autograd's incoming gradient inside the kernel: a weighted sum of
+    l1_loss, ssim and l1_ssim_loss (train.py:529 written out by hand) against the restatement."""
+    from gsd_amd.loss import l1_loss, l1_ssim_loss, ssim
+    from oracle import loss_ref
+    gen = torch.Generator().manual_seed(7)
+    gt = torch.rand(3, 70, 90, generator=gen).to(DEV)
+    base = (gt + 0.1 * torch.randn(3, 70, 90, generator=gen).to(DEV)).clamp(0, 1)
+    x1 = base.clone().requires_grad_(True)
+    x2 = base.clone().requires_grad_(True)
+    (0.8 * l1_loss(x1, gt) + 0.2 * (1.0 - ssim(x1, gt)) - 2.5 * l1_ssim_loss(x1, gt, 0.3)).backward()
+    (0.8 * loss_ref.l1_loss(x2, gt) + 0.2 * (1.0 - loss_ref.ssim(x2, gt))
+     - 2.5 * loss_ref.l1_ssim_loss(x2, gt, 0.3)).backward()
+    assert rel_l2(x1.grad, x2.grad) <= 1e-4
+
+
 def test_identical_images_and_batched_input():
     from gsd_amd.loss import l1_ssim_loss, ssim
     x = torch.rand(1, 3, 50, 70, generator=torch.Generator().manual_seed(1)).to(DEV).requires_grad_(True)
