@@ -240,6 +240,9 @@ const char* gsd_last_error(void) { return g_err.c_str(); }
 size_t gsd_geom_buffer_bytes(int32_t P, int32_t width, int32_t height) {
     return carve_geom(nullptr, (size_t)(P < 0 ? 0 : P), grid_tiles(width, height), nullptr);
 }
+size_t gsd_backward_scratch_bytes(int32_t P) {
+    return up(sizeof(float) * gsd::kGradRec * (size_t)(P < 0 ? 0 : P)) + kAlign;
+}
 size_t gsd_image_buffer_bytes(int32_t width, int32_t height) {
     const size_t gx = (size_t)(width + gsd::kTileX - 1) / gsd::kTileX, gy = (size_t)(height + gsd::kTileY - 1) / gsd::kTileY;
     return carve_img(nullptr, (size_t)width * (size_t)height, gx * gy, nullptr);
@@ -368,7 +371,7 @@ int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, vo
 
 int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const void* geom_buffer,
                            const void* binning_buffer, const void* image_buffer, int64_t K,
-                           const float* dL_dout_color, float* dL_dmeans2D, float* dL_dconic, float* dL_dopacity,
+                           const float* dL_dout_color, float* dL_dmeans2D, void* scratch, float* dL_dopacity,
                            float* dL_dcolors, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
                            float* dL_dscales, float* dL_drotations, void* stream) {
     int rc = validate(a, false);
@@ -376,7 +379,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     if (a->P == 0) return GSD_OK;
     if (!geom_buffer || !image_buffer || (K > 0 && !binning_buffer))
         return fail(GSD_ERR_STATE, "state buffers from the matching forward are required");
-    if (!dL_dout_color || !dL_dmeans2D || !dL_dconic || !dL_dopacity || !dL_dcolors || !dL_dmeans3D ||
+    if (!dL_dout_color || !dL_dmeans2D || !scratch || !dL_dopacity || !dL_dcolors || !dL_dmeans3D ||
         (a->cov3D_precomp && !dL_dcov3D))
         return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
     if ((a->shs && !dL_dsh) || (a->scales && (!dL_dscales || !dL_drotations)))
@@ -394,8 +397,11 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
     rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
     rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
-    rp.dL_dpix = dL_dout_color; rp.dL_dmean2D = dL_dmeans2D; rp.dL_dconic = dL_dconic;
-    rp.dL_dopacity = dL_dopacity; rp.dL_dcolors = dL_dcolors;
+    rp.dL_dpix = dL_dout_color;
+    // the per-Gaussian gradient records (scratch) start at zero; render_bwd adds into them
+    float* rec = reinterpret_cast<float*>(align_ptr(scratch));
+    rp.grad_rec = rec;
+    GSD_HIP(hipMemsetAsync(rec, 0, sizeof(float) * gsd::kGradRec * (size_t)a->P, s));
     if (K > 0) {
         timed(kRenderBwd, s, [&] { gsd::launch_render_bwd(rp, s); });
         GSD_CHECK(a->debug, s);
@@ -408,7 +414,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     p.means3D = a->means3D; p.radii = radii ? radii : g.radii; p.shs = a->shs; p.clamped = g.clamped;
     p.scales = a->scales; p.rotations = a->rotations; p.cov3D_precomp = a->cov3D_precomp;
     p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
-    p.dL_dmean2D = dL_dmeans2D; p.dL_dconic = dL_dconic; p.dL_dcolor = dL_dcolors;
+    p.grad_rec = rec; p.dL_dmean2D = dL_dmeans2D; p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolors;
     p.dL_dmeans3D = dL_dmeans3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = dL_dsh; p.dL_dscales = dL_dscales;
     p.dL_drotations = dL_drotations;
     if (const gsd_sh_split* sp = a->sh_split) {

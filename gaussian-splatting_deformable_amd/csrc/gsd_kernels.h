@@ -42,6 +42,11 @@ struct PreprocessParams {
     uint32_t* err_flags;
 };
 
+// Per-Gaussian gradient record of the rasterizer backward: 16 floats (one 64-B segment, the memory-side
+// unit of a global atomic) holding dL/dmean2D x,y | dL/dconic a,b,c | dL/dopacity | dL/dcolor r,g,b.
+constexpr int kGradRec = 16;
+enum GradRecField { kRecMean2D = 0, kRecConic = 2, kRecOpacity = 5, kRecColor = 6, kRecUsed = 9 };
+
 struct PreprocessBwdParams {
     int P, D, M;
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
@@ -58,9 +63,10 @@ struct PreprocessBwdParams {
     const float* view;
     const float* proj;
     const float* campos;
-    const float* dL_dmean2D;  // (P,3)
-    const float* dL_dconic;   // (P,4)
-    const float* dL_dcolor;   // (P,3)
+    const float* grad_rec;    // (P, kGradRec) per-Gaussian gradient records accumulated by k_render_bwd
+    float* dL_dmean2D;        // (P,3) outputs unpacked from the records (written for every Gaussian)
+    float* dL_dopacity;       // (P)
+    float* dL_dcolor;         // (P,3)
     float* dL_dmeans3D;
     float* dL_dcov3D;
     float* dL_dsh;
@@ -114,10 +120,7 @@ struct RenderBwdParams {
     const float* final_T;
     const uint32_t* n_contrib;
     const float* dL_dpix;
-    float* dL_dmean2D;  // (P,3)
-    float* dL_dconic;   // (P,4)
-    float* dL_dopacity; // (P)
-    float* dL_dcolors;  // (P,3)
+    float* grad_rec;    // (P, kGradRec), zeroed before the launch
 };
 
 struct ActivateParams {

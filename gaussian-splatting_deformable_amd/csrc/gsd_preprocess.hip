@@ -357,6 +357,17 @@ __device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int i
 // not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  Accumulating SH
 // sinks are left untouched.
 __device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx) {
+    if (p.dL_dmean2D) {
+        p.dL_dmean2D[3 * idx] = 0.f;
+        p.dL_dmean2D[3 * idx + 1] = 0.f;
+        p.dL_dmean2D[3 * idx + 2] = 0.f;
+    }
+    if (p.dL_dopacity) p.dL_dopacity[idx] = 0.f;
+    if (p.dL_dcolor) {
+        p.dL_dcolor[3 * idx] = 0.f;
+        p.dL_dcolor[3 * idx + 1] = 0.f;
+        p.dL_dcolor[3 * idx + 2] = 0.f;
+    }
     p.dL_dmeans3D[3 * idx] = 0.f;
     p.dL_dmeans3D[3 * idx + 1] = 0.f;
     p.dL_dmeans3D[3 * idx + 2] = 0.f;
@@ -397,7 +408,23 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         q = reinterpret_cast<const float4*>(p.rotations)[idx];
         c3 = cov3d_from_scale_rot(scale, p.scale_modifier, q);
     }
-    const float4 dcon4 = reinterpret_cast<const float4*>(p.dL_dconic)[idx];
+    // the rasterizer's per-Gaussian record: unpack the API outputs (rasterize_points.cu:180-188) and use it
+    const float4* rec4 = reinterpret_cast<const float4*>(p.grad_rec + (size_t)idx * kGradRec);
+    const float4 r0 = rec4[0], r1 = rec4[1];
+    const float r8 = p.grad_rec[(size_t)idx * kGradRec + 8];
+    // r0 = (mean2D x, mean2D y, conic a, conic b), r1 = (conic c, opacity, color r, color g), r8 = color b
+    if (p.dL_dmean2D) {
+        p.dL_dmean2D[3 * idx] = r0.x;
+        p.dL_dmean2D[3 * idx + 1] = r0.y;
+        p.dL_dmean2D[3 * idx + 2] = 0.f;
+    }
+    if (p.dL_dopacity) p.dL_dopacity[idx] = r1.y;
+    if (p.dL_dcolor) {
+        p.dL_dcolor[3 * idx] = r1.z;
+        p.dL_dcolor[3 * idx + 1] = r1.w;
+        p.dL_dcolor[3 * idx + 2] = r8;
+    }
+    const float4 dcon4 = make_float4(r0.z, r0.w, 0.f, r1.x);
     float3 dmean;
     Cov6 dcov;
     cov2d_bwd(m, c3, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, Vm, make_float3(dcon4.x, dcon4.y, dcon4.w), dmean,
@@ -413,7 +440,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     const float* P = Pm.m;
     const float mul1 = (P[0] * m.x + P[4] * m.y + P[8] * m.z + P[12]) * mw * mw;
     const float mul2 = (P[1] * m.x + P[5] * m.y + P[9] * m.z + P[13]) * mw * mw;
-    const float d2x = p.dL_dmean2D[3 * idx], d2y = p.dL_dmean2D[3 * idx + 1];
+    const float d2x = r0.x, d2y = r0.y;
     float3 dm2;
     dm2.x = (P[0] * mw - P[3] * mul1) * d2x + (P[1] * mw - P[3] * mul2) * d2y;
     dm2.y = (P[4] * mw - P[7] * mul1) * d2x + (P[5] * mw - P[7] * mul2) * d2y;
@@ -426,9 +453,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         const float len = sqrtf(dot3(dir_orig, dir_orig));
         const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
         const uint8_t cl = p.clamped[idx];
-        const float3 dc = make_float3(p.dL_dcolor[3 * idx] * ((cl & 1) ? 0 : 1),
-                                      p.dL_dcolor[3 * idx + 1] * ((cl & 2) ? 0 : 1),
-                                      p.dL_dcolor[3 * idx + 2] * ((cl & 4) ? 0 : 1));
+        const float3 dc = make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r8 * ((cl & 4) ? 0 : 1));
         constexpr int nc = (DEG + 1) * (DEG + 1);
         float s[48];
         load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s);

@@ -106,10 +106,13 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
 }
 
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
-// Shared by both passes so their skip decisions are identical.
-// exp via the hardware 2^x (v_exp_f32, 1 ulp) on power * log2(e): <= ~5 ulp over the range that matters
+// Shared by both passes so their skip decisions are identical.  power is evaluated exactly as the
+// reference writes it (no contraction), so alpha differs from the reference only through exp:
+// the hardware 2^x (v_exp_f32, 1 ulp) on power * log2(e), <= ~5 ulp over the range that matters
 // (power in [-12, 0]), against ~10 VALU ops for the libm-accurate expf.  Results stay inside the image /
-// n_contrib tolerances of DESIGN.md 4; GSD_PRECISE_EXP restores expf.
+// n_contrib tolerances of DESIGN.md 4; GSD_PRECISE_EXP restores expf.  (Carrying log2(e) in the staged
+// conic and contracting power to FMAs saves 4 ops but moves alpha across the 1/255 threshold for some
+// pixels: image errors of 2e-3 at 400x400.)
 __device__ __forceinline__ float gauss_exp(float power) {
 #ifdef GSD_PRECISE_EXP
     return expf(power);
@@ -117,9 +120,10 @@ __device__ __forceinline__ float gauss_exp(float power) {
     return __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
 #endif
 }
-
-__device__ __forceinline__ float record_alpha(float2 xy, float4 co, float pxf, float pyf, float& G) {
-    const float dx = xy.x - pxf, dy = xy.y - pyf;
+__device__ __forceinline__ float record_alpha(float2 xy, float4 co, float pxf, float pyf, float& G, float& dx,
+                                              float& dy) {
+    dx = xy.x - pxf;
+    dy = xy.y - pyf;
     const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
     G = gauss_exp(power);
     return power > 0.0f ? 0.0f : fminf(0.99f, co.w * G);
@@ -194,8 +198,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 slot[u] = list[min(j0 + u, m - 1)];
-                float G;
-                a[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, G);
+                float G, dx, dy;
+                a[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, G, dx, dy);
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
 #pragma unroll
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float4 s_box[kTilePix];
-    __shared__ float s_acc[9][kTilePix];
+    __shared__ float s_acc[9][kTilePix + 1];  // +1: a record's nine sums sit in nine different banks
     __shared__ uint8_t s_list[4][kTilePix];
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
@@ -267,8 +271,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         dpix1 = p.dL_dpix[plane + pid];
         dpix2 = p.dL_dpix[2 * plane + pid];
     }
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;  // accum_rec (with last_color / last_alpha folded in)
+    float adot = 0.f;  // accum_rec . dL/dpixel (accum_rec with last_color / last_alpha folded in)
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
+    const float kbg = -T_final * bg_dot;
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
@@ -295,60 +300,57 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         const int m = wave_compact<true>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
         for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
             // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
-            float Gs[kBwdBatch], As[kBwdBatch];
+            float Gs[kBwdBatch], As[kBwdBatch], Os[kBwdBatch], Dx[kBwdBatch], Dy[kBwdBatch];
             int slot[kBwdBatch];
 #pragma unroll
             for (int u = 0; u < kBwdBatch; ++u) {
                 slot[u] = list[min(j0 + u, m - 1)];
-                As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u]);
+                const float4 co = s_co[slot[u]];
+                As[u] = record_alpha(s_xy[slot[u]], co, pxf, pyf, Gs[u], Dx[u], Dy[u]);
+                Os[u] = co.w;
             }
             // ... then the sequential back-to-front recurrence (backward.cu:482-555), branch-free: a record
             // a lane skips (past its last contributor, alpha < 1/255, or beyond the list) gets alpha = G = 0,
-            // which leaves T unchanged (1/(1-0) == 1 exactly) and zeroes its partials.  accum_rec is folded
-            // forward at the end of each record (acc = alpha c + (1-alpha) acc) rather than at the start of
-            // the next contributing one (backward.cu:516-520): the same operations on the same values, and a
-            // skipped record (alpha = 0) leaves it unchanged without a select.
-            // Partials are scaled after the reduction (it is linear): v0 by -W/2, v1 by -H/2, v2..v4 by -1/2,
-            // applied once per (record, tile) in the flush below.  Records 0/1 and 2/3 are folded across the
-            // wave halves as soon as each pair exists (pair32), so at most 27 partials are live.
+            // which leaves T unchanged (1/(1-0) == 1 exactly) and zeroes its partials.
+            // accum_rec only enters through (c - accum_rec) . dL/dpixel, so the lane keeps the scalar
+            // adot = accum_rec . dL/dpixel, folded forward at the end of each record (accum_rec = alpha c +
+            // (1-alpha) accum_rec, backward.cu:516-520, dotted with dL/dpixel): one FMA instead of six ops.
+            // The mean2D / conic partials are reduced as the moments q dx, q dy, q dx^2, q dx dy, q dy^2
+            // (q = o G dL/dalpha); the flush below turns them into dL/dmean2D = (a, b; b, c) (q dx, q dy)
+            // (-W/2, -H/2) and dL/dconic = -1/2 (q dx^2, q dx dy, q dy^2) -- linear, so exact up to rounding,
+            // and 5 ops per record instead of 12.  Records 0/1 and 2/3 are folded across the wave halves as
+            // soon as each pair exists (pair32), so at most 27 partials are live.
             float h[2][9], v[9], prev[9];
             bool any = false;
 #pragma unroll
             for (int u = 0; u < kBwdBatch; ++u) {
                 // gradient arithmetic has no bit-exact contract: let the compiler fuse to FMA
 #pragma clang fp contract(fast)
-                const bool valid = inside && j0 + u < m && front_base - slot[u] < last_contributor &&
-                                   As[u] >= 1.0f / 255.0f;
+                // non-short-circuit (&): straight-line selects instead of exec-mask branches.  A pixel outside
+                // the image has last_contributor 0, and a slot's list position is >= 0, so `inside` is implied.
+                const bool valid = (j0 + u < m) & (front_base - slot[u] < last_contributor) &
+                                   (As[u] >= 1.0f / 255.0f);
                 any |= valid;
                 const float alpha = valid ? As[u] : 0.f;
                 const float G = valid ? Gs[u] : 0.f;
-                const float2 xy = s_xy[slot[u]];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float4 co = s_co[slot[u]];
                 const float inv1ma = fast_recip(1.f - alpha);
                 T = T * inv1ma;  // backward.cu:503 (T recovered by division)
-                const float dchannel_dcolor = alpha * T;
+                const float aT = alpha * T;
                 const float4 c = s_rgb[slot[u]];
-                float dL_dalpha = (c.x - acc0) * dpix0;
-                dL_dalpha += (c.y - acc1) * dpix1;
-                dL_dalpha += (c.z - acc2) * dpix2;
-                v[6] = dchannel_dcolor * dpix0;
-                v[7] = dchannel_dcolor * dpix1;
-                v[8] = dchannel_dcolor * dpix2;
-                dL_dalpha *= T;
-                dL_dalpha += (-T_final * inv1ma) * bg_dot;
-                // backward.cu:530-554 with q = G dL/dG: dL/dmean2D = q (conic . d) (-W/2, -H/2),
-                // dL/dconic = q (dx^2, dx dy, dy^2) (-1/2), dL/dopacity = G dL/dalpha
+                const float cd = c.x * dpix0 + c.y * dpix1 + c.z * dpix2;
+                const float diff = cd - adot;
+                const float dL_dalpha = diff * T + kbg * inv1ma;  // backward.cu:512-529
+                v[6] = aT * dpix0;
+                v[7] = aT * dpix1;
+                v[8] = aT * dpix2;
                 v[5] = G * dL_dalpha;
-                const float q = co.w * v[5];
-                v[0] = q * (dx * co.x + dy * co.y);
-                v[1] = q * (dy * co.z + dx * co.y);
-                v[2] = q * (dx * dx);
-                v[3] = q * (dx * dy);
-                v[4] = q * (dy * dy);
-                acc0 = alpha * c.x + (1.f - alpha) * acc0;
-                acc1 = alpha * c.y + (1.f - alpha) * acc1;
-                acc2 = alpha * c.z + (1.f - alpha) * acc2;
+                const float q = Os[u] * v[5];
+                v[0] = q * Dx[u];
+                v[1] = q * Dy[u];
+                v[2] = v[0] * Dx[u];
+                v[3] = v[0] * Dy[u];
+                v[4] = v[1] * Dy[u];
+                adot = fmaf(alpha, diff, adot);
 #pragma unroll
                 for (int k = 0; k < 9; ++k) {
                     if (u & 1)
@@ -371,20 +373,23 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             }
         }
         lds_barrier();
-        if (tid < n) {
-            const uint32_t g = s_id[tid];
-            const float a0 = s_acc[0][tid] * -ddelx_dx, a1 = s_acc[1][tid] * -ddely_dy,
-                        a2 = -0.5f * s_acc[2][tid], a3 = -0.5f * s_acc[3][tid], a4 = -0.5f * s_acc[4][tid],
-                        a5 = s_acc[5][tid], a6 = s_acc[6][tid], a7 = s_acc[7][tid], a8 = s_acc[8][tid];
-            if (a0 != 0.f) atomicAdd(p.dL_dmean2D + 3 * g, a0);
-            if (a1 != 0.f) atomicAdd(p.dL_dmean2D + 3 * g + 1, a1);
-            if (a2 != 0.f) atomicAdd(p.dL_dconic + 4 * g, a2);
-            if (a3 != 0.f) atomicAdd(p.dL_dconic + 4 * g + 1, a3);
-            if (a4 != 0.f) atomicAdd(p.dL_dconic + 4 * g + 3, a4);
-            if (a5 != 0.f) atomicAdd(p.dL_dopacity + g, a5);
-            if (a6 != 0.f) atomicAdd(p.dL_dcolors + 3 * g, a6);
-            if (a7 != 0.f) atomicAdd(p.dL_dcolors + 3 * g + 1, a7);
-            if (a8 != 0.f) atomicAdd(p.dL_dcolors + 3 * g + 2, a8);
+        if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
+            const float4 co = s_co[tid];
+            const float m0 = s_acc[0][tid], m1 = s_acc[1][tid];
+            s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
+            s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
+            s_acc[2][tid] *= -0.5f;
+            s_acc[3][tid] *= -0.5f;
+            s_acc[4][tid] *= -0.5f;
+        }
+        lds_barrier();
+        // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,
+        // each inside one 64-B segment of its Gaussian's gradient record -- ~7 memory-side atomic requests
+        // instead of 64 when every lane adds one quantity of a different Gaussian (0.43 of 1.16 ms).
+        for (int e = tid; e < n * kRecUsed; e += kTilePix) {
+            const int r = e / kRecUsed, q = e - kRecUsed * r;
+            const float a = s_acc[q][r];
+            if (a != 0.f) atomicAdd(p.grad_rec + (size_t)s_id[r] * kGradRec + q, a);
         }
     }
 }

@@ -168,19 +168,16 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dev, P, M = a.dev, a.P, a.M
     split = sh_split is not None
     want_cov = not split or a.cov3D is not None
-    # two slabs: the per-pixel atomic accumulation targets, zero-filled with a single memset, and the per-Gaussian
-    # outputs the backward writes for every Gaussian (zeros where radii == 0), left unfilled; the float4-accessed
-    # arrays (conic, rotation) come first so they stay 16-B aligned
-    acc_w = [4, 3, 3, 1]
-    out_w = [4, 3, 6 if want_cov else 0, 0 if split else M * 3, 3]
-    views = []
-    for fill, widths in ((torch.zeros, acc_w), (torch.empty, out_w)):
-        slab = fill(P * sum(widths), dtype=torch.float32, device=dev)
-        off = 0
-        for w in widths:
-            views.append(slab[off:off + P * w].view(P, w) if w else None)
-            off += P * w
-    dconic, dmeans2D, dcolors, dopacity, drot, dmeans3D, dcov3D, dsh, dscales = views
+    # every output is written by the backward for every Gaussian, so one unfilled slab holds them all (the
+    # float4-accessed rotation first, 16-B aligned); the library zeroes its own scratch (the gradient records)
+    widths = [4, 3, 3, 1, 3, 6 if want_cov else 0, 0 if split else M * 3, 3]
+    slab = torch.empty(P * sum(widths), dtype=torch.float32, device=dev)
+    views, off = [], 0
+    for w in widths:
+        views.append(slab[off:off + P * w].view(P, w) if w else None)
+        off += P * w
+    drot, dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales = views
+    scratch = torch.empty(lib.gsd_backward_scratch_bytes(P), dtype=torch.uint8, device=dev)
     if dsh is not None:
         dsh = dsh.view(P, M, 3)
     if P != 0:
@@ -189,7 +186,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         with torch.cuda.device(dev):
             _native.check(lib.gsd_rasterize_backward(
                 ctypes.byref(a.c), _ptr(radii_c), _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer), int(R),
-                _ptr(dout), _ptr(dmeans2D), _ptr(dconic), _ptr(dopacity), _ptr(dcolors), _ptr(dmeans3D),
+                _ptr(dout), _ptr(dmeans2D), _ptr(scratch), _ptr(dopacity), _ptr(dcolors), _ptr(dmeans3D),
                 _ptr(dcov3D), _ptr(dsh if M else None), _ptr(dscales), _ptr(drot), _stream(dev)))
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
 

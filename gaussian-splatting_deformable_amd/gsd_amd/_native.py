@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -46,6 +46,7 @@ SIGNATURES = {
     "gsd_last_error": (ctypes.c_char_p, []),
     "gsd_geom_buffer_bytes": (_sz, [_i32, _i32, _i32]),
     "gsd_image_buffer_bytes": (_sz, [_i32, _i32]),
+    "gsd_backward_scratch_bytes": (_sz, [_i32]),
     "gsd_binning_buffer_bytes": (_sz, [_i64]),
     "gsd_state_layout": (None, [_i32, _i32, _i32, _i64, ctypes.POINTER(_sz), ctypes.POINTER(_sz),
                                 ctypes.POINTER(_sz)]),

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 3
+#define GSD_ABI_VERSION 4
 
 enum {
     GSD_OK = 0,
@@ -128,19 +128,22 @@ int gsd_rasterize_forward_render(const gsd_raster_args* args, void* geom_buffer,
                                  void* binning_buffer, int64_t num_rendered, const int32_t* radii,
                                  float* out_color, void* stream);
 
-/* Backward (rasterizer_impl.cu:340-434).  The per-pixel accumulation targets
- * dL_dmeans2D (P,3), dL_dcolors (P,3), dL_dopacity (P,1) and the scratch
- * dL_dconic (P,4) (float4 view of (P,2,2)) must be zero-filled by the caller
- * (torch::zeros upstream, rasterize_points.cu:151-159).  The per-Gaussian
- * outputs dL_dmeans3D (P,3), dL_dcov3D (P,6), dL_dsh (P,M,3) (may be NULL if
- * M == 0), dL_dscales (P,3) and dL_drotations (P,4) are written for every
- * Gaussian (zeros where radii == 0 and above the active SH degree), so they
- * need no fill.  With args->sh_split set, dL_dsh is not used (the split sinks
- * receive dL/dSH; with accumulate != 0 only visible Gaussians' entries change);
- * dL_dcov3D may be NULL when cov3D_precomp is NULL (it is then not written). */
+/* Backward (rasterizer_impl.cu:340-434).  Every output is written for every
+ * Gaussian (zeros where radii == 0 and above the active SH degree), so none
+ * needs a fill: dL_dmeans2D (P,3), dL_dcolors (P,3), dL_dopacity (P,1),
+ * dL_dmeans3D (P,3), dL_dcov3D (P,6), dL_dsh (P,M,3) (may be NULL if M == 0),
+ * dL_dscales (P,3), dL_drotations (P,4).  scratch holds
+ * gsd_backward_scratch_bytes(P) bytes of device memory (replacing the
+ * reference's dL_dconic2D temporary, rasterize_points.cu:153): the call zeroes
+ * it and accumulates the per-pixel gradients there, one 64-B record per
+ * Gaussian (dL/dmean2D, dL/dconic, dL/dopacity, dL/dcolor).
+ * With args->sh_split set, dL_dsh is not used (the split sinks receive dL/dSH;
+ * with accumulate != 0 only visible Gaussians' entries change); dL_dcov3D may
+ * be NULL when cov3D_precomp is NULL (it is then not written). */
+size_t gsd_backward_scratch_bytes(int32_t P);
 int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, const void* geom_buffer,
                            const void* binning_buffer, const void* image_buffer, int64_t num_rendered,
-                           const float* dL_dout_color, float* dL_dmeans2D, float* dL_dconic,
+                           const float* dL_dout_color, float* dL_dmeans2D, void* scratch,
                            float* dL_dopacity, float* dL_dcolors, float* dL_dmeans3D, float* dL_dcov3D,
                            float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream);
 
