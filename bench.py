@@ -201,6 +201,7 @@ def main():
     # fwd+bwd ms/view: render + loss + backward of one view (no optimizer / collective),
     # hipEvents on the current stream, median over >= 100 views
     times = []
+    flat.invalidate()
     for _ in range(max(100, args.steps)):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -209,7 +210,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
-        flat.zero()
+        flat.invalidate()   # as after the optimizer step: the next backward stores into the slab
     times.sort()
     fwd_bwd_ms = times[len(times) // 2]
 

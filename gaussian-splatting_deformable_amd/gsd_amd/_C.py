@@ -274,7 +274,7 @@ def activate_forward(xyz, scaling, rotation, opacity, f_dc, f_rest, dxyz=None, d
 
 
 def activate_backward(scaling, rotation, opacity, dscale, drot, g_means, g_scales, g_rot, g_opac, g_shs, sinks,
-                      has_off, rest_shape):
+                      has_off, rest_shape, accumulate=True):
     """Backward of activate_forward.  sinks: None, or the parameter .grad buffers to add into in place
     (6, or 4 when the SH were left split: rest_shape None).
     -> ((g_xyz, g_scaling, g_rotation, g_opacity, g_fdc, g_frest), (g_dxyz, g_dscale, g_drot, g_dsh))."""
@@ -296,7 +296,7 @@ def activate_backward(scaling, rotation, opacity, dscale, drot, g_means, g_scale
         acc = 0
     else:
         outs = list(sinks) + ([None, None] if split else [])
-        acc = 1
+        acc = int(bool(accumulate))
     offg = [torch.empty(P, 3, device=dev) if has_off[0] else None,
             torch.empty(P, 3, device=dev) if has_off[1] else None,
             torch.empty(P, 4, device=dev) if has_off[2] else None,

@@ -19,10 +19,16 @@ from . import _C
 
 def _sinks(params):
     """Parameters registered as in-place gradient owners (FlatGrads sets _gsd_inplace_grad) get their .grad
-    updated by the kernels; anything else (e.g. torch.autograd.grad calls) gets returned grads."""
+    updated by the kernels; anything else (e.g. torch.autograd.grad calls) gets returned grads.
+    -> (sinks or None, accumulate): accumulate False means the views were stale and are stored into."""
     sinks = [p.grad if (getattr(p, "_gsd_inplace_grad", False) and p.grad is not None
                         and p.grad.is_contiguous() and p.grad.dtype == torch.float32) else None for p in params]
-    return sinks if all(s is not None for s in sinks) else None
+    if not all(s is not None for s in sinks):
+        return None, True
+    flats = {id(getattr(p, "_gsd_flat", None)): getattr(p, "_gsd_flat", None) for p in params}
+    if len(flats) == 1 and None not in flats.values():
+        return sinks, next(iter(flats.values())).claim(params)
+    return sinks, True
 
 
 class _Activate(torch.autograd.Function):
@@ -41,9 +47,9 @@ class _Activate(torch.autograd.Function):
         scaling, rotation, opacity, dscale, drot = ctx.saved_tensors
         dscale = dscale if ctx.has_off[1] else None
         drot = drot if ctx.has_off[2] else None
-        sinks = _sinks(ctx.params)
+        sinks, acc = _sinks(ctx.params)
         grads = _C.activate_backward(scaling, rotation, opacity, dscale, drot, g_means, g_scales, g_rot, g_opac, g_shs,
-                                     sinks, ctx.has_off, ctx.rest_shape)
+                                     sinks, ctx.has_off, ctx.rest_shape, accumulate=acc)
         g_params, g_offsets = grads
         if sinks is not None:
             g_params = (None,) * 6
@@ -70,10 +76,10 @@ class _ActivateSplitSH(torch.autograd.Function):
         scaling, rotation, opacity, dscale, drot = ctx.saved_tensors
         dscale = dscale if ctx.has_off[1] else None
         drot = drot if ctx.has_off[2] else None
-        sinks = _sinks(ctx.params)
+        sinks, acc = _sinks(ctx.params)
         (g_xyz, g_scaling, g_rotation, g_opacity, _, _), g_offsets = _C.activate_backward(
             scaling, rotation, opacity, dscale, drot, g_means, g_scales, g_rot, g_opac, None, sinks, ctx.has_off,
-            None)
+            None, accumulate=acc)
         g_params = (None,) * 4 if sinks is not None else (g_xyz, g_scaling, g_rotation, g_opacity)
         g_offsets = tuple(g if need else None for g, need in zip(g_offsets[:3], ctx.has_off[:3]))
         return (*g_params, *g_offsets)

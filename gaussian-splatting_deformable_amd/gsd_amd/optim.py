@@ -57,9 +57,12 @@ class FusedAdam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None, zero_grad: bool = False):
-        """One Adam step for every group; ``zero_grad`` also clears the gradient slab in the same pass."""
+        """One Adam step for every group.  ``zero_grad`` then marks the gradient slab stale instead of writing
+        zeros (FlatGrads.invalidate): the next backward stores into it, as after torch's
+        zero_grad(set_to_none=True)."""
         loss = closure() if closure is not None else None
         self.flat.collect()
+        self.flat.settle()
         self.step_count += 1
         g0 = self.param_groups[0]
         beta1, beta2 = g0["betas"]
@@ -70,9 +73,9 @@ class FusedAdam(torch.optim.Optimizer):
             _native.check(lib.gsd_adam_step(self.param_slab.numel(), _ptr(self.param_slab), _ptr(self.flat.slab),
                                             _ptr(self.exp_avg), _ptr(self.exp_avg_sq), len(self.param_groups),
                                             self._begin, lrs, self.step_count, beta1, beta2, float(g0["eps"]),
-                                            int(bool(zero_grad)), _stream(dev)))
+                                            0, _stream(dev)))
         if zero_grad:
-            self.flat.attach()
+            self.flat.invalidate()
         return loss
 
     def moments(self, p: torch.Tensor):
@@ -112,6 +115,7 @@ class FusedAdam(torch.optim.Optimizer):
             p.data = view
             off += n
         self.param_slab, self.exp_avg, self.exp_avg_sq = param_slab, exp_avg, exp_avg_sq
+        self.flat.remove_hooks()
         self.flat = FlatGrads(ps, device=dev)
         begins, off = [], 0
         for g in self.param_groups:

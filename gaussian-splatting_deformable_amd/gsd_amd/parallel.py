@@ -34,7 +34,14 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
 
 
 class FlatGrads:
-    """Owns one contiguous gradient slab; each parameter's .grad is a view of it."""
+    """Owns one contiguous gradient slab; each parameter's .grad is a view of it.
+
+    A parameter's view can be *stale* (``invalidate``: what the fused Adam step leaves instead of writing
+    zeros): its contents are a previous step's and the next gradient producer stores instead of adding --
+    torch's ``zero_grad(set_to_none=True)`` semantics (the first backward assigns, later ones accumulate)
+    without a memset.  The fused HIP backwards ask ``claim`` whether to store or add; any other producer
+    (autograd's AccumulateGrad) goes through a hook that zeroes a stale view first; a view still stale at
+    the optimizer step holds no gradient and is zeroed then."""
 
     def __init__(self, params, device=None):
         self.params = [p for p in params if p is not None]
@@ -47,16 +54,63 @@ class FlatGrads:
             v = self.slab[off:off + p.numel()].view_as(p)
             self.views.append(v)
             off += p.numel()
+        self.stale = set()
+        self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
+        self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
         self.attach()
+
+    def _before_accumulate(self, p):
+        def hook(grad):
+            if id(p) in self.stale:
+                self._view_of[id(p)].zero_()
+                self.stale.discard(id(p))
+            return grad
+        return hook
+
+    def remove_hooks(self):
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []
 
     def attach(self):
         for p, v in zip(self.params, self.views):
             p.grad = v
             p._gsd_inplace_grad = True  # fused HIP backwards may add into this .grad directly
+            p._gsd_flat = self
 
     def zero(self):
         self.slab.zero_()
+        self.stale.clear()
         self.attach()
+
+    def invalidate(self):
+        """Mark every view stale (no memory traffic): the next gradient producer stores instead of adding."""
+        self.stale = {id(p) for p in self.params}
+        self._version = self.slab._version
+
+    def claim(self, params) -> bool:
+        """A fused backward is about to produce the gradients of ``params`` in place: True = add into the
+        views, False = store (they were all stale).  A mix zeroes the stale ones and adds."""
+        ids = [id(p) for p in params]
+        fresh = [i for i in ids if i in self.stale]
+        if fresh and len(fresh) == len(ids):
+            self.stale.difference_update(ids)
+            return False
+        for i in fresh:
+            self._view_of[i].zero_()
+            self.stale.discard(i)
+        return True
+
+    def settle(self):
+        """Before the gradients are consumed: views nothing wrote since ``invalidate`` hold zero gradient --
+        unless no backward ran at all and the slab was written in place (gradients set by hand, e.g.
+        ``p.grad.copy_(g)``), which then stand as written."""
+        if len(self.stale) == len(self.params) and self.slab._version != getattr(self, "_version", None):
+            self.stale.clear()
+            return
+        for i in list(self.stale):
+            self._view_of[i].zero_()
+        self.stale.clear()
 
     def collect(self):
         """Copy any .grad autograd replaced (instead of accumulating in place) back into the slab."""
@@ -64,10 +118,12 @@ class FlatGrads:
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                 v.copy_(p.grad)
                 p.grad = v
+                self.stale.discard(id(p))
 
     def allreduce(self, op=None, async_op=False):
         """Sum the slab across ranks (no-op for world size 1)."""
         self.collect()
+        self.settle()
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return None
         return dist.all_reduce(self.slab, op=op or dist.ReduceOp.SUM, async_op=async_op)

@@ -120,7 +120,7 @@ class _RasterizeSplitSH(torch.autograd.Function):
         rs = ctx.raster_settings
         means3D, scales, rotations, radii, f_dc, f_rest, sh_offset, geomBuffer, binningBuffer, imgBuffer = \
             ctx.saved_tensors
-        sinks = _sinks(ctx.params)
+        sinks, acc = _sinks(ctx.params)
         if sinks is not None:
             d_dc, d_rest = sinks
         else:
@@ -129,7 +129,7 @@ class _RasterizeSplitSH(torch.autograd.Function):
         d_off = None
         if ctx.has_offset:
             d_off = torch.zeros(f_dc.size(0), 1 + f_rest.size(1), 3, device=f_dc.device)
-        split = _C.ShSplit(f_dc, f_rest, offset, d_dc, d_rest, d_off, accumulate=sinks is not None)
+        split = _C.ShSplit(f_dc, f_rest, offset, d_dc, d_rest, d_off, accumulate=sinks is not None and acc)
         g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
             rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
             rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,

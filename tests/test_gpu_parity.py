@@ -289,10 +289,12 @@ class _FixedOffsets:
 
 
 @pytest.mark.parametrize("offsets", [False, True])
-@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("inplace", [False, "zero", "stale"])
 def test_fused_preamble_render_matches_reference_path(offsets, inplace):
     """render(): fused HIP preamble + split-SH rasterizer vs the reference-literal torch preamble: same image,
-    parameter grads and offset grads, with plain autograd .grad or in-place FlatGrads accumulation."""
+    parameter grads and offset grads, with plain autograd .grad or in-place FlatGrads accumulation -- into a
+    zeroed slab, or into a stale one (after FlatGrads.invalidate, as the fused Adam step leaves it: the first
+    backward stores, the second adds)."""
     from gsd_amd import DeformableGaussians, default_pipe, render
     from gsd_amd.camera import synthetic_camera
     from gsd_amd.parallel import FlatGrads
@@ -306,6 +308,9 @@ def test_fused_preamble_render_matches_reference_path(offsets, inplace):
         pc = DeformableGaussians(params, sh_degree=3, offset_model=offs)
         pc.fused_preamble = fused
         flat = FlatGrads(pc.parameters()) if inplace else None
+        if inplace == "stale":
+            flat.slab.fill_(123.0)
+            flat.invalidate()
         for _ in range(2 if inplace else 1):  # twice: the in-place path must accumulate, not overwrite
             out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
             (out["render"] * torch.linspace(0, 1, 320, device=DEV)).sum().backward()
