@@ -199,20 +199,30 @@ def main():
     K_end = int(gsdC.last_forward.get("num_rendered", 0))
     restore()
     # fwd+bwd ms/view: render + loss + backward of one view (no optimizer / collective),
-    # hipEvents on the current stream, median over >= 100 views
-    times = []
-    flat.invalidate()
-    for _ in range(max(100, args.steps)):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        o = render(cam, pc, pipe, bg)
-        l1_ssim_loss(o["render"], target, 0.2).backward()
-        e1.record()
-        torch.cuda.synchronize()
-        times.append(e0.elapsed_time(e1))
-        flat.invalidate()   # as after the optimizer step: the next backward stores into the slab
-    times.sort()
-    fwd_bwd_ms = times[len(times) // 2]
+    # hipEvents on the current stream, median over >= 100 views, two ways:
+    #   queued  -- a ~1 ms spin kernel ahead of the first event holds the stream while the host enqueues the
+    #              view, so the time is the device's (the host still waits for num_rendered mid-forward, as the
+    #              reference does, and whatever it does after that read-back is on the clock);
+    #   synced  -- the host starts enqueueing after the first event: its Python prologue is on the clock too.
+    def fwd_bwd(queued):
+        ts = []
+        flat.invalidate()
+        for _ in range(max(100, args.steps)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if queued:
+                torch.cuda._sleep(2_000_000)
+            e0.record()
+            o = render(cam, pc, pipe, bg)
+            l1_ssim_loss(o["render"], target, 0.2).backward()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+            flat.invalidate()   # as after the optimizer step: the next backward stores into the slab
+        ts.sort()
+        return ts[len(ts) // 2]
+
+    fwd_bwd_ms = fwd_bwd(True)
+    fwd_bwd_synced_ms = fwd_bwd(False)
 
     # per-kernel device times: a separate pass of full steps with the C-ABI's hipEvent timing on
     restore()
@@ -262,6 +272,7 @@ def main():
                        "parallelism": f"dp{world}", "visible": V, "num_rendered": K,
                        "num_rendered_timed_first": K_start, "num_rendered_timed_last": K_end},
             "fwd_bwd_ms_per_view": round(fwd_bwd_ms, 4),
+            "fwd_bwd_ms_per_view_host_synced": round(fwd_bwd_synced_ms, 4),
             "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
             "roofline": roof,
             "cpu_baseline": cpu,

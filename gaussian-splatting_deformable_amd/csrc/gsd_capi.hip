@@ -369,6 +369,20 @@ int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, vo
     return GSD_OK;
 }
 
+int gsd_rasterize_forward(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, void* binning_buffer,
+                          size_t binning_bytes, int32_t* radii, float* out_color, int64_t* num_rendered,
+                          void* stream) {
+    int rc = gsd_rasterize_forward_bin(a, geom_buffer, image_buffer, radii, num_rendered, stream);
+    if (rc) return rc;
+    if (a->P == 0) return GSD_OK;
+    if (gsd_binning_buffer_bytes(*num_rendered) > binning_bytes) {
+        g_err = "binning buffer too small for num_rendered: allocate gsd_binning_buffer_bytes(num_rendered)";
+        return GSD_NEED_BINNING;
+    }
+    return gsd_rasterize_forward_render(a, geom_buffer, image_buffer, binning_buffer, *num_rendered, radii,
+                                        out_color, stream);
+}
+
 int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const void* geom_buffer,
                            const void* binning_buffer, const void* image_buffer, int64_t K,
                            const float* dL_dout_color, float* dL_dmeans2D, void* scratch, float* dL_dopacity,

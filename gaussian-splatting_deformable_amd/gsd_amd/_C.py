@@ -120,6 +120,9 @@ class _Args:
             sh_split=None if sh_split is None else ctypes.addressof(sh_split.c))
 
 
+_K_GUESS = {}   # device -> last num_rendered
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                         prefiltered, debug, sh_split=None):
@@ -142,15 +145,23 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         stream = _stream(dev)
         geom = torch.empty(lib.gsd_geom_buffer_bytes(P, W, H), **byte)
         img = torch.empty(lib.gsd_image_buffer_bytes(W, H), **byte)
-        K = _i64(0)
-        _native.check(lib.gsd_rasterize_forward_bin(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(radii),
-                                                    ctypes.byref(K), stream))
-        num_rendered = int(K.value)
-        last_forward.update(P=P, W=W, H=H, num_rendered=num_rendered)
-        binning = torch.empty(lib.gsd_binning_buffer_bytes(num_rendered), **byte)
         color = torch.empty(3, H, W, dtype=torch.float32, device=dev)
-        _native.check(lib.gsd_rasterize_forward_render(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(binning),
-                                                       num_rendered, _ptr(radii), _ptr(color), stream))
+        # the binning buffer is sized before num_rendered is known (the last count on this device plus
+        # headroom, or 4 instances per Gaussian), so both phases run in one native call and the device idles
+        # only for the count's read-back; a short buffer costs one more allocation and call
+        guess = max(_K_GUESS.get(dev, 4 * P), 1)
+        binning = torch.empty(lib.gsd_binning_buffer_bytes(guess + guess // 4), **byte)
+        K = _i64(0)
+        rc = lib.gsd_rasterize_forward(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(binning), binning.numel(),
+                                       _ptr(radii), _ptr(color), ctypes.byref(K), stream)
+        num_rendered = int(K.value)
+        if rc == _native.GSD_NEED_BINNING:
+            binning = torch.empty(lib.gsd_binning_buffer_bytes(num_rendered), **byte)
+            rc = lib.gsd_rasterize_forward_render(ctypes.byref(a.c), _ptr(geom), _ptr(img), _ptr(binning),
+                                                  num_rendered, _ptr(radii), _ptr(color), stream)
+        _native.check(rc)
+        _K_GUESS[dev] = num_rendered
+        last_forward.update(P=P, W=W, H=H, num_rendered=num_rendered)
     return num_rendered, color, radii, geom, binning, img
 
 

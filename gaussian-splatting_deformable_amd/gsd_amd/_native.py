@@ -52,6 +52,7 @@ SIGNATURES = {
                                 ctypes.POINTER(_sz)]),
     "gsd_rasterize_forward_bin": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "gsd_rasterize_forward_render": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "gsd_rasterize_forward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _sz, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "gsd_rasterize_backward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),
@@ -117,6 +118,9 @@ def load():
         raise ImportError(f"gsd: {LIB_PATH} has ABI {lib.gsd_abi_version()}, expected {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+GSD_NEED_BINNING = 4
 
 
 def check(rc: int) -> None:

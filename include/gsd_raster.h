@@ -49,7 +49,9 @@ enum {
     GSD_OK = 0,
     GSD_ERR_ARG = 1,     /* invalid argument (AT_ERROR / std::runtime_error upstream) */
     GSD_ERR_HIP = 2,     /* HIP runtime error (CHECK_CUDA upstream, auxiliary.h:166-173) */
-    GSD_ERR_STATE = 3    /* inconsistent state buffers (wrong size / wrong call order) */
+    GSD_ERR_STATE = 3,   /* inconsistent state buffers (wrong size / wrong call order) */
+    GSD_NEED_BINNING = 4 /* gsd_rasterize_forward: binning_buffer smaller than gsd_binning_buffer_bytes(
+                            *num_rendered); phase 1 is done -- allocate and call gsd_rasterize_forward_render */
 };
 
 /* Split SH operand (optional, ABI 3).  The reference's render() materialises
@@ -127,6 +129,15 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* args, void* geom_buffer, vo
 int gsd_rasterize_forward_render(const gsd_raster_args* args, void* geom_buffer, void* image_buffer,
                                  void* binning_buffer, int64_t num_rendered, const int32_t* radii,
                                  float* out_color, void* stream);
+
+/* Both forward phases in one call, for a caller that allocates the binning buffer before num_rendered is
+ * known (e.g. from the previous view's count plus headroom): phase 1, the num_rendered read-back, and -- when
+ * binning_bytes >= gsd_binning_buffer_bytes(*num_rendered) -- phase 2 without returning to the caller in
+ * between (the device idles only for the read-back, not for the caller's allocation and second call).
+ * Returns GSD_NEED_BINNING (phase 1 done, *num_rendered set) when the buffer is too small. */
+int gsd_rasterize_forward(const gsd_raster_args* args, void* geom_buffer, void* image_buffer, void* binning_buffer,
+                          size_t binning_bytes, int32_t* radii, float* out_color, int64_t* num_rendered,
+                          void* stream);
 
 /* Backward (rasterizer_impl.cu:340-434).  Every output is written for every
  * Gaussian (zeros where radii == 0 and above the active SH degree), so none

@@ -1,0 +1,26 @@
+#!/usr/bin/env python
+"""Idle gaps between consecutive kernels of a rocprofv3 kernel trace (one bench step, the last complete one
+between two Adam launches): prints each kernel's start offset, duration and the gap before it.
+    python scripts/trace_gaps.py gpurun_out/prof/bench_kernel_trace.csv"""
+import csv
+import sys
+
+
+def main(path):
+    r = sorted(csv.DictReader(open(path)), key=lambda x: int(x["Start_Timestamp"]))
+    idx = [i for i, x in enumerate(r) if "k_adam" in x["Kernel_Name"]]
+    a, b = idx[-2], idx[-1]
+    t_prev = int(r[a]["End_Timestamp"])
+    gaps = busy = 0
+    for x in r[a + 1:b + 1]:
+        s, e = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
+        gap = max(0, s - t_prev)
+        gaps += gap
+        busy += e - s
+        print(f"gap {gap / 1e3:7.1f} us  dur {(e - s) / 1e3:8.1f} us  {x['Kernel_Name'][:70]}")
+        t_prev = max(t_prev, e)
+    print(f"step: busy {busy / 1e3:.1f} us, gaps {gaps / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/bench_kernel_trace.csv")

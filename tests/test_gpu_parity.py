@@ -170,6 +170,16 @@ def test_dense_tile_merge_path(oracle_mod):
     assert counts.max() > 4096
 
 
+def test_binning_buffer_too_small_retries(oracle_mod):
+    """The binning buffer is sized from the previous count before the forward knows num_rendered; a short one
+    (GSD_NEED_BINNING) is re-allocated and phase 2 re-run -- same results as a well-sized one."""
+    from gsd_amd import _C
+    d = scene_inputs(6_000, 640, 360, 3, seed=4, device=DEV)
+    _C._K_GUESS[torch.device(DEV)] = 1
+    check_forward(oracle_mod, d)
+    assert _C._K_GUESS[torch.device(DEV)] > 1000
+
+
 def test_empty_and_culled():
     d = scene_inputs(100, 64, 64, 0, seed=1, device=DEV)
     d["means3D"] = d["means3D"] * torch.tensor([1.0, 1.0, -1.0], device=DEV)   # all behind the camera
