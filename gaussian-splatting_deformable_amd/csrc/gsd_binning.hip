@@ -241,9 +241,9 @@ __device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n
                 if ((r & j) == 0) {
                     const bool asc = (((t * E + r) & k) == 0);
                     const unsigned long long a = x[r], b = x[r | j];
-                    const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
-                    x[r] = asc ? lo : hi;
-                    x[r | j] = asc ? hi : lo;
+                    const bool swap = (b < a) == asc;
+                    x[r] = swap ? b : a;
+                    x[r | j] = swap ? a : b;
                 }
             }
         } else {
@@ -259,8 +259,7 @@ __device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n
                 const int e = t * E + r;
                 const unsigned long long p = lds ? s[e ^ j] : shfl_xor_u64(x[r], j / E);
                 const bool keep_min = (((e & j) == 0) == ((e & k) == 0));
-                const unsigned long long lo = x[r] < p ? x[r] : p, hi = x[r] < p ? p : x[r];
-                x[r] = keep_min ? lo : hi;
+                x[r] = ((x[r] < p) == keep_min) ? x[r] : p;  // equal keys are identical (padding)
             }
         }
     };
