@@ -185,11 +185,11 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kAdam, kDensify, kKnn, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
-                                               "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "adam",         "densify_stats",
+                                               "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "sh_grad_views", "adam",         "densify_stats",
                                                "knn"};
 struct TimingState {
     bool on = false;
@@ -435,9 +435,28 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
         p.sh_dc = sp->dc; p.sh_rest = sp->rest; p.sh_off = sp->offset;
         p.dL_dsh = nullptr; p.dsh_dc = sp->d_dc; p.dsh_rest = sp->d_rest; p.dsh_off = sp->d_offset;
         p.sh_accumulate = sp->accumulate;
+        p.d_rgb = sp->d_rgb;
     }
     timed(kPreBwd, s, [&] { gsd::launch_preprocess_bwd(p, s); });
     GSD_CHECK(a->debug, s);
+    return GSD_OK;
+}
+
+int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
+                      int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
+                      void* stream) {
+    if (P < 0 || n_views < 0 || M < 1 || M < (D + 1) * (D + 1))
+        return fail(GSD_ERR_ARG, "sh_grad_views: need P >= 0, n_views >= 0, M >= (D+1)^2");
+    if (view_stride < 3 * (int64_t)P + 3) return fail(GSD_ERR_ARG, "sh_grad_views: view_stride < 3 P + 3");
+    if (P == 0) return GSD_OK;
+    if (!means3D || (n_views > 0 && !views)) return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::ShViewsParams p{};
+    p.P = P; p.D = D; p.M = M; p.n_views = n_views; p.view_stride = view_stride;
+    p.means3D = means3D; p.views = views; p.d_dc = d_dc; p.d_rest = d_rest; p.d_off = d_offset;
+    p.accumulate = accumulate;
+    hipStream_t s = as_stream(stream);
+    timed(kShViews, s, [&] { gsd::launch_sh_grad_views(p, s); });
+    GSD_CHECK(false, s);
     return GSD_OK;
 }
 

@@ -74,6 +74,7 @@ struct PreprocessBwdParams {
     float* dsh_rest;
     float* dsh_off;
     int sh_accumulate;
+    float* d_rgb;          // (P,3) masked dL/dRGB instead of the SH sinks (gsd_sh_split.d_rgb), or NULL
     float* dL_dscales;
     float* dL_drotations;
 };
@@ -171,6 +172,15 @@ void launch_activate_fwd(const ActivateParams& p, hipStream_t s);
 void launch_activate_bwd(const ActivateBwdParams& p, hipStream_t s);
 void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s);
 void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s);
+struct ShViewsParams {
+    int P, D, M, n_views;
+    long long view_stride;
+    const float* means3D;
+    const float* views;
+    float *d_dc, *d_rest, *d_off;
+    int accumulate;
+};
+void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
 void launch_tile_scan(int num_tiles, const uint32_t* tile_count, uint2* ranges, uint32_t* tile_cursor,
                       uint32_t* counters, hipStream_t s);

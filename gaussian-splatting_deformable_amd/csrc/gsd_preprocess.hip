@@ -381,6 +381,12 @@ __device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int i
         p.dL_dscales[3 * idx + 2] = 0.f;
     }
     if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.d_rgb) {  // the SH gradient is assembled from the views' d_rgb rows (gsd_sh_grad_views)
+        p.d_rgb[3 * idx] = 0.f;
+        p.d_rgb[3 * idx + 1] = 0.f;
+        p.d_rgb[3 * idx + 2] = 0.f;
+        return;
+    }
     if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0);
 }
 
@@ -461,7 +467,11 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         const float3 gx = sh_channel_bwd(DEG, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
         const float3 gy = sh_channel_bwd(DEG, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
         const float3 gz = sh_channel_bwd(DEG, s + 2, dc.z, dir.x, dir.y, dir.z, ds + 2);
-        if (p.dL_dsh) {
+        if (p.d_rgb) {  // this view's factor of the SH gradient; the sinks are filled by gsd_sh_grad_views
+            p.d_rgb[3 * idx] = dc.x;
+            p.d_rgb[3 * idx + 1] = dc.y;
+            p.d_rgb[3 * idx + 2] = dc.z;
+        } else if (p.dL_dsh) {
             float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
 #pragma unroll
             for (int k = 0; k < nc * 3; ++k) drow[k] = ds[k];
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
             if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + (size_t)idx * (p.M - 1) * 3, ds, acc);
             if (p.dsh_off) sink_sh<0, nc * 3>(p.dsh_off + (size_t)idx * p.M * 3, ds, acc);
         }
-        if (p.M > nc) zero_sh_tail(p, idx, nc);
+        if (p.M > nc && !p.d_rgb) zero_sh_tail(p, idx, nc);
         // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
         const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
                                         gx.z * dc.x + gy.z * dc.y + gz.z * dc.z);
@@ -493,6 +503,92 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         p.dL_dscales[3 * idx + 2] = dscale.z;
     }
     if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = drot;
+}
+
+}  // namespace gsd
+
+namespace gsd {
+
+// dL/dsh_k = sum_v B_k(dir_v) dL/dRGB_v (the per-view SH backward of backward.cu:20-139, summed over the views
+// whose masked dL/dRGB rows were exchanged).  One lane per Gaussian; the 3 (D+1)^2 sums stay in registers.
+template <int DEG>
+__global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= p.P) return;
+    constexpr int nc = (DEG + 1) * (DEG + 1);
+    const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+    float acc[48];
+#pragma unroll
+    for (int k = 0; k < 48; ++k) acc[k] = 0.f;
+    for (int v = 0; v < p.n_views; ++v) {
+        const float* row = p.views + (size_t)v * (size_t)p.view_stride;
+        const float* cam = row + (size_t)p.P * 3;
+        const float3 g = make_float3(row[3 * idx], row[3 * idx + 1], row[3 * idx + 2]);
+        const float3 d0 = make_float3(m.x - cam[0], m.y - cam[1], m.z - cam[2]);
+        const float len = sqrtf(dot3(d0, d0));
+        const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
+        float b[16];
+        b[0] = kSH0;
+        if (DEG > 0) {
+            b[1] = -kSH1 * y;
+            b[2] = kSH1 * z;
+            b[3] = -kSH1 * x;
+        }
+        if (DEG > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            b[4] = kSH2_0 * (x * y);
+            b[5] = kSH2_1 * (y * z);
+            b[6] = kSH2_2 * (2.f * zz - xx - yy);
+            b[7] = kSH2_3 * (x * z);
+            b[8] = kSH2_4 * (xx - yy);
+            if (DEG > 2) {
+                b[9] = kSH3_0 * y * (3.f * xx - yy);
+                b[10] = kSH3_1 * (x * y) * z;
+                b[11] = kSH3_2 * y * (4.f * zz - xx - yy);
+                b[12] = kSH3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                b[13] = kSH3_4 * x * (4.f * zz - xx - yy);
+                b[14] = kSH3_5 * z * (xx - yy);
+                b[15] = kSH3_6 * x * (xx - 3.f * yy);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < nc; ++k) {
+            acc[3 * k] += b[k] * g.x;
+            acc[3 * k + 1] += b[k] * g.y;
+            acc[3 * k + 2] += b[k] * g.z;
+        }
+    }
+    const bool add = p.accumulate != 0;
+    if (p.d_dc) {
+        float* d = p.d_dc + (size_t)idx * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = (add ? d[c] : 0.f) + acc[c];
+    }
+    if (p.d_rest) {
+        float* d = p.d_rest + (size_t)idx * (p.M - 1) * 3;
+#pragma unroll
+        for (int k = 3; k < nc * 3; ++k) d[k - 3] = (add ? d[k - 3] : 0.f) + acc[k];
+        if (!add)
+            for (int k = nc * 3; k < p.M * 3; ++k) d[k - 3] = 0.f;
+    }
+    if (p.d_off) {
+        float* d = p.d_off + (size_t)idx * p.M * 3;
+#pragma unroll
+        for (int k = 0; k < nc * 3; ++k) d[k] = (add ? d[k] : 0.f) + acc[k];
+        if (!add)
+            for (int k = nc * 3; k < p.M * 3; ++k) d[k] = 0.f;
+    }
+}
+
+void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s) {
+    if (p.P <= 0) return;
+    const dim3 g((p.P + 255) / 256), b(256);
+    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+        case 0: hipLaunchKernelGGL(k_sh_grad_views<0>, g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL(k_sh_grad_views<1>, g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL(k_sh_grad_views<2>, g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL(k_sh_grad_views<3>, g, b, 0, s, p); break;
+    }
 }
 
 }  // namespace gsd

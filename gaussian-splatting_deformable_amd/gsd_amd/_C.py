@@ -66,7 +66,7 @@ class ShSplit:
     additive offset (P,1+R,3) read in place instead of shs = cat(dc, rest) + offset; for the backward,
     the gradient sinks (any may be None) and whether they are added into (accumulate) or stored."""
 
-    def __init__(self, dc, rest, offset=None, d_dc=None, d_rest=None, d_offset=None, accumulate=False):
+    def __init__(self, dc, rest, offset=None, d_dc=None, d_rest=None, d_offset=None, accumulate=False, d_rgb=None):
         dev = dc.device
         self.dc = _dev_f32(dc, "features_dc", dev)
         self.rest = _dev_f32(rest, "features_rest", dev)
@@ -76,9 +76,11 @@ class ShSplit:
             if t is not None and (not t.is_contiguous() or t.dtype != torch.float32 or t.device != dev):
                 raise RuntimeError("sh_split gradient sinks must be contiguous float32 on the same device")
         self.M = 1 + int(self.rest.size(1))
+        self.d_rgb = d_rgb   # (P*3,) view: the view's masked dL/dRGB instead of the SH gradient (sh_grad_views)
         self.c = _native.ShSplit(dc=_ptr(self.dc).value, rest=_ptr(self.rest).value, offset=_ptr(self.offset).value,
                                  d_dc=_ptr(self.sinks[0]).value, d_rest=_ptr(self.sinks[1]).value,
-                                 d_offset=_ptr(self.sinks[2]).value, accumulate=int(bool(accumulate)))
+                                 d_offset=_ptr(self.sinks[2]).value, accumulate=int(bool(accumulate)),
+                                 d_rgb=_ptr(d_rgb).value)
 
 
 class _Args:
@@ -200,6 +202,20 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                 _ptr(dout), _ptr(dmeans2D), _ptr(scratch), _ptr(dopacity), _ptr(dcolors), _ptr(dmeans3D),
                 _ptr(dcov3D), _ptr(dsh if M else None), _ptr(dscales), _ptr(drot), _stream(dev)))
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
+
+
+def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None, accumulate=False):
+    """gsd_sh_grad_views: the SH gradient summed over the views whose rows views (n_views, view_stride) hold
+    [masked dL/dRGB (P*3) | campos (3) | pad] -> written into / added to the given sinks."""
+    lib = _native.load()
+    dev = means3D.device
+    if views.dim() != 2 or not views.is_contiguous() or views.dtype != torch.float32 or views.device != dev:
+        raise RuntimeError("sh_grad_views: views must be a contiguous (n_views, stride) float32 device tensor")
+    m = _dev_f32(means3D, "means3D", dev)
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_sh_grad_views(int(P), int(D), int(M), int(views.size(0)), _ptr(m), _ptr(views),
+                                            int(views.size(1)), _ptr(d_dc), _ptr(d_rest), _ptr(d_offset),
+                                            int(bool(accumulate)), _stream(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

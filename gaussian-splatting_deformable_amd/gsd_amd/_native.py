@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -24,7 +24,7 @@ class ShSplit(ctypes.Structure):
     """Mirror of ``gsd_sh_split`` (include/gsd_raster.h)."""
 
     _fields_ = [("dc", _vp), ("rest", _vp), ("offset", _vp), ("d_dc", _vp), ("d_rest", _vp), ("d_offset", _vp),
-                ("accumulate", _i32)]
+                ("accumulate", _i32), ("d_rgb", _vp)]
 
 
 class RasterArgs(ctypes.Structure):
@@ -53,6 +53,7 @@ SIGNATURES = {
     "gsd_rasterize_forward_bin": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "gsd_rasterize_forward_render": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gsd_rasterize_forward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _sz, _vp, _vp, ctypes.POINTER(_i64), _vp]),
+    "gsd_sh_grad_views": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp]),
     "gsd_rasterize_backward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),

@@ -14,7 +14,7 @@ from typing import NamedTuple
 import torch
 import torch.nn as nn
 
-from . import _C
+from . import _C, parallel
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -83,19 +83,26 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_gaussians_split_sh(means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations,
-                                 raster_settings):
+                                 raster_settings, sh_views=False):
     """The fused render() path's rasterizer call (no reference counterpart: the reference builds
     shs = cat(f_dc, f_rest) + sh_offset in torch first, gaussian_renderer/__init__.py:129-134).  The SH
     pieces are read in place, and their gradients are written by the rasterizer backward -- added
-    straight into ``.grad`` for parameters registered with FlatGrads.  -> (color, radii)."""
+    straight into ``.grad`` for parameters registered with FlatGrads.  -> (color, radii).
+
+    ``sh_views``: the caller guarantees means3D is the same on every data-parallel rank (no per-view
+    deformation).  Then, with more than one rank, the backward exchanges each view's masked dL/dRGB (12 B per
+    Gaussian, one all_gather) and every rank sums the SH gradient of all views itself (gsd_sh_grad_views)
+    instead of all-reducing the 192-B SH gradient (parallel.FlatGrads leaves it out of its all-reduce)."""
     return _RasterizeSplitSH.apply(means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations,
-                                   raster_settings)
+                                   raster_settings, sh_views)
 
 
 class _RasterizeSplitSH(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations, raster_settings):
+    def forward(ctx, means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations, raster_settings,
+                sh_views=False):
         rs = raster_settings
+        ctx.sh_views = bool(sh_views)
         split = _C.ShSplit(f_dc, f_rest, sh_offset)
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(
             rs.bg, means3D, None, opacities, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
@@ -126,6 +133,12 @@ class _RasterizeSplitSH(torch.autograd.Function):
         else:
             d_dc, d_rest = torch.zeros_like(f_dc), torch.zeros_like(f_rest)
         offset = sh_offset if ctx.has_offset else None
+        world = parallel.data_parallel_world()
+        if ctx.sh_views and world > 1 and sinks is not None and offset is None and parallel.SH_VIEWS:
+            g_m2d, g_op, g_m3d, g_sc, g_rot = _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations,
+                                                                 radii, f_dc, f_rest, geomBuffer, binningBuffer,
+                                                                 imgBuffer, sinks, acc, world)
+            return g_m3d, g_m2d, None, None, None, g_op, g_sc, g_rot, None, None
         d_off = None
         if ctx.has_offset:
             d_off = torch.zeros(f_dc.size(0), 1 + f_rest.size(1), 3, device=f_dc.device)
@@ -136,7 +149,36 @@ class _RasterizeSplitSH(torch.autograd.Function):
             binningBuffer, imgBuffer, rs.debug, sh_split=split)
         if sinks is not None:
             d_dc = d_rest = None
-        return g_m3d, g_m2d, d_dc, d_rest, d_off, g_op, g_sc, g_rot, None
+        return g_m3d, g_m2d, d_dc, d_rest, d_off, g_op, g_sc, g_rot, None, None
+
+
+def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radii, f_dc, f_rest, geomBuffer,
+                       binningBuffer, imgBuffer, sinks, acc, world):
+    """Data-parallel backward of the split-SH rasterizer with the SH gradient exchanged per view: this rank's
+    row [masked dL/dRGB (P*3) | campos (3) | pad] is all-gathered and every rank runs gsd_sh_grad_views over
+    all rows into its SH sinks, which FlatGrads then leaves out of the gradient all-reduce."""
+    import torch.distributed as dist
+    P, dev = int(f_dc.size(0)), f_dc.device
+    stride = 3 * P + 4
+    row = torch.empty(stride, dtype=torch.float32, device=dev)
+    row[3 * P:3 * P + 3].copy_(rs.campos.reshape(-1))
+    row[3 * P + 3:].zero_()
+    split = _C.ShSplit(f_dc, f_rest, None, None, None, None, accumulate=False, d_rgb=row[:3 * P])
+    g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
+        rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
+        rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
+        binningBuffer, imgBuffer, rs.debug, sh_split=split)
+    views = torch.empty(world, stride, dtype=torch.float32, device=dev)
+    if dist.get_backend() == "nccl":   # RCCL: one all_gather into the (world, stride) buffer
+        dist.all_gather_into_tensor(views, row)
+    else:                              # gloo (tests): through host memory
+        parts = [torch.empty(stride, dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(parts, row.cpu())
+        views.copy_(torch.stack(parts))
+    _C.sh_grad_views(rs.sh_degree, means3D, views, P, 1 + int(f_rest.size(1)), d_dc=sinks[0], d_rest=sinks[1],
+                     accumulate=acc)
+    parallel.mark_reduced(ctx.params)
+    return g_m2d, g_op, g_m3d, g_sc, g_rot
 
 
 class GaussianRasterizationSettings(NamedTuple):

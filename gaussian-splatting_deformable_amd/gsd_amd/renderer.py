@@ -243,8 +243,11 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
         # zero offsets are read-only expanded views of a cached zero row (in-place writes raise)
         means3D_offset = means3D - means3D_ori if moved else _zeros(1, 3, means3D).expand(P, 3)
         rot_offset = rot_offset if rot_offset is not None else _zeros(1, 4, means3D).expand(P, 4)
+        # undeformed means are the same on every data-parallel rank: the SH gradient can then be exchanged as
+        # per-view dL/dRGB rows (gsd_amd.rasterizer.rasterize_gaussians_split_sh)
         rendered_image, radii = rasterize_gaussians_split_sh(means3D, means2D, pc._features_dc, pc._features_rest,
-                                                             dsh, opacity, scales, rotations, raster_settings)
+                                                             dsh, opacity, scales, rotations, raster_settings,
+                                                             sh_views=not moved)
         return RenderPackage(render=rendered_image, viewspace_points=screenspace_points, radii=radii,
                              means3D=means3D, means3D_ori=means3D_ori, rotations=rotations,
                              means3D_offset=means3D_offset, opacities=opacity, rot_offset=rot_offset)

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 4
+#define GSD_ABI_VERSION 5
 
 enum {
     GSD_OK = 0,
@@ -68,9 +68,13 @@ typedef struct gsd_sh_split {
     float* d_dc;           /* backward sink dL/d dc (P,1,3), or NULL */
     float* d_rest;         /* backward sink dL/d rest (P,M-1,3), or NULL */
     float* d_offset;       /* backward sink dL/d offset (P,M,3), or NULL */
-    int32_t accumulate;    /* backward: 1 = add into the sinks, 0 = store.  Entries of Gaussians with
-                              radii == 0 and of coefficients above the active degree are not touched
-                              (zero-fill the sinks first when storing, as for every backward output). */
+    int32_t accumulate;    /* backward: 1 = add into the sinks (entries of Gaussians with radii == 0 and of
+                              coefficients above the active degree are then left as they are), 0 = store
+                              (every entry written, zeros included) */
+    float* d_rgb;          /* backward: NULL, or (P,3): then dL/dRGB masked by the colour clamp -- the view's
+                              factor of the SH gradient, dL/dsh_k = B_k(dir) dL/dRGB -- is written here for every
+                              Gaussian (zeros where radii == 0) instead of the SH gradient into the sinks;
+                              gsd_sh_grad_views sums such rows of several views into the SH gradient */
 } gsd_sh_split;
 
 /* Raster settings + per-Gaussian inputs of one view.  Mirrors the 19 arguments
@@ -157,6 +161,16 @@ int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, co
                            const float* dL_dout_color, float* dL_dmeans2D, void* scratch,
                            float* dL_dopacity, float* dL_dcolors, float* dL_dmeans3D, float* dL_dcov3D,
                            float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream);
+
+/* SH gradient of several views from their gsd_sh_split.d_rgb rows (data-parallel training: each rank
+ * exchanges its view's (P,3) row, 12 B per Gaussian, instead of all-reducing the 192-B SH gradient):
+ *   dL/dsh_k[c] = sum_v B_k(normalize(means3D - campos_v)) * d_rgb_v[c]    (backward.cu:20-139 per view)
+ * views: n_views rows of view_stride floats, row v = [d_rgb_v (P*3) | campos_v (3)].  means3D (P,3) must be
+ * the positions every view rendered (the same on every rank).  Sinks as in gsd_sh_split (any may be NULL);
+ * accumulate 0 stores every entry (coefficients above degree D as zeros), 1 adds. */
+int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
+                      int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
+                      void* stream);
 
 /* Near-plane visibility test (auxiliary.h:139-164): present[i] = 1/0. */
 int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -1,0 +1,71 @@
+"""Two data-parallel ranks on one GPU (gloo through host memory, 2 processes): one render + backward per rank,
+then FlatGrads.allreduce.  The SH gradient takes the per-view exchange path (rasterizer._backward_sh_views: the
+ranks all-gather masked dL/dRGB rows and each runs gsd_sh_grad_views); the rest is all-reduced.  Both ranks'
+slabs must equal one process accumulating both views."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+WORKER = r'''
+import os, sys
+sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting_deformable_amd"), ROOT]
+import torch, torch.distributed as dist
+from gsd_amd import DeformableGaussians, default_pipe, render
+from gsd_amd.camera import synthetic_camera
+from gsd_amd.parallel import FlatGrads
+from gsd_amd.scene import make_gaussians
+
+def step(pc, yaw):
+    cam = synthetic_camera(320, 240, yaw_deg=yaw).to("cuda:0")
+    out = render(cam, pc, default_pipe(), torch.zeros(3, device="cuda:0"))
+    w = torch.linspace(0.5, 1.5, 320, device="cuda:0")
+    (out["render"] * w).sum().backward()
+
+rank, world, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+params = make_gaussians(20_000, 320, 240, seed=21, device="cuda:0")
+pc = DeformableGaussians(params, sh_degree=3)
+flat = FlatGrads(pc.parameters())
+flat.slab.fill_(7.0)
+flat.invalidate()
+if rank >= 0:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[4], RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    step(pc, 4.0 * rank)
+    flat.allreduce()
+    dist.destroy_process_group()
+else:                      # the single-process reference: both views into one slab
+    for r in range(world):
+        step(pc, 4.0 * r)
+    flat.allreduce()
+torch.save(flat.slab.cpu(), out)
+'''
+
+
+def test_two_ranks_match_one_process(tmp_path):
+    script = tmp_path / "worker.py"
+    script.write_text("ROOT = %r\n" % ROOT + WORKER)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    port = str(29600 + os.getpid() % 200)
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), "2", str(tmp_path / f"r{r}.pt"), port], env=env)
+             for r in range(2)]
+    rcs = [p.wait(timeout=300) for p in procs]
+    assert rcs == [0, 0]
+    ref = subprocess.run([sys.executable, str(script), "-1", "2", str(tmp_path / "ref.pt"), port], env=env,
+                         timeout=300)
+    assert ref.returncode == 0
+    want = torch.load(tmp_path / "ref.pt", weights_only=True)
+    for r in range(2):
+        got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        assert torch.isfinite(got).all()
+        rel = float((got - want).norm() / want.norm())
+        assert rel <= 1e-5, (r, rel)

@@ -9,6 +9,8 @@ Bars (DESIGN.md "Parity"):
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -362,3 +364,52 @@ def test_config4_invariants():
     tiles = (np.arange(1080)[:, None] // 16) * ((W + 15) // 16) + (np.arange(W)[None] // 16)
     assert np.all(nc <= counts[tiles])
     assert torch.isfinite(color).all()
+
+
+def test_sh_grad_views_sums_per_view_sh_gradients():
+    """gsd_sh_grad_views over two views' masked dL/dRGB rows (gsd_sh_split.d_rgb) equals the sum of the two
+    views' SH gradients from the ordinary split-SH backward; the d_rgb mode leaves every other gradient as it
+    was (up to the float-atomic summation order, which varies from run to run)."""
+    from gsd_amd import _C
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.scene import make_gaussians
+    P, W, H = 20_000, 320, 240
+    g = make_gaussians(P, W, H, seed=12, device=DEV)
+    means = g.xyz.contiguous()
+    scales, rots = torch.exp(g.scaling), torch.nn.functional.normalize(g.rotation, dim=1)
+    opac = torch.sigmoid(g.opacity)
+    f_dc, f_rest = g.features_dc.contiguous(), g.features_rest.contiguous()
+    bg = torch.zeros(3, device=DEV)
+    rows, sums, others = [], [torch.zeros_like(f_dc), torch.zeros_like(f_rest)], []
+    for k, yaw in enumerate((0.0, 7.0)):
+        cam = synthetic_camera(W, H, yaw_deg=yaw).to(DEV)
+        tx, ty = math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2)
+        split = _C.ShSplit(f_dc, f_rest)
+        fwd = _C.rasterize_gaussians(bg, means, None, opac, scales, rots, 1.0, None, cam.world_view_transform,
+                                     cam.full_proj_transform, tx, ty, H, W, None, 3, cam.camera_center, False, False,
+                                     sh_split=split)
+        K, color, radii, geom, binning, img = fwd
+        dpix = torch.randn(3, H, W, generator=torch.Generator().manual_seed(k)).mul_(1e-3).to(DEV)
+        d_dc, d_rest = torch.empty_like(f_dc), torch.empty_like(f_rest)
+        res = []
+        for mode in ("sinks", "rgb"):
+            row = torch.full((3 * P + 4,), float("nan"), device=DEV)
+            row[3 * P:3 * P + 3] = cam.camera_center
+            sp = (_C.ShSplit(f_dc, f_rest, None, d_dc, d_rest, None, accumulate=False) if mode == "sinks" else
+                  _C.ShSplit(f_dc, f_rest, None, None, None, None, d_rgb=row[:3 * P]))
+            res.append(_C.rasterize_gaussians_backward(bg, means, radii, None, scales, rots, 1.0, None,
+                                                       cam.world_view_transform, cam.full_proj_transform, tx, ty,
+                                                       dpix, None, 3, cam.camera_center, geom, K, binning, img,
+                                                       False, sh_split=sp))
+        for a, b in zip(res[0], res[1]):   # the same up to the float-atomic summation order
+            if a is not None:
+                assert rel_l2(a.cpu(), b.cpu()) <= 1e-5
+        sums[0] += d_dc
+        sums[1] += d_rest
+        rows.append(row)
+    views = torch.stack(rows)
+    out_dc, out_rest = torch.full_like(f_dc, float("nan")), torch.full_like(f_rest, float("nan"))
+    _C.sh_grad_views(3, means, views, P, 16, d_dc=out_dc, d_rest=out_rest, accumulate=False)
+    assert rel_l2(out_dc.cpu(), sums[0].cpu()) <= 1e-5 and rel_l2(out_rest.cpu(), sums[1].cpu()) <= 1e-5
+    _C.sh_grad_views(3, means, views, P, 16, d_dc=out_dc, d_rest=out_rest, accumulate=True)
+    assert rel_l2(out_rest.cpu(), 2 * sums[1].cpu()) <= 1e-5

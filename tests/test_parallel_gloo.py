@@ -67,3 +67,44 @@ def test_two_rank_gradient_allreduce_equals_sum_of_views(tmp_path):
     for r in range(world):
         got = np.load(tmp_path / f"rank{r}.npy")
         np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-9)
+
+
+def _worker_sh_views(rank, world, port, out_dir):
+    """The data-parallel protocol of the per-view SH exchange: each rank holds the all-view SH gradient (what
+    gsd_sh_grad_views assembles from the gathered dL/dRGB rows -- emulated here from the oracle's per-view SH
+    gradients after an all_gather), marks it reduced, and FlatGrads.allreduce sums only the other gradients
+    (two contiguous runs around the SH view)."""
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd.parallel import FlatGrads, init_from_env, mark_reduced
+    r, _, w = init_from_env(backend="gloo")
+    grads = view_grads(yaw=2.0 * r)
+    params = [torch.nn.Parameter(torch.zeros(g.shape)) for g in grads]
+    fg = FlatGrads(params, device="cpu")
+    fg.invalidate()
+    sh_mine = torch.from_numpy(grads[1]).contiguous()
+    parts = [torch.empty_like(sh_mine) for _ in range(w)]
+    dist.all_gather(parts, sh_mine)
+    for i, (p, g) in enumerate(zip(params, grads)):
+        assert fg.claim([p]) is False
+        p.grad.copy_(sum(parts) if i == 1 else torch.from_numpy(g))
+    mark_reduced([params[1]])
+    fg.allreduce()
+    assert not fg.reduced
+    np.save(os.path.join(out_dir, f"rank{r}.npy"), fg.slab.numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_sh_views_protocol(tmp_path):
+    from oracle import oracle
+    oracle.build()
+    world = 2
+    mp.spawn(_worker_sh_views, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = sum(np.concatenate([g.reshape(-1) for g in view_grads(2.0 * r)]) for r in range(world))
+    for r in range(world):
+        got = np.load(tmp_path / f"rank{r}.npy")
+        np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-9)
