@@ -103,11 +103,13 @@ class FlatGrads:
     def zero(self):
         self.slab.zero_()
         self.stale.clear()
+        self.reduced = set()
         self.attach()
 
     def invalidate(self):
         """Mark every view stale (no memory traffic): the next gradient producer stores instead of adding."""
         self.stale = {id(p) for p in self.params}
+        self.reduced = set()
         self._version = self.slab._version
 
     def claim(self, params) -> bool:
