@@ -167,6 +167,8 @@ int validate(const gsd_raster_args* a, bool forward) {
         return fail(GSD_ERR_ARG, "Please provide excatly one of either SHs or precomputed colors!");
     if (a->sh_split && (!a->sh_split->dc || (a->M > 1 && !a->sh_split->rest)))
         return fail(GSD_ERR_ARG, "sh_split needs dc, and rest when M > 1");
+    if (a->activation && !(a->scales && a->rotations && a->opacities))
+        return fail(GSD_ERR_ARG, "activation needs the raw scaling, rotation and opacity");
     const bool have_sr = a->scales && a->rotations;
     if (have_sr == (a->cov3D_precomp != nullptr) || ((a->scales == nullptr) != (a->rotations == nullptr)))
         return fail(GSD_ERR_ARG,
@@ -305,6 +307,7 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
         p.sh_dc = sp->dc; p.sh_rest = sp->rest; p.sh_off = sp->offset;
     }
     p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
+    p.raw_act = a->activation != nullptr;
     p.radii = radii ? radii : g.radii;
     p.means2D = g.means2D; p.depths = g.depths; p.conic_opacity = g.conic_opacity; p.rgb = g.rgb;
     p.clamped = g.clamped; p.tile_count = use_hist ? nullptr : im.tile_count; p.err_flags = im.counters + 1;
@@ -393,11 +396,13 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     if (a->P == 0) return GSD_OK;
     if (!geom_buffer || !image_buffer || (K > 0 && !binning_buffer))
         return fail(GSD_ERR_STATE, "state buffers from the matching forward are required");
-    if (!dL_dout_color || !dL_dmeans2D || !scratch || !dL_dopacity || !dL_dcolors || !dL_dmeans3D ||
-        (a->cov3D_precomp && !dL_dcov3D))
+    const gsd_activation* act = a->activation;
+    if (!dL_dout_color || !dL_dmeans2D || !scratch || (a->cov3D_precomp && !dL_dcov3D))
         return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
-    if ((a->shs && !dL_dsh) || (a->scales && (!dL_dscales || !dL_drotations)))
+    if (!act && (!dL_dopacity || !dL_dcolors || !dL_dmeans3D || (a->scales && (!dL_dscales || !dL_drotations))))
         return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
+    if (a->shs && !dL_dsh) return fail(GSD_ERR_ARG, "gradient outputs must be allocated");
+    if (act && a->cov3D_precomp) return fail(GSD_ERR_ARG, "activation needs scales/rotations, not cov3D_precomp");
     hipStream_t s = as_stream(stream);
     Geom g;
     Img im;
@@ -436,6 +441,11 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
         p.dL_dsh = nullptr; p.dsh_dc = sp->d_dc; p.dsh_rest = sp->d_rest; p.dsh_off = sp->d_offset;
         p.sh_accumulate = sp->accumulate;
         p.d_rgb = sp->d_rgb;
+    }
+    if (act) {
+        p.raw_act = 1; p.raw_opacity = a->opacities;
+        p.a_xyz = act->d_xyz; p.a_scaling = act->d_scaling; p.a_rotation = act->d_rotation;
+        p.a_opacity = act->d_opacity; p.a_accumulate = act->accumulate;
     }
     timed(kPreBwd, s, [&] { gsd::launch_preprocess_bwd(p, s); });
     GSD_CHECK(a->debug, s);

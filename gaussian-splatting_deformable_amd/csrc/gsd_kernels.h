@@ -40,6 +40,7 @@ struct PreprocessParams {
     uint8_t* clamped;
     uint32_t* tile_count;
     uint32_t* err_flags;
+    int raw_act;           // scales / rotations / opacities are raw parameters (gsd_activation)
 };
 
 // Per-Gaussian gradient record of the rasterizer backward: 16 floats (one 64-B segment, the memory-side
@@ -75,6 +76,10 @@ struct PreprocessBwdParams {
     float* dsh_off;
     int sh_accumulate;
     float* d_rgb;          // (P,3) masked dL/dRGB instead of the SH sinks (gsd_sh_split.d_rgb), or NULL
+    int raw_act;           // raw parameters: gradients go to the sinks below (gsd_activation)
+    const float* raw_opacity;
+    float *a_xyz, *a_scaling, *a_rotation, *a_opacity;
+    int a_accumulate;
     float* dL_dscales;
     float* dL_drotations;
 };

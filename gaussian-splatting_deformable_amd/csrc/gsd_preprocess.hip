@@ -60,6 +60,17 @@ __device__ __forceinline__ void load_sh(const float* __restrict__ shs, const flo
     }
 }
 
+// The preamble's activations, the same float operations as k_activate_fwd (gsd_activate.hip): exp(scaling),
+// F.normalize(rotation) (eps 1e-12), sigmoid(opacity) -- used when the rasterizer is handed raw parameters.
+__device__ __forceinline__ float3 act_scale(const float* s, int i) {
+    return make_float3(expf(s[3 * i]), expf(s[3 * i + 1]), expf(s[3 * i + 2]));
+}
+__device__ __forceinline__ float4 act_rot(float4 q) {
+    const float n = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    return make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
+}
+__device__ __forceinline__ float act_opac(float o) { return 1.f / (1.f + expf(-o)); }
+
 template <int DEG>
 __device__ __forceinline__ float3 sh_to_rgb(const float (&s)[48], float3 pos, float3 cam, uint8_t& clamp_bits) {
     constexpr int deg = DEG;
@@ -122,8 +133,12 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3.v[k] = p.cov3D_precomp[6 * idx + k];
     } else {
-        const float3 s = make_float3(p.scales[3 * idx], p.scales[3 * idx + 1], p.scales[3 * idx + 2]);
-        const float4 q = reinterpret_cast<const float4*>(p.rotations)[idx];
+        float3 s = make_float3(p.scales[3 * idx], p.scales[3 * idx + 1], p.scales[3 * idx + 2]);
+        float4 q = reinterpret_cast<const float4*>(p.rotations)[idx];
+        if (p.raw_act) {
+            s = act_scale(p.scales, idx);
+            q = act_rot(q);
+        }
         c3 = cov3d_from_scale_rot(s, p.scale_modifier, q);
     }
     const float3 cov = cov2d_fwd(mean, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, c3, V);
@@ -155,7 +170,8 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     p.depths[idx] = pv.z;
     p.radii[idx] = (int)my_radius;
     p.means2D[idx] = pix;
-    p.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, p.opacities[idx]);
+    const float opac = p.raw_act ? act_opac(p.opacities[idx]) : p.opacities[idx];
+    p.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, opac);
     // per-tile instance counts by global atomics -- only on the fallback path for very
     // large tile grids; normally k_tile_hist builds them from LDS histograms instead
     if (!p.tile_count) return;
@@ -353,6 +369,48 @@ __device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int i
     }
 }
 
+// dL/d(raw parameters) of one Gaussian from the activated-space gradients (k_activate_bwd's formulas):
+// xyz: identity; scaling: * exp(scaling); rotation: (I - u u^T) / |q| (u = q / |q|); opacity: * s (1 - s).
+__device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, float3 dmean, float3 dscale,
+                                          float3 scale, float4 drot, float dopac) {
+    const bool acc = p.a_accumulate != 0;
+    auto put = [acc](float* d, float v) { *d = acc ? *d + v : v; };
+    if (p.a_xyz) {
+        put(p.a_xyz + 3 * i, dmean.x);
+        put(p.a_xyz + 3 * i + 1, dmean.y);
+        put(p.a_xyz + 3 * i + 2, dmean.z);
+    }
+    if (p.a_scaling) {
+        put(p.a_scaling + 3 * i, dscale.x * scale.x);
+        put(p.a_scaling + 3 * i + 1, dscale.y * scale.y);
+        put(p.a_scaling + 3 * i + 2, dscale.z * scale.z);
+    }
+    if (p.a_rotation) {
+        const float4 q = reinterpret_cast<const float4*>(p.rotations)[i];
+        const float nraw = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+        float4 gq;
+        if (nraw > 1e-12f) {
+            const float inv = 1.f / nraw;
+            const float4 u = make_float4(q.x * inv, q.y * inv, q.z * inv, q.w * inv);
+            const float ug = u.x * drot.x + u.y * drot.y + u.z * drot.z + u.w * drot.w;
+            gq = make_float4((drot.x - u.x * ug) * inv, (drot.y - u.y * ug) * inv, (drot.z - u.z * ug) * inv,
+                             (drot.w - u.w * ug) * inv);
+        } else {
+            gq = make_float4(drot.x * 1e12f, drot.y * 1e12f, drot.z * 1e12f, drot.w * 1e12f);
+        }
+        float4* d = reinterpret_cast<float4*>(p.a_rotation) + i;
+        if (acc) {
+            const float4 o = *d;
+            gq = make_float4(o.x + gq.x, o.y + gq.y, o.z + gq.z, o.w + gq.w);
+        }
+        *d = gq;
+    }
+    if (p.a_opacity) {
+        const float sg = act_opac(p.raw_opacity[i]);
+        put(p.a_opacity + i, dopac * sg * (1.f - sg));
+    }
+}
+
 // Gradients of a Gaussian the backward skips (radii == 0): every per-Gaussian output is written, so callers need
 // not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  Accumulating SH
 // sinks are left untouched.
@@ -368,9 +426,18 @@ __device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int i
         p.dL_dcolor[3 * idx + 1] = 0.f;
         p.dL_dcolor[3 * idx + 2] = 0.f;
     }
-    p.dL_dmeans3D[3 * idx] = 0.f;
-    p.dL_dmeans3D[3 * idx + 1] = 0.f;
-    p.dL_dmeans3D[3 * idx + 2] = 0.f;
+    if (p.raw_act) {
+        if (!p.a_accumulate) {  // stored: zeros (accumulating: + 0 changes nothing)
+            if (p.a_xyz) for (int k = 0; k < 3; ++k) p.a_xyz[3 * idx + k] = 0.f;
+            if (p.a_scaling) for (int k = 0; k < 3; ++k) p.a_scaling[3 * idx + k] = 0.f;
+            if (p.a_rotation) reinterpret_cast<float4*>(p.a_rotation)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (p.a_opacity) p.a_opacity[idx] = 0.f;
+        }
+    } else {
+        p.dL_dmeans3D[3 * idx] = 0.f;
+        p.dL_dmeans3D[3 * idx + 1] = 0.f;
+        p.dL_dmeans3D[3 * idx + 2] = 0.f;
+    }
     if (p.dL_dcov3D) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = 0.f;
@@ -412,6 +479,10 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     } else {
         scale = make_float3(p.scales[3 * idx], p.scales[3 * idx + 1], p.scales[3 * idx + 2]);
         q = reinterpret_cast<const float4*>(p.rotations)[idx];
+        if (p.raw_act) {
+            scale = act_scale(p.scales, idx);
+            q = act_rot(q);
+        }
         c3 = cov3d_from_scale_rot(scale, p.scale_modifier, q);
     }
     // the rasterizer's per-Gaussian record: unpack the API outputs (rasterize_points.cu:180-188) and use it
@@ -490,13 +561,16 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         const float3 dmn = dnormvdv(dir_orig, ddir);
         dmean = make_float3(dmean.x + dmn.x, dmean.y + dmn.y, dmean.z + dmn.z);
     }
-    p.dL_dmeans3D[3 * idx] = dmean.x;
-    p.dL_dmeans3D[3 * idx + 1] = dmean.y;
-    p.dL_dmeans3D[3 * idx + 2] = dmean.z;
-
     float3 dscale = make_float3(0.f, 0.f, 0.f);
     float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
     if (p.scales) cov3d_bwd(scale, p.scale_modifier, q, dcov, dscale, drot);
+    if (p.raw_act) {  // through the activations into the raw parameters' sinks (k_activate_bwd's formulas)
+        raw_grads(p, idx, dmean, dscale, scale, drot, r1.y);
+        return;
+    }
+    p.dL_dmeans3D[3 * idx] = dmean.x;
+    p.dL_dmeans3D[3 * idx + 1] = dmean.y;
+    p.dL_dmeans3D[3 * idx + 2] = dmean.z;
     if (p.dL_dscales) {
         p.dL_dscales[3 * idx] = dscale.x;
         p.dL_dscales[3 * idx + 1] = dscale.y;

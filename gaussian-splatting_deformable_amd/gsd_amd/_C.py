@@ -88,7 +88,7 @@ class _Args:
 
     def __init__(self, background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                  viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                 prefiltered, debug, sh_split=None):
+                 prefiltered, debug, sh_split=None, activation=None):
         dev = means3D.device
         if dev.type != "cuda":
             raise RuntimeError("means3D must be a HIP device tensor: this rasterizer has no CPU implementation")
@@ -119,7 +119,9 @@ class _Args:
             scales=_ptr(self.scales).value, rotations=_ptr(self.rotations).value,
             cov3D_precomp=_ptr(self.cov3D).value, viewmatrix=_ptr(self.view).value,
             projmatrix=_ptr(self.proj).value, campos=_ptr(self.campos).value,
-            sh_split=None if sh_split is None else ctypes.addressof(sh_split.c))
+            sh_split=None if sh_split is None else ctypes.addressof(sh_split.c),
+            activation=None if activation is None else ctypes.addressof(activation))
+        self.activation = activation
 
 
 _K_GUESS = {}   # device -> last num_rendered
@@ -127,7 +129,7 @@ _K_GUESS = {}   # device -> last num_rendered
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug, sh_split=None):
+                        prefiltered, debug, sh_split=None, activation=None):
     """RasterizeGaussiansCUDA (rasterize_points.cu:35-115):
     -> (num_rendered, color (3,H,W), radii (P,) int32, geomBuffer, binningBuffer, imgBuffer).
     ``sh_split`` (a ShSplit, with ``sh`` empty) is this library's extension for the fused render path."""
@@ -136,7 +138,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     lib = _native.load()
     a = _Args(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
               projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
-              sh_split)
+              sh_split, activation)
     dev, P, H, W = a.dev, a.P, a.H, a.W
     radii = torch.empty(P, dtype=torch.int32, device=dev)   # preprocess writes every entry (forward.cu:174)
     byte = dict(dtype=torch.uint8, device=dev)
@@ -169,21 +171,27 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
-                                 campos, geomBuffer, R, binningBuffer, imageBuffer, debug, sh_split=None):
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer, debug, sh_split=None,
+                                 activation=None, raw_opacity=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196):
     -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
     With ``sh_split`` the SH gradients go to its sinks and dL_dsh is None; so is dL_dcov3D when no
-    cov3D_precomp was given (the scales/rotations gradients are what such a caller uses)."""
+    cov3D_precomp was given (the scales/rotations gradients are what such a caller uses).  With
+    ``activation`` (a _native.Activation; scales / rotations and ``raw_opacity`` are then the raw parameters)
+    the parameter gradients go to its sinks and only dL_dmeans2D (and dL_dcov3D, dL_dsh) are returned."""
     lib = _native.load()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))  # rasterize_points.cu:142-143
-    a = _Args(background, means3D, colors, None, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
-              projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos, False, debug, sh_split)
+    a = _Args(background, means3D, colors, raw_opacity if activation is not None else None, scales, rotations,
+              scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
+              False, debug, sh_split, activation)
     dev, P, M = a.dev, a.P, a.M
     split = sh_split is not None
     want_cov = not split or a.cov3D is not None
     # every output is written by the backward for every Gaussian, so one unfilled slab holds them all (the
     # float4-accessed rotation first, 16-B aligned); the library zeroes its own scratch (the gradient records)
-    widths = [4, 3, 3, 1, 3, 6 if want_cov else 0, 0 if split else M * 3, 3]
+    act = activation is not None   # raw parameters: their gradients go to the activation sinks
+    widths = [0 if act else 4, 3, 0 if act else 3, 0 if act else 1, 0 if act else 3, 6 if want_cov else 0,
+              0 if split else M * 3, 0 if act else 3]
     slab = torch.empty(P * sum(widths), dtype=torch.float32, device=dev)
     views, off = [], 0
     for w in widths:

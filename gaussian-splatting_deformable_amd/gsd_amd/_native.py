@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -27,6 +27,12 @@ class ShSplit(ctypes.Structure):
                 ("accumulate", _i32), ("d_rgb", _vp)]
 
 
+class Activation(ctypes.Structure):
+    """Mirror of ``gsd_activation`` (include/gsd_raster.h)."""
+
+    _fields_ = [("d_xyz", _vp), ("d_scaling", _vp), ("d_rotation", _vp), ("d_opacity", _vp), ("accumulate", _i32)]
+
+
 class RasterArgs(ctypes.Structure):
     """Mirror of ``gsd_raster_args`` (include/gsd_raster.h)."""
 
@@ -36,7 +42,7 @@ class RasterArgs(ctypes.Structure):
         ("prefiltered", _i32), ("debug", _i32),
         ("background", _vp), ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp),
         ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp), ("projmatrix", _vp),
-        ("campos", _vp), ("sh_split", _vp),
+        ("campos", _vp), ("sh_split", _vp), ("activation", _vp),
     ]
 
 

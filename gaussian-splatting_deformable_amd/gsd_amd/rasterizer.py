@@ -14,7 +14,7 @@ from typing import NamedTuple
 import torch
 import torch.nn as nn
 
-from . import _C, parallel
+from . import _C, _native, parallel
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -108,15 +108,40 @@ class _RasterizeSplitSH(torch.autograd.Function):
             rs.bg, means3D, None, opacities, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
             rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, None, rs.sh_degree, rs.campos, rs.prefiltered,
             rs.debug, sh_split=split)
-        ctx.raster_settings = rs
-        ctx.num_rendered = num_rendered
-        ctx.has_offset = sh_offset is not None
-        ctx.mark_non_differentiable(radii)
-        ctx.set_materialize_grads(False)   # no zero-filled int32 gradient for radii
-        ctx.params = (f_dc, f_rest)
-        ctx.save_for_backward(means3D, scales, rotations, radii, f_dc, f_rest,
-                              sh_offset if sh_offset is not None else torch.empty(0), geomBuffer, binningBuffer,
-                              imgBuffer)
+        _save(ctx, rs, num_rendered, radii, means3D, scales, rotations, f_dc, f_rest, sh_offset, geomBuffer,
+              binningBuffer, imgBuffer)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _):
+        if grad_out_color is None:
+            return (None,) * 10
+        g_m2d, d_dc, d_rest, d_off, rest = _split_sh_backward(ctx, grad_out_color)
+        g_op, g_m3d, g_sc, g_rot = rest
+        return g_m3d, g_m2d, d_dc, d_rest, d_off, g_op, g_sc, g_rot, None, None
+
+
+def rasterize_gaussians_raw(xyz, means2D, f_dc, f_rest, scaling, rotation, opacity, raster_settings,
+                            sh_views=False):
+    """The fused render() path without offsets: the raw parameters (_xyz, _features_dc, _features_rest,
+    _scaling, _rotation, _opacity) go straight to the rasterizer, which applies exp / normalize / sigmoid itself
+    (gsd_activation) and whose backward writes their gradients -- into ``.grad`` for FlatGrads parameters.
+    Replaces the preamble kernels of gsd_amd.activate (gaussian_renderer/__init__.py:79-140). -> (color, radii)"""
+    return _RasterizeRaw.apply(xyz, means2D, f_dc, f_rest, scaling, rotation, opacity, raster_settings, sh_views)
+
+
+class _RasterizeRaw(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xyz, means2D, f_dc, f_rest, scaling, rotation, opacity, raster_settings, sh_views=False):
+        rs = raster_settings
+        ctx.sh_views = bool(sh_views)
+        split = _C.ShSplit(f_dc, f_rest, None)
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(
+            rs.bg, xyz, None, opacity, scaling, rotation, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
+            rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, None, rs.sh_degree, rs.campos, rs.prefiltered,
+            rs.debug, sh_split=split, activation=_native.Activation())
+        _save(ctx, rs, num_rendered, radii, xyz, scaling, rotation, f_dc, f_rest, None, geomBuffer, binningBuffer,
+              imgBuffer, opacity=opacity)
         return color, radii
 
     @staticmethod
@@ -124,36 +149,69 @@ class _RasterizeSplitSH(torch.autograd.Function):
         from .activate import _sinks
         if grad_out_color is None:
             return (None,) * 9
-        rs = ctx.raster_settings
-        means3D, scales, rotations, radii, f_dc, f_rest, sh_offset, geomBuffer, binningBuffer, imgBuffer = \
-            ctx.saved_tensors
-        sinks, acc = _sinks(ctx.params)
-        if sinks is not None:
-            d_dc, d_rest = sinks
+        saved = ctx.saved_tensors
+        xyz, scaling, rotation, opacity = saved[0], saved[1], saved[2], saved[10]
+        sinks, acc = _sinks((xyz, scaling, rotation, opacity))
+        if sinks is None:
+            sinks, acc = [torch.empty_like(t) for t in (xyz, scaling, rotation, opacity)], False
+            ret = sinks
         else:
-            d_dc, d_rest = torch.zeros_like(f_dc), torch.zeros_like(f_rest)
-        offset = sh_offset if ctx.has_offset else None
-        world = parallel.data_parallel_world()
-        if ctx.sh_views and world > 1 and sinks is not None and offset is None and parallel.SH_VIEWS:
-            g_m2d, g_op, g_m3d, g_sc, g_rot = _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations,
-                                                                 radii, f_dc, f_rest, geomBuffer, binningBuffer,
-                                                                 imgBuffer, sinks, acc, world)
-            return g_m3d, g_m2d, None, None, None, g_op, g_sc, g_rot, None, None
-        d_off = None
-        if ctx.has_offset:
-            d_off = torch.zeros(f_dc.size(0), 1 + f_rest.size(1), 3, device=f_dc.device)
-        split = _C.ShSplit(f_dc, f_rest, offset, d_dc, d_rest, d_off, accumulate=sinks is not None and acc)
-        g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
-            rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
-            rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
-            binningBuffer, imgBuffer, rs.debug, sh_split=split)
-        if sinks is not None:
-            d_dc = d_rest = None
-        return g_m3d, g_m2d, d_dc, d_rest, d_off, g_op, g_sc, g_rot, None, None
+            ret = [None] * 4
+        act = _native.Activation(d_xyz=sinks[0].data_ptr(), d_scaling=sinks[1].data_ptr(),
+                                 d_rotation=sinks[2].data_ptr(), d_opacity=sinks[3].data_ptr(),
+                                 accumulate=int(bool(acc)))
+        g_m2d, d_dc, d_rest, _, _ = _split_sh_backward(ctx, grad_out_color, activation=act, raw_opacity=opacity)
+        return ret[0], g_m2d, d_dc, d_rest, ret[1], ret[2], ret[3], None, None
+
+
+def _save(ctx, rs, num_rendered, radii, means3D, scales, rotations, f_dc, f_rest, sh_offset, geomBuffer,
+          binningBuffer, imgBuffer, opacity=None):
+    ctx.raster_settings = rs
+    ctx.num_rendered = num_rendered
+    ctx.has_offset = sh_offset is not None
+    ctx.mark_non_differentiable(radii)
+    ctx.set_materialize_grads(False)   # no zero-filled int32 gradient for radii
+    ctx.params = (f_dc, f_rest)
+    ctx.save_for_backward(means3D, scales, rotations, radii, f_dc, f_rest,
+                          sh_offset if sh_offset is not None else torch.empty(0), geomBuffer, binningBuffer,
+                          imgBuffer, opacity if opacity is not None else torch.empty(0))
+
+
+def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None):
+    """Shared backward of the split-SH rasterizer paths -> (dL/dmeans2D, d_dc, d_rest, d_offset,
+    (dL/dopacity, dL/dmeans3D, dL/dscales, dL/drotations)); the SH gradients are None when they went into
+    the parameters' .grad in place, the last four when ``activation`` took them."""
+    from .activate import _sinks
+    rs = ctx.raster_settings
+    means3D, scales, rotations, radii, f_dc, f_rest, sh_offset, geomBuffer, binningBuffer, imgBuffer, opac = \
+        ctx.saved_tensors
+    sinks, acc = _sinks(ctx.params)
+    offset = sh_offset if ctx.has_offset else None
+    world = parallel.data_parallel_world()
+    if ctx.sh_views and world > 1 and sinks is not None and offset is None and parallel.SH_VIEWS:
+        g_m2d, g_op, g_m3d, g_sc, g_rot = _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations,
+                                                             radii, f_dc, f_rest, geomBuffer, binningBuffer,
+                                                             imgBuffer, sinks, acc, world, activation, raw_opacity)
+        return g_m2d, None, None, None, (g_op, g_m3d, g_sc, g_rot)
+    if sinks is not None:
+        d_dc, d_rest = sinks
+    else:
+        d_dc, d_rest = torch.zeros_like(f_dc), torch.zeros_like(f_rest)
+    d_off = None
+    if ctx.has_offset:
+        d_off = torch.zeros(f_dc.size(0), 1 + f_rest.size(1), 3, device=f_dc.device)
+    split = _C.ShSplit(f_dc, f_rest, offset, d_dc, d_rest, d_off, accumulate=sinks is not None and acc)
+    g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
+        rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
+        rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
+        binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity)
+    if sinks is not None:
+        d_dc = d_rest = None
+    return g_m2d, d_dc, d_rest, d_off, (g_op, g_m3d, g_sc, g_rot)
 
 
 def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radii, f_dc, f_rest, geomBuffer,
-                       binningBuffer, imgBuffer, sinks, acc, world):
+                       binningBuffer, imgBuffer, sinks, acc, world, activation=None, raw_opacity=None):
     """Data-parallel backward of the split-SH rasterizer with the SH gradient exchanged per view: this rank's
     row [masked dL/dRGB (P*3) | campos (3) | pad] is all-gathered and every rank runs gsd_sh_grad_views over
     all rows into its SH sinks, which FlatGrads then leaves out of the gradient all-reduce."""
@@ -167,7 +225,7 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
     g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
-        binningBuffer, imgBuffer, rs.debug, sh_split=split)
+        binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity)
     views = torch.empty(world, stride, dtype=torch.float32, device=dev)
     if dist.get_backend() == "nccl":   # RCCL: one all_gather into the (world, stride) buffer
         dist.all_gather_into_tensor(views, row)

@@ -19,7 +19,8 @@ import torch.nn.functional as F
 
 from .activate import activate_split_sh
 from .deform import se3_deform
-from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_split_sh
+from .rasterizer import (GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians_raw,
+                         rasterize_gaussians_split_sh)
 from .sh import eval_sh
 
 
@@ -174,17 +175,24 @@ def _zeros(P, w, like):
 
 
 class RenderPackage(dict):
-    """render()'s returned dict; "visibility_filter" (radii > 0) is computed the first time it is read."""
+    """render()'s returned dict; "visibility_filter" (radii > 0) -- and, on the raw-parameter path, the
+    activated "rotations" / "opacities" (torch ops, differentiable) -- are computed the first time they are
+    read."""
+
+    lazy = {}
 
     def __missing__(self, key):
         if key == "visibility_filter":
             v = self["radii"] > 0
-            self[key] = v
-            return v
-        raise KeyError(key)
+        elif key in self.lazy:
+            v = self.lazy[key]()
+        else:
+            raise KeyError(key)
+        self[key] = v
+        return v
 
     def __contains__(self, key):
-        return key == "visibility_filter" or dict.__contains__(self, key)
+        return key == "visibility_filter" or key in self.lazy or dict.__contains__(self, key)
 
 
 class _Time:
@@ -231,6 +239,21 @@ def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1
         # concatenated -- the rasterizer reads features_dc / features_rest / the SH offset in place
         P = means3D.size(0)
         dx, scale_offset, rot_offset, mlp_shs = pc.offset_model(means3D, _time_for(pc.offset_model, tm), iteration)
+        if (dx is None and scale_offset is None and rot_offset is None and mlp_shs is None
+                and getattr(pc, "deform", "additive") != "se3"):
+            # no offsets: the raw parameters go straight to the rasterizer, which activates them itself
+            # (gsd_activation) -- no preamble kernels.  The activated tensors of the returned dict are built
+            # by torch only if read (RenderPackage), so they still carry gradients.
+            rendered_image, radii = rasterize_gaussians_raw(pc._xyz, means2D, pc._features_dc, pc._features_rest,
+                                                            pc._scaling, pc._rotation, pc._opacity, raster_settings,
+                                                            sh_views=True)
+            pkg = RenderPackage(render=rendered_image, viewspace_points=screenspace_points, radii=radii,
+                                means3D=pc._xyz, means3D_ori=pc._xyz,
+                                means3D_offset=_zeros(1, 3, pc._xyz).expand(P, 3),
+                                rot_offset=_zeros(1, 4, pc._xyz).expand(P, 4))
+            pkg.lazy = {"rotations": lambda: pc.rotation_activation(pc._rotation),
+                        "opacities": lambda: pc.opacity_activation(pc._opacity)}
+            return pkg
         dsh = None if mlp_shs is None else mlp_shs.reshape(P, -1, 3)
         means3D, scales, rotations, opacity = activate_split_sh(pc._xyz, pc._scaling, pc._rotation, pc._opacity, dx,
                                                                 scale_offset, rot_offset)

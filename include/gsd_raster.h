@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 5
+#define GSD_ABI_VERSION 6
 
 enum {
     GSD_OK = 0,
@@ -77,6 +77,21 @@ typedef struct gsd_sh_split {
                               gsd_sh_grad_views sums such rows of several views into the SH gradient */
 } gsd_sh_split;
 
+/* Optional activation of the per-Gaussian inputs inside the rasterizer (the render() preamble without
+ * offsets, gaussian_renderer/__init__.py:79-140 with scene/gaussian_model.py:761-797): with
+ * gsd_raster_args.activation set, args->scales, ->rotations and ->opacities are the RAW parameters
+ * (_scaling, _rotation, _opacity) and the rasterizer uses exp(scaling), normalize(rotation) (F.normalize,
+ * eps 1e-12) and sigmoid(opacity) -- the same float operations as gsd_activate_forward.  The backward then
+ * writes the raw-parameter gradients into the sinks below instead of dL_dmeans3D / dL_dscales /
+ * dL_drotations / dL_dopacity (which may be NULL). */
+typedef struct gsd_activation {
+    float* d_xyz;          /* (P,3) dL/d means3D (= dL/d _xyz), or NULL */
+    float* d_scaling;      /* (P,3) dL/d _scaling, or NULL */
+    float* d_rotation;     /* (P,4) dL/d _rotation, or NULL */
+    float* d_opacity;      /* (P,1) dL/d _opacity, or NULL */
+    int32_t accumulate;    /* 1 = add into the sinks, 0 = store (every Gaussian written) */
+} gsd_activation;
+
 /* Raster settings + per-Gaussian inputs of one view.  Mirrors the 19 arguments
  * of _C.rasterize_gaussians (rasterize_points.cu:36-55).  Absent optional
  * inputs are NULL (the reference passes empty tensors -> nullptr). */
@@ -101,6 +116,7 @@ typedef struct gsd_raster_args {
     const float* projmatrix;    /* (4,4) full projection, scene/cameras.py:57 */
     const float* campos;        /* (3) */
     const gsd_sh_split* sh_split; /* NULL, or the split SH operand above (then shs == NULL) */
+    const gsd_activation* activation; /* NULL, or: scales / rotations / opacities are raw parameters */
 } gsd_raster_args;
 
 int gsd_abi_version(void);
