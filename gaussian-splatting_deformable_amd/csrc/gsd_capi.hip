@@ -154,6 +154,17 @@ gsd::HistParams hist_params(const gsd_raster_args* a, const Geom& g, int T) {
     return hp;
 }
 
+// element strides of the split SH operand (0, 0 = contiguous rows)
+template <typename Prm>
+void set_sh_strides(Prm& p, const gsd_sh_split* sp, int M) {
+    const bool dc_set = sp && (sp->dc_stride_g || sp->dc_stride_e);
+    const bool rest_set = sp && (sp->rest_stride_g || sp->rest_stride_e);
+    p.dc_sg = dc_set ? sp->dc_stride_g : 3;
+    p.dc_se = dc_set ? sp->dc_stride_e : 1;
+    p.rest_sg = rest_set ? sp->rest_stride_g : 3LL * (M > 1 ? M - 1 : 0);
+    p.rest_se = rest_set ? sp->rest_stride_e : 1;
+}
+
 int validate(const gsd_raster_args* a, bool forward) {
     if (!a) return fail(GSD_ERR_ARG, "null gsd_raster_args");
     if (a->P < 0) return fail(GSD_ERR_ARG, "means3D must have dimensions (num_points, 3)");
@@ -306,6 +317,7 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     if (const gsd_sh_split* sp = a->sh_split) {
         p.sh_dc = sp->dc; p.sh_rest = sp->rest; p.sh_off = sp->offset;
     }
+    set_sh_strides(p, a->sh_split, a->M);
     p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
     p.raw_act = a->activation != nullptr;
     p.radii = radii ? radii : g.radii;
@@ -442,6 +454,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
         p.sh_accumulate = sp->accumulate;
         p.d_rgb = sp->d_rgb;
     }
+    set_sh_strides(p, a->sh_split, a->M);
     if (act) {
         p.raw_act = 1; p.raw_opacity = a->opacities;
         p.a_xyz = act->d_xyz; p.a_scaling = act->d_scaling; p.a_rotation = act->d_rotation;
@@ -454,7 +467,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
 
 int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
                       int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
-                      void* stream) {
+                      const gsd_sh_split* layout, void* stream) {
     if (P < 0 || n_views < 0 || M < 1 || M < (D + 1) * (D + 1))
         return fail(GSD_ERR_ARG, "sh_grad_views: need P >= 0, n_views >= 0, M >= (D+1)^2");
     if (view_stride < 3 * (int64_t)P + 3) return fail(GSD_ERR_ARG, "sh_grad_views: view_stride < 3 P + 3");
@@ -464,6 +477,7 @@ int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const fl
     p.P = P; p.D = D; p.M = M; p.n_views = n_views; p.view_stride = view_stride;
     p.means3D = means3D; p.views = views; p.d_dc = d_dc; p.d_rest = d_rest; p.d_off = d_offset;
     p.accumulate = accumulate;
+    set_sh_strides(p, layout, M);
     hipStream_t s = as_stream(stream);
     timed(kShViews, s, [&] { gsd::launch_sh_grad_views(p, s); });
     GSD_CHECK(false, s);

@@ -27,6 +27,7 @@ struct PreprocessParams {
     const float* sh_dc;    // split SH operand (gsd_sh_split), used when shs == nullptr
     const float* sh_rest;
     const float* sh_off;
+    long long dc_sg, dc_se, rest_sg, rest_se;  // split SH element strides (Gaussian, element)
     const float* cov3D_precomp;
     const float* colors_precomp;
     const float* view;
@@ -57,6 +58,7 @@ struct PreprocessBwdParams {
     const float* sh_dc;    // split SH operand, used when shs == nullptr
     const float* sh_rest;
     const float* sh_off;
+    long long dc_sg, dc_se, rest_sg, rest_se;  // strides of sh_dc / dsh_dc and sh_rest / dsh_rest
     const uint8_t* clamped;
     const float* scales;
     const float* rotations;
@@ -183,6 +185,7 @@ struct ShViewsParams {
     const float* means3D;
     const float* views;
     float *d_dc, *d_rest, *d_off;
+    long long dc_sg, dc_se, rest_sg, rest_se;
     int accumulate;
 };
 void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s);

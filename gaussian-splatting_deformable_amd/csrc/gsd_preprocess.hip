@@ -38,21 +38,31 @@ __device__ __forceinline__ float sh_channel(int deg, const float* __restrict__ s
 // registers: from its (P,M,3) row, or from the split operand (dc | rest, plus
 // the optional offset -- the same float add as the reference's
 // get_features + mlp_shs, gaussian_renderer/__init__.py:134).
+// Element strides of the split operand: element e of Gaussian g at [g * sg + e * se] (gsd_sh_split).
+struct ShStrides {
+    long long dc_sg, dc_se, rest_sg, rest_se;
+};
+template <typename Prm>
+__device__ __forceinline__ ShStrides sh_strides(const Prm& p) {
+    return ShStrides{p.dc_sg, p.dc_se, p.rest_sg, p.rest_se};
+}
+
 template <int NC>
 __device__ __forceinline__ void load_sh(const float* __restrict__ shs, const float* __restrict__ dc,
                                         const float* __restrict__ rest, const float* __restrict__ off, int M,
-                                        int idx, float (&s)[48]) {
+                                        int idx, float (&s)[48], const ShStrides& st) {
     if (shs) {
         const float* row = shs + (size_t)idx * M * 3;
 #pragma unroll
         for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
         return;
     }
+    const float* d = dc + idx * st.dc_sg;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) s[k] = dc[(size_t)idx * 3 + k];
-    const float* r = rest + (size_t)idx * (M - 1) * 3;
+    for (int k = 0; k < 3; ++k) s[k] = d[k * st.dc_se];
+    const float* r = rest + idx * st.rest_sg;
 #pragma unroll
-    for (int k = 3; k < NC * 3; ++k) s[k] = r[k - 3];
+    for (int k = 3; k < NC * 3; ++k) s[k] = r[(k - 3) * st.rest_se];
     if (off) {
         const float* o = off + (size_t)idx * M * 3;
 #pragma unroll
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     } else {
         const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         float sh[48];
-        load_sh<(DEG + 1) * (DEG + 1)>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, sh);
+        load_sh<(DEG + 1) * (DEG + 1)>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, sh, sh_strides(p));
         const float3 rgb = sh_to_rgb<DEG>(sh, mean, cam, cl);
         col = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
     }
@@ -344,12 +354,12 @@ __device__ __forceinline__ void cov3d_bwd(const float3 scale, float mod, const f
 
 // dst[k - K0] (+)= ds[k] for k in [K0, K1)
 template <int K0, int K1>
-__device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&ds)[48], bool acc) {
+__device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&ds)[48], bool acc, long long se = 1) {
     float old[K1 - K0 > 0 ? K1 - K0 : 1];
 #pragma unroll
-    for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[k - K0] : 0.f;
+    for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[(k - K0) * se] : 0.f;
 #pragma unroll
-    for (int k = K0; k < K1; ++k) dst[k - K0] = old[k - K0] + ds[k];
+    for (int k = K0; k < K1; ++k) dst[(k - K0) * se] = old[k - K0] + ds[k];
 }
 
 // SH gradient entries [from, M) x 3 of one Gaussian: the coefficients above the active degree get zero
@@ -360,10 +370,10 @@ __device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int i
         for (int k = 3 * from; k < p.M * 3; ++k) p.dL_dsh[(size_t)idx * p.M * 3 + k] = 0.f;
     } else if (!p.sh_accumulate) {
         if (p.dsh_dc && from == 0)
-            for (int k = 0; k < 3; ++k) p.dsh_dc[(size_t)idx * 3 + k] = 0.f;
+            for (int k = 0; k < 3; ++k) p.dsh_dc[idx * p.dc_sg + k * p.dc_se] = 0.f;
         if (p.dsh_rest)
             for (int k = 3 * (from > 1 ? from - 1 : 0); k < (p.M - 1) * 3; ++k)
-                p.dsh_rest[(size_t)idx * (p.M - 1) * 3 + k] = 0.f;
+                p.dsh_rest[idx * p.rest_sg + k * p.rest_se] = 0.f;
         if (p.dsh_off)
             for (int k = 3 * from; k < p.M * 3; ++k) p.dsh_off[(size_t)idx * p.M * 3 + k] = 0.f;
     }
@@ -533,7 +543,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         const float3 dc = make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r8 * ((cl & 4) ? 0 : 1));
         constexpr int nc = (DEG + 1) * (DEG + 1);
         float s[48];
-        load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s);
+        load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s, sh_strides(p));
         float ds[48];
         const float3 gx = sh_channel_bwd(DEG, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
         const float3 gy = sh_channel_bwd(DEG, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
@@ -550,8 +560,8 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
             // accumulate: every old value is loaded before the first store, so the loads issue together
             // instead of each waiting behind a store it might alias
             const bool acc = p.sh_accumulate != 0;
-            if (p.dsh_dc) sink_sh<0, 3>(p.dsh_dc + (size_t)idx * 3, ds, acc);
-            if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + (size_t)idx * (p.M - 1) * 3, ds, acc);
+            if (p.dsh_dc) sink_sh<0, 3>(p.dsh_dc + idx * p.dc_sg, ds, acc, p.dc_se);
+            if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + idx * p.rest_sg, ds, acc, p.rest_se);
             if (p.dsh_off) sink_sh<0, nc * 3>(p.dsh_off + (size_t)idx * p.M * 3, ds, acc);
         }
         if (p.M > nc && !p.d_rgb) zero_sh_tail(p, idx, nc);
@@ -634,16 +644,17 @@ __global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
     }
     const bool add = p.accumulate != 0;
     if (p.d_dc) {
-        float* d = p.d_dc + (size_t)idx * 3;
+        float* d = p.d_dc + idx * p.dc_sg;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) d[c] = (add ? d[c] : 0.f) + acc[c];
+        for (int c = 0; c < 3; ++c) d[c * p.dc_se] = (add ? d[c * p.dc_se] : 0.f) + acc[c];
     }
     if (p.d_rest) {
-        float* d = p.d_rest + (size_t)idx * (p.M - 1) * 3;
+        float* d = p.d_rest + idx * p.rest_sg;
+        const long long se = p.rest_se;
 #pragma unroll
-        for (int k = 3; k < nc * 3; ++k) d[k - 3] = (add ? d[k - 3] : 0.f) + acc[k];
+        for (int k = 3; k < nc * 3; ++k) d[(k - 3) * se] = (add ? d[(k - 3) * se] : 0.f) + acc[k];
         if (!add)
-            for (int k = nc * 3; k < p.M * 3; ++k) d[k - 3] = 0.f;
+            for (int k = nc * 3; k < p.M * 3; ++k) d[(k - 3) * se] = 0.f;
     }
     if (p.d_off) {
         float* d = p.d_off + (size_t)idx * p.M * 3;

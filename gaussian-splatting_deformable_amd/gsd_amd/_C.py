@@ -68,19 +68,51 @@ class ShSplit:
 
     def __init__(self, dc, rest, offset=None, d_dc=None, d_rest=None, d_offset=None, accumulate=False, d_rgb=None):
         dev = dc.device
-        self.dc = _dev_f32(dc, "features_dc", dev)
-        self.rest = _dev_f32(rest, "features_rest", dev)
+        # dc / rest may be strided (P,K,3) views -- e.g. FusedAdam's coefficient-major slabs -- as long as the
+        # element e = 3 k + c sits at g * stride(0) + e * stride(2); anything else is copied contiguous
+        self.dc, dcs = _sh_operand(dc, "features_dc", dev)
+        self.rest, rs = _sh_operand(rest, "features_rest", dev)
         self.offset = None if offset is None else _dev_f32(offset, "sh offset", dev)
         self.sinks = [None if t is None else t for t in (d_dc, d_rest, d_offset)]
-        for t in self.sinks:
-            if t is not None and (not t.is_contiguous() or t.dtype != torch.float32 or t.device != dev):
-                raise RuntimeError("sh_split gradient sinks must be contiguous float32 on the same device")
+        for t, want in zip(self.sinks, (dcs, rs, None)):
+            if t is None:
+                continue
+            if t.dtype != torch.float32 or t.device != dev:
+                raise RuntimeError("sh_split gradient sinks must be float32 on the same device")
+            if (t.is_contiguous() and want is None) or (want is not None and _sh_strides(t) == want):
+                continue
+            if not t.is_contiguous() or want is not None:
+                raise RuntimeError("sh_split gradient sinks must have their parameter's layout")
         self.M = 1 + int(self.rest.size(1))
         self.d_rgb = d_rgb   # (P*3,) view: the view's masked dL/dRGB instead of the SH gradient (sh_grad_views)
         self.c = _native.ShSplit(dc=_ptr(self.dc).value, rest=_ptr(self.rest).value, offset=_ptr(self.offset).value,
                                  d_dc=_ptr(self.sinks[0]).value, d_rest=_ptr(self.sinks[1]).value,
                                  d_offset=_ptr(self.sinks[2]).value, accumulate=int(bool(accumulate)),
-                                 d_rgb=_ptr(d_rgb).value)
+                                 d_rgb=_ptr(d_rgb).value, dc_stride_g=(dcs or (0, 0))[0],
+                                 dc_stride_e=(dcs or (0, 0))[1], rest_stride_g=(rs or (0, 0))[0],
+                                 rest_stride_e=(rs or (0, 0))[1])
+
+
+def _sh_strides(t):
+    """(stride_g, stride_e) of a (P,K,3) tensor whose element (g, 3k+c) is at g*stride_g + (3k+c)*stride_e,
+    or None when contiguous (the default layout) or not expressible that way."""
+    if t.is_contiguous() or t.dim() != 3:
+        return None
+    sg, sk, sc = t.stride()
+    if t.size(1) > 1 and sk != 3 * sc:
+        return None
+    return (sg, sc)
+
+
+def _sh_operand(t, name, dev):
+    if t.device != dev:
+        raise RuntimeError(f"{name} must be on {dev} (got {t.device}); the rasterizer has no CPU path")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    st = _sh_strides(t)
+    if st is None and not t.is_contiguous():
+        t = t.contiguous()
+    return t, st
 
 
 class _Args:
@@ -212,7 +244,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
 
 
-def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None, accumulate=False):
+def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None, accumulate=False, layout=None):
     """gsd_sh_grad_views: the SH gradient summed over the views whose rows views (n_views, view_stride) hold
     [masked dL/dRGB (P*3) | campos (3) | pad] -> written into / added to the given sinks."""
     lib = _native.load()
@@ -223,7 +255,8 @@ def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None
     with torch.cuda.device(dev):
         _native.check(lib.gsd_sh_grad_views(int(P), int(D), int(M), int(views.size(0)), _ptr(m), _ptr(views),
                                             int(views.size(1)), _ptr(d_dc), _ptr(d_rest), _ptr(d_offset),
-                                            int(bool(accumulate)), _stream(dev)))
+                                            int(bool(accumulate)),
+                                            None if layout is None else ctypes.byref(layout.c), _stream(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

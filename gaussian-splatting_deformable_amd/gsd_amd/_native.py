@@ -24,7 +24,8 @@ class ShSplit(ctypes.Structure):
     """Mirror of ``gsd_sh_split`` (include/gsd_raster.h)."""
 
     _fields_ = [("dc", _vp), ("rest", _vp), ("offset", _vp), ("d_dc", _vp), ("d_rest", _vp), ("d_offset", _vp),
-                ("accumulate", _i32), ("d_rgb", _vp)]
+                ("accumulate", _i32), ("d_rgb", _vp), ("dc_stride_g", _i64), ("dc_stride_e", _i64),
+                ("rest_stride_g", _i64), ("rest_stride_e", _i64)]
 
 
 class Activation(ctypes.Structure):
@@ -59,7 +60,7 @@ SIGNATURES = {
     "gsd_rasterize_forward_bin": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "gsd_rasterize_forward_render": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gsd_rasterize_forward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _sz, _vp, _vp, ctypes.POINTER(_i64), _vp]),
-    "gsd_sh_grad_views": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp]),
+    "gsd_sh_grad_views": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp]),
     "gsd_rasterize_backward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),

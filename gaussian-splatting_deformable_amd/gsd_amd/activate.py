@@ -22,7 +22,8 @@ def _sinks(params):
     updated by the kernels; anything else (e.g. torch.autograd.grad calls) gets returned grads.
     -> (sinks or None, accumulate): accumulate False means the views were stale and are stored into."""
     sinks = [p.grad if (getattr(p, "_gsd_inplace_grad", False) and p.grad is not None
-                        and p.grad.is_contiguous() and p.grad.dtype == torch.float32) else None for p in params]
+                        and p.grad.dtype == torch.float32
+                        and (p.grad.is_contiguous() or p.grad.stride() == p.stride())) else None for p in params]
     if not all(s is not None for s in sinks):
         return None, True
     flats = {id(getattr(p, "_gsd_flat", None)): getattr(p, "_gsd_flat", None) for p in params}

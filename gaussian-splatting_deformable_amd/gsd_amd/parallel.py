@@ -38,6 +38,27 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     return rank, local, world
 
 
+def slab_view(slab, off, like=None, shape=None, coef_major=False):
+    """A view of slab[off : off + n] shaped like ``like`` with ``like``'s memory order (any permutation of a
+    contiguous layout), or, given ``shape``, contiguous -- or coefficient-major when ``coef_major`` and the
+    shape is an SH tensor (P, K, 3): stored as (K, 3, P), so the (P,K,3) view has strides (1, 3P, P)."""
+    if like is not None:
+        shape = tuple(like.shape)
+        n = like.numel()
+        if not like.is_contiguous() and like.dim() > 1:
+            perm = sorted(range(like.dim()), key=lambda d: -like.stride(d))
+            if like.permute(perm).is_contiguous():
+                inv = [perm.index(d) for d in range(like.dim())]
+                return slab[off:off + n].view([shape[d] for d in perm]).permute(inv)
+        return slab[off:off + n].view(shape)
+    n = 1
+    for d in shape:
+        n *= d
+    if coef_major and len(shape) == 3 and shape[2] == 3:
+        return slab[off:off + n].view(shape[1], 3, shape[0]).permute(2, 0, 1)
+    return slab[off:off + n].view(shape)
+
+
 SH_VIEWS = os.environ.get("GSD_SH_VIEWS", "1") != "0"   # exchange per-view dL/dRGB instead of the SH gradient
 
 
@@ -72,7 +93,7 @@ class FlatGrads:
         off = 0
         self.views = []
         for p in self.params:
-            v = self.slab[off:off + p.numel()].view_as(p)
+            v = slab_view(self.slab, off, like=p)   # the parameter's memory order (FusedAdam's layouts)
             self.views.append(v)
             off += p.numel()
         self.stale = set()

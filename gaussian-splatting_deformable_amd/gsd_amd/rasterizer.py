@@ -234,7 +234,7 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
         dist.all_gather(parts, row.cpu())
         views.copy_(torch.stack(parts))
     _C.sh_grad_views(rs.sh_degree, means3D, views, P, 1 + int(f_rest.size(1)), d_dc=sinks[0], d_rest=sinks[1],
-                     accumulate=acc)
+                     accumulate=acc, layout=split)
     parallel.mark_reduced(ctx.params)
     return g_m2d, g_op, g_m3d, g_sc, g_rot
 

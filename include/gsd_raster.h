@@ -75,6 +75,12 @@ typedef struct gsd_sh_split {
                               factor of the SH gradient, dL/dsh_k = B_k(dir) dL/dRGB -- is written here for every
                               Gaussian (zeros where radii == 0) instead of the SH gradient into the sinks;
                               gsd_sh_grad_views sums such rows of several views into the SH gradient */
+    int64_t dc_stride_g, dc_stride_e;     /* element e (= 3 k + channel) of Gaussian g of dc and d_dc at
+                                             [g * stride_g + e * stride_e]; 0, 0 = contiguous (P,1,3) */
+    int64_t rest_stride_g, rest_stride_e; /* the same for rest / d_rest; 0, 0 = contiguous (P,M-1,3).
+                                             Coefficient-major storage (stride_g 1, stride_e P: what
+                                             gsd_amd.optim.FusedAdam lays out) makes every SH access of a
+                                             wave one contiguous 256-B run instead of 64 rows */
 } gsd_sh_split;
 
 /* Optional activation of the per-Gaussian inputs inside the rasterizer (the render() preamble without
@@ -178,7 +184,8 @@ int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, co
                            float* dL_dopacity, float* dL_dcolors, float* dL_dmeans3D, float* dL_dcov3D,
                            float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream);
 
-/* SH gradient of several views from their gsd_sh_split.d_rgb rows (data-parallel training: each rank
+/* (layout: NULL, or a gsd_sh_split whose stride fields describe d_dc / d_rest; its pointers are ignored.)
+ * SH gradient of several views from their gsd_sh_split.d_rgb rows (data-parallel training: each rank
  * exchanges its view's (P,3) row, 12 B per Gaussian, instead of all-reducing the 192-B SH gradient):
  *   dL/dsh_k[c] = sum_v B_k(normalize(means3D - campos_v)) * d_rgb_v[c]    (backward.cu:20-139 per view)
  * views: n_views rows of view_stride floats, row v = [d_rgb_v (P*3) | campos_v (3)].  means3D (P,3) must be
@@ -186,7 +193,7 @@ int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, co
  * accumulate 0 stores every entry (coefficients above degree D as zeros), 1 adds. */
 int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
                       int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
-                      void* stream);
+                      const gsd_sh_split* layout, void* stream);
 
 /* Near-plane visibility test (auxiliary.h:139-164): present[i] = 1/0. */
 int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -262,3 +262,26 @@ def test_knn_init_matches_bruteforce(P, dup):
         assert g.features_dc.shape == (P, 1, 3) and g.features_rest.shape == (P, 15, 3)
         assert torch.allclose(g.scaling[:, 0].cpu(), torch.log(torch.sqrt(torch.clamp_min(torch.from_numpy(ref),
                                                                                             1e-7))))
+
+
+def test_coefficient_major_sh_layout_same_gradients():
+    """FusedAdam(coef_major=True) stores the SH parameters coefficient-major (permuted slab views, gsd_sh_split
+    strides): render + backward + one step give the same parameters as the default contiguous layout."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    params = make_gaussians(20_000, 320, 240, seed=8, device=DEV)
+    cam = synthetic_camera(320, 240).to(DEV)
+    outs = []
+    for cm in (False, True):
+        pc = DeformableGaussians(params, sh_degree=3)
+        opt = FusedAdam([{"params": [p], "lr": 1e-3} for p in pc.parameters()], lr=0.0, eps=1e-15, coef_major=cm)
+        assert pc._features_rest.is_contiguous() == (not cm)
+        for _ in range(2):
+            out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+            (out["render"] * torch.linspace(0, 1, 320, device=DEV)).sum().backward()
+            opt.step(zero_grad=True)
+        outs.append([p.detach().clone() for p in pc.parameters()])
+    for a, b in zip(*outs):
+        assert rel_l2(a, b) <= 1e-5
