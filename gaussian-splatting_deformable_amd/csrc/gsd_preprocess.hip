@@ -42,9 +42,12 @@ __device__ __forceinline__ float sh_channel(int deg, const float* __restrict__ s
 struct ShStrides {
     long long dc_sg, dc_se, rest_sg, rest_se;
 };
-template <typename Prm>
+// kStr = false: contiguous rows, strides as compile-time constants (so the row loads stay wide); the
+// general strided form is a separate instantiation (launchers pick by the strides).
+template <bool kStr, typename Prm>
 __device__ __forceinline__ ShStrides sh_strides(const Prm& p) {
-    return ShStrides{p.dc_sg, p.dc_se, p.rest_sg, p.rest_se};
+    if (kStr) return ShStrides{p.dc_sg, p.dc_se, p.rest_sg, p.rest_se};
+    return ShStrides{3, 1, 3LL * (p.M - 1), 1};
 }
 
 template <int NC>
@@ -57,12 +60,24 @@ __device__ __forceinline__ void load_sh(const float* __restrict__ shs, const flo
         for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
         return;
     }
+    // contiguous rows (element stride 1) keep compile-time offsets (wide loads); 2x faster than the general
+    // strided form on them
     const float* d = dc + idx * st.dc_sg;
+    if (st.dc_se == 1) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) s[k] = d[k * st.dc_se];
+        for (int k = 0; k < 3; ++k) s[k] = d[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s[k] = d[k * st.dc_se];
+    }
     const float* r = rest + idx * st.rest_sg;
+    if (st.rest_se == 1) {
 #pragma unroll
-    for (int k = 3; k < NC * 3; ++k) s[k] = r[(k - 3) * st.rest_se];
+        for (int k = 3; k < NC * 3; ++k) s[k] = r[k - 3];
+    } else {
+#pragma unroll
+        for (int k = 3; k < NC * 3; ++k) s[k] = r[(k - 3) * st.rest_se];
+    }
     if (off) {
         const float* o = off + (size_t)idx * M * 3;
 #pragma unroll
@@ -120,7 +135,7 @@ __device__ __forceinline__ float3 cov2d_fwd(const float3 mean, float fx, float f
 // Forward preprocess: forward.cu:155-256 (+ the per-tile instance count of
 // the binning stage, folded in so the rect is computed once).
 // ---------------------------------------------------------------------------
-template <int DEG>
+template <int DEG, bool kStr>
 __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= p.P) return;
@@ -171,7 +186,7 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     } else {
         const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
         float sh[48];
-        load_sh<(DEG + 1) * (DEG + 1)>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, sh, sh_strides(p));
+        load_sh<(DEG + 1) * (DEG + 1)>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, sh, sh_strides<kStr>(p));
         const float3 rgb = sh_to_rgb<DEG>(sh, mean, cam, cl);
         col = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
     }
@@ -356,6 +371,13 @@ __device__ __forceinline__ void cov3d_bwd(const float3 scale, float mod, const f
 template <int K0, int K1>
 __device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&ds)[48], bool acc, long long se = 1) {
     float old[K1 - K0 > 0 ? K1 - K0 : 1];
+    if (se == 1) {  // contiguous rows: compile-time offsets
+#pragma unroll
+        for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[k - K0] : 0.f;
+#pragma unroll
+        for (int k = K0; k < K1; ++k) dst[k - K0] = old[k - K0] + ds[k];
+        return;
+    }
 #pragma unroll
     for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[(k - K0) * se] : 0.f;
 #pragma unroll
@@ -365,15 +387,15 @@ __device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&d
 // SH gradient entries [from, M) x 3 of one Gaussian: the coefficients above the active degree get zero
 // gradients (and all of them for a skipped Gaussian), as in the reference's zero-initialised dL_dsh.
 // Accumulating split sinks are left untouched.
-__device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int idx, int from) {
+__device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int idx, int from, const ShStrides& st) {
     if (p.dL_dsh) {
         for (int k = 3 * from; k < p.M * 3; ++k) p.dL_dsh[(size_t)idx * p.M * 3 + k] = 0.f;
     } else if (!p.sh_accumulate) {
         if (p.dsh_dc && from == 0)
-            for (int k = 0; k < 3; ++k) p.dsh_dc[idx * p.dc_sg + k * p.dc_se] = 0.f;
+            for (int k = 0; k < 3; ++k) p.dsh_dc[idx * st.dc_sg + k * st.dc_se] = 0.f;
         if (p.dsh_rest)
             for (int k = 3 * (from > 1 ? from - 1 : 0); k < (p.M - 1) * 3; ++k)
-                p.dsh_rest[idx * p.rest_sg + k * p.rest_se] = 0.f;
+                p.dsh_rest[idx * st.rest_sg + k * st.rest_se] = 0.f;
         if (p.dsh_off)
             for (int k = 3 * from; k < p.M * 3; ++k) p.dsh_off[(size_t)idx * p.M * 3 + k] = 0.f;
     }
@@ -424,7 +446,7 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
 // Gradients of a Gaussian the backward skips (radii == 0): every per-Gaussian output is written, so callers need
 // not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  Accumulating SH
 // sinks are left untouched.
-__device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx) {
+__device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx, const ShStrides& st) {
     if (p.dL_dmean2D) {
         p.dL_dmean2D[3 * idx] = 0.f;
         p.dL_dmean2D[3 * idx + 1] = 0.f;
@@ -464,15 +486,16 @@ __device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int i
         p.d_rgb[3 * idx + 2] = 0.f;
         return;
     }
-    if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0);
+    if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0, st);
 }
 
-template <int DEG>
+template <int DEG, bool kStr>
 __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= p.P) return;
+    const ShStrides st = sh_strides<kStr>(p);
     if (!(p.radii[idx] > 0)) {  // backward.cu:359-360 skips it; its gradients are the zeros torch::zeros holds
-        zero_outputs(p, idx);
+        zero_outputs(p, idx, st);
         return;
     }
     const Mat4 Vm = load_mat4(p.view);
@@ -543,7 +566,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         const float3 dc = make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r8 * ((cl & 4) ? 0 : 1));
         constexpr int nc = (DEG + 1) * (DEG + 1);
         float s[48];
-        load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s, sh_strides(p));
+        load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s, st);
         float ds[48];
         const float3 gx = sh_channel_bwd(DEG, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
         const float3 gy = sh_channel_bwd(DEG, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
@@ -560,11 +583,11 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
             // accumulate: every old value is loaded before the first store, so the loads issue together
             // instead of each waiting behind a store it might alias
             const bool acc = p.sh_accumulate != 0;
-            if (p.dsh_dc) sink_sh<0, 3>(p.dsh_dc + idx * p.dc_sg, ds, acc, p.dc_se);
-            if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + idx * p.rest_sg, ds, acc, p.rest_se);
+            if (p.dsh_dc) sink_sh<0, 3>(p.dsh_dc + idx * st.dc_sg, ds, acc, st.dc_se);
+            if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + idx * st.rest_sg, ds, acc, st.rest_se);
             if (p.dsh_off) sink_sh<0, nc * 3>(p.dsh_off + (size_t)idx * p.M * 3, ds, acc);
         }
-        if (p.M > nc && !p.d_rgb) zero_sh_tail(p, idx, nc);
+        if (p.M > nc && !p.d_rgb) zero_sh_tail(p, idx, nc, st);
         // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
         const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
                                         gx.z * dc.x + gy.z * dc.y + gz.z * dc.z);
@@ -651,8 +674,13 @@ __global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
     if (p.d_rest) {
         float* d = p.d_rest + idx * p.rest_sg;
         const long long se = p.rest_se;
+        if (se == 1) {
 #pragma unroll
-        for (int k = 3; k < nc * 3; ++k) d[(k - 3) * se] = (add ? d[(k - 3) * se] : 0.f) + acc[k];
+            for (int k = 3; k < nc * 3; ++k) d[k - 3] = (add ? d[k - 3] : 0.f) + acc[k];
+        } else {
+#pragma unroll
+            for (int k = 3; k < nc * 3; ++k) d[(k - 3) * se] = (add ? d[(k - 3) * se] : 0.f) + acc[k];
+        }
         if (!add)
             for (int k = nc * 3; k < p.M * 3; ++k) d[(k - 3) * se] = 0.f;
     }
@@ -679,25 +707,39 @@ void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s) {
 }  // namespace gsd
 
 namespace gsd {
-void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
-    if (p.P <= 0) return;
+template <typename Prm>
+static bool strided_sh(const Prm& p) {
+    return p.sh_dc && !(p.dc_sg == 3 && p.dc_se == 1 && p.rest_sg == 3LL * (p.M - 1) && p.rest_se == 1);
+}
+template <bool kStr>
+static void launch_fwd(const PreprocessParams& p, hipStream_t s) {
     const dim3 g((p.P + 255) / 256), b(256);
     switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {  // degrees > 3 evaluate as 3, like forward.cu:32-60
-        case 0: hipLaunchKernelGGL(k_preprocess_fwd<0>, g, b, 0, s, p); break;
-        case 1: hipLaunchKernelGGL(k_preprocess_fwd<1>, g, b, 0, s, p); break;
-        case 2: hipLaunchKernelGGL(k_preprocess_fwd<2>, g, b, 0, s, p); break;
-        default: hipLaunchKernelGGL(k_preprocess_fwd<3>, g, b, 0, s, p); break;
+        case 0: hipLaunchKernelGGL((k_preprocess_fwd<0, kStr>), g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((k_preprocess_fwd<1, kStr>), g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_preprocess_fwd<2, kStr>), g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL((k_preprocess_fwd<3, kStr>), g, b, 0, s, p); break;
+    }
+}
+void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
+    if (p.P <= 0) return;
+    if (strided_sh(p)) launch_fwd<true>(p, s);
+    else launch_fwd<false>(p, s);
+}
+template <bool kStr>
+static void launch_bwd(const PreprocessBwdParams& p, hipStream_t s) {
+    const dim3 g((p.P + 255) / 256), b(256);
+    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+        case 0: hipLaunchKernelGGL((k_preprocess_bwd<0, kStr>), g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((k_preprocess_bwd<1, kStr>), g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_preprocess_bwd<2, kStr>), g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL((k_preprocess_bwd<3, kStr>), g, b, 0, s, p); break;
     }
 }
 void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s) {
     if (p.P <= 0) return;
-    const dim3 g((p.P + 255) / 256), b(256);
-    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
-        case 0: hipLaunchKernelGGL(k_preprocess_bwd<0>, g, b, 0, s, p); break;
-        case 1: hipLaunchKernelGGL(k_preprocess_bwd<1>, g, b, 0, s, p); break;
-        case 2: hipLaunchKernelGGL(k_preprocess_bwd<2>, g, b, 0, s, p); break;
-        default: hipLaunchKernelGGL(k_preprocess_bwd<3>, g, b, 0, s, p); break;
-    }
+    if (strided_sh(p)) launch_bwd<true>(p, s);
+    else launch_bwd<false>(p, s);
 }
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s) {
     if (P > 0) hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);
