@@ -202,6 +202,26 @@ __device__ __forceinline__ float fin16(float h01, float h23) {
     return t;
 }
 __device__ __forceinline__ int fin16_column(int lane) { return (((lane >> 4) & 1) << 1) | (lane >> 5); }
+// Distance-16 transposed step: lanes with bit 4 clear return a summed over lanes l and l ^ 16, lanes with
+// bit 4 set return b summed the same way.
+__device__ __forceinline__ float pair16(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Distance-4 step after sum8 (row_ror:4): lanes with bits 2-3 clear return the sum over lanes l, l ^ 4,
+// l ^ 8, l ^ 12 of the input to sum8.
+__device__ __forceinline__ float sum4(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+}
+// Lane (l & ~3) + i's value in every lane of the quad (DPP quad_perm [i, i, i, i]).
+template <int I>
+__device__ __forceinline__ float quad_bcast(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), I * 0x55, 0xf, 0xf, false));
+}
+// Distance-8 step (row_ror:8 == lane ^ 8 inside a 16-lane row): every lane returns v(l) + v(l ^ 8).
+__device__ __forceinline__ float sum8(float v) {
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+}
 
 // Transposed butterfly: c[k] is this lane's value for column k (k = 0..7).
 // Returns, in every lane l, the 64-lane total of column (l >> 3).  Six

@@ -31,7 +31,8 @@ namespace gsd {
 // forward: records whose alphas are evaluated together (ILP across the exps); measured 2/3/4/6/8/16 ->
 // 4 is fastest (0.33 ms vs 0.38 at 8: fewer alphas wasted past a pixel's termination)
 constexpr int kBatch = 4;
-constexpr int kBwdBatch = 4;  // backward: records per reduction (pair32 + fin16)
+constexpr int kBwdBatch = 4;  // backward: records whose alphas are evaluated together
+constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
 
 // Bounding box of {d : alpha(d) >= 1/255} for a record, inflated for safety.
 // Q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o); half-widths sqrt(t c/det), sqrt(t a/det).
@@ -136,6 +137,22 @@ __device__ __forceinline__ float fast_recip(float d) {
     return fmaf(fmaf(-d, r, 1.0f), r, r);
 }
 
+// Record-major accumulation of the backward (k_render_bwd phase 2): pixel I of the lane's quad contributes
+// v = G dL/dalpha and w = alpha T (read from LDS) with its dL/dpixel (DPP quad broadcast from lane I).
+struct RecordSums {
+    float S0 = 0.f, S1 = 0.f, S3 = 0.f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+    __device__ __forceinline__ void add(float2 vw, float dx, float3 d) {
+#pragma clang fp contract(fast)
+        S0 += vw.x;
+        const float t = vw.x * dx;
+        S1 += t;
+        S3 = fmaf(t, dx, S3);
+        C0 = fmaf(vw.y, d.x, C0);
+        C1 = fmaf(vw.y, d.y, C1);
+        C2 = fmaf(vw.y, d.z, C2);
+    }
+};
+
 struct TileGeom {
     int tile, wave, lane, px, py;
     float qx0, qy0;
@@ -237,9 +254,19 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ float2 s_xy[kTilePix];
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
-    __shared__ float4 s_box[kTilePix];
     __shared__ float s_acc[9][kTilePix + 1];  // +1: a record's nine sums sit in nine different banks
     __shared__ uint8_t s_list[4][kTilePix];
+#ifdef GSD_BWD_BUTTERFLY
+    __shared__ float4 s_box[kTilePix];
+#else
+    // the alpha boxes are read only by the compaction, the (G dL/dalpha, alpha T) hand-off only after it (a
+    // barrier apart): one region, 30 KB of LDS per workgroup in all -> 5 workgroups per CU
+    __shared__ union {
+        float4 box[kTilePix];
+        float2 qa[4][kBwdGroup][65];  // per wave: per record and pixel; +1 pad
+    } s_u;
+    float4* s_box = s_u.box;
+#endif
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
     const int lane = tg.lane;
@@ -271,6 +298,15 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         dpix1 = p.dL_dpix[plane + pid];
         dpix2 = p.dL_dpix[2 * plane + pid];
     }
+#ifndef GSD_BWD_BUTTERFLY
+    float2(*qa)[65] = s_u.qa[tg.wave];
+    // dL/dpixel of the four pixels of the lane's quad (DPP quad broadcasts), for phase 2 below
+    float3 dpq[4];
+    dpq[0] = make_float3(quad_bcast<0>(dpix0), quad_bcast<0>(dpix1), quad_bcast<0>(dpix2));
+    dpq[1] = make_float3(quad_bcast<1>(dpix0), quad_bcast<1>(dpix1), quad_bcast<1>(dpix2));
+    dpq[2] = make_float3(quad_bcast<2>(dpix0), quad_bcast<2>(dpix1), quad_bcast<2>(dpix2));
+    dpq[3] = make_float3(quad_bcast<3>(dpix0), quad_bcast<3>(dpix1), quad_bcast<3>(dpix2));
+#endif
     float adot = 0.f;  // accum_rec . dL/dpixel (accum_rec with last_color / last_alpha folded in)
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float kbg = -T_final * bg_dot;
@@ -298,6 +334,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
         const int m = wave_compact<true>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
+#ifndef GSD_BWD_BUTTERFLY
+        lds_barrier();  // every wave is done with s_box before s_u.qa is written
+#endif
+#ifdef GSD_BWD_BUTTERFLY
         for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
             // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
             float Gs[kBwdBatch], As[kBwdBatch], Os[kBwdBatch], Dx[kBwdBatch], Dy[kBwdBatch];
@@ -372,15 +412,97 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 }
             }
         }
+#else
+        for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
+            // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
+            // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
+            // v = G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
+            // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
+            // needed from the lane.
+            bool any = false;
+#pragma unroll
+            for (int sb = 0; sb < kBwdGroup / kBwdBatch; ++sb) {
+                const int jb = j0 + sb * kBwdBatch;
+                if (sb > 0 && jb >= m) {  // wave-uniform: the tail of the list
+#pragma unroll
+                    for (int u = 0; u < kBwdBatch; ++u) qa[sb * kBwdBatch + u][lane] = make_float2(0.f, 0.f);
+                    continue;
+                }
+                float Gs[kBwdBatch], As[kBwdBatch];
+                int slot[kBwdBatch];
+#pragma unroll
+                for (int u = 0; u < kBwdBatch; ++u) {
+                    slot[u] = list[min(jb + u, m - 1)];
+                    float dx, dy;
+                    As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u], dx, dy);
+                }
+#pragma unroll
+                for (int u = 0; u < kBwdBatch; ++u) {
+#pragma clang fp contract(fast)
+                    const bool valid = (jb + u < m) & (front_base - slot[u] < last_contributor) &
+                                       (As[u] >= 1.0f / 255.0f);
+                    any |= valid;
+                    const float alpha = valid ? As[u] : 0.f;
+                    const float G = valid ? Gs[u] : 0.f;
+                    const float inv1ma = fast_recip(1.f - alpha);
+                    T = T * inv1ma;  // backward.cu:503 (T recovered by division)
+                    const float4 c = s_rgb[slot[u]];
+                    const float cd = fmaf(c.z, dpix2, fmaf(c.y, dpix1, c.x * dpix0));
+                    const float diff = cd - adot;
+                    const float dL_dalpha = fmaf(diff, T, kbg * inv1ma);  // backward.cu:512-529
+                    qa[sb * kBwdBatch + u][lane] = make_float2(G * dL_dalpha, alpha * T);
+                    adot = fmaf(alpha, diff, adot);
+                }
+            }
+            if (!__ballot(any)) continue;  // wave-uniform: no pixel took any of these records
+            __builtin_amdgcn_wave_barrier();
+            // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
+            // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i is
+            // (qx0 + 4 (g & 1) + i, qy0 + (g >> 1)): dx = mx - px runs over i, dy = my - py is the lane's
+            // constant.  Sums: S0 = sum v, S1 = sum v dx, S3 = sum v dx^2, C = sum w dL/dpixel; the dy
+            // moments follow as dy S0, dy S1, dy^2 S0 (backward.cu:545-554 expanded over pixels).
+            const int r = lane & 3, grp = lane >> 2;
+            const int rs = list[min(j0 + r, m - 1)];
+            const float2 mxy = s_xy[rs];
+            const float px0 = tg.qx0 + (float)(4 * (grp & 1));
+            float dxi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dxi[i] = mxy.x - (px0 + (float)i);
+            const float dy = mxy.y - (tg.qy0 + (float)(grp >> 1));
+            RecordSums acc;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc.add(qa[r][4 * grp + i], dxi[i], dpq[i]);
+            const float S0 = acc.S0, S1 = acc.S1, S3 = acc.S3, C0 = acc.C0, C1 = acc.C1, C2 = acc.C2;
+            // the nine sums in s_acc order (kRecMean2D.. moments, opacity, colour), summed over the 16 groups
+            // g (lane bits 5, 4 transposed; bits 3, 2 by row rotations): afterwards lane 4 g + r with bits 2-3
+            // clear holds record r's total of quantity (bit 5) + 2 (bit 4) [+ 4 for c1, 8 for c2]
+            const float a0 = S1, a1 = dy * S0, a2 = S3, a3 = dy * S1, a4 = dy * dy * S0, a5 = S0;
+            const float c0 = sum4(sum8(pair16(pair32(a0, a1), pair32(a2, a3))));
+            const float c1 = sum4(sum8(pair16(pair32(a4, a5), pair32(C0, C1))));
+            const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
+            __builtin_amdgcn_wave_barrier();  // phase-1 writes of the next group must wait for these reads
+            if (!(lane & 12) && j0 + r < m) {
+                const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
+                atomicAdd(&s_acc[qk][rs], c0);
+                atomicAdd(&s_acc[4 + qk][rs], c1);
+                if (qk == 0) atomicAdd(&s_acc[8][rs], c2);
+            }
+        }
+#endif
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
             const float4 co = s_co[tid];
-            const float m0 = s_acc[0][tid], m1 = s_acc[1][tid];
+#ifdef GSD_BWD_BUTTERFLY
+            const float o = 1.f;
+#else
+            const float o = co.w;  // the moments were summed over G dL/dalpha; q = o G dL/dalpha
+#endif
+            const float m0 = s_acc[0][tid] * o, m1 = s_acc[1][tid] * o;
             s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
             s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
-            s_acc[2][tid] *= -0.5f;
-            s_acc[3][tid] *= -0.5f;
-            s_acc[4][tid] *= -0.5f;
+            s_acc[2][tid] *= -0.5f * o;
+            s_acc[3][tid] *= -0.5f * o;
+            s_acc[4][tid] *= -0.5f * o;
         }
         lds_barrier();
         // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,
