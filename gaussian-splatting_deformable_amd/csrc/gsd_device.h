@@ -183,6 +183,15 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Hand-off of LDS data between lanes of one wave.  The wave's LDS instructions execute in issue order, so
+// only the compiler has to be stopped from reordering them: it reasons per lane, and a load of another lane's
+// slot whose address provably differs from this lane's stores may otherwise be hoisted above them
+// (__builtin_amdgcn_wave_barrier alone is not a memory barrier to the compiler).
+__device__ __forceinline__ void wave_lds_handoff() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // wave_sum4 in two halves, so columns 0/1 can be folded as soon as they exist
 // (fewer live registers): pair32(c0, c1) leaves lanes 0-31 with column 0 and
 // lanes 32-63 with column 1 (each over lane l and l ^ 32); fin16(pair32(c0, c1),

@@ -16,13 +16,15 @@
 // pairs never reach the ALUs on the bench scene.
 //
 // Backward: the reference issues 9 float atomicAdds per (pixel, Gaussian) pair
-// (backward.cu:523,545-554), all 256 lanes on the same address.  Here each
-// wave computes 4 records' partials, reduces them across its 64 lanes with one
-// transposed butterfly per quantity (wave_sum4: permlane32/16 swaps + DPP),
-// 4 lanes add the 4 wave totals into LDS accumulators, and after each
-// 256-record batch every record's 9 sums go to HBM as one set of global
-// atomics: at most 9 global atomics per (Gaussian, tile) instance instead of
-// 9 per (Gaussian, pixel) pair.
+// (backward.cu:523,545-554), all 256 lanes on the same address.  Here the work
+// per record is split in two phases.  Pixel-major: each lane replays its pixel
+// back to front and hands two numbers per record to LDS, G dL/dalpha and
+// alpha T.  Record-major: every one of the record's nine sums (dL/dmean2D,
+// dL/dconic, dL/dopacity, dL/dcolor) is a dot product of those two with
+// per-pixel factors (the pixel offsets and dL/dpixel), so a quad of lanes sums
+// one record over 4 pixels each and a short transposed butterfly finishes it;
+// the sums go to LDS accumulators and, after each 256-record batch, to HBM as
+// one set of global atomics per (Gaussian, tile) instance.
 #include "gsd_kernels.h"
 
 namespace gsd {
@@ -102,7 +104,7 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
         }
         m += __popcll(mask);
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_handoff();
     return m;
 }
 
@@ -256,9 +258,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float s_acc[9][kTilePix + 1];  // +1: a record's nine sums sit in nine different banks
     __shared__ uint8_t s_list[4][kTilePix];
-#ifdef GSD_BWD_BUTTERFLY
-    __shared__ float4 s_box[kTilePix];
-#else
     // the alpha boxes are read only by the compaction, the (G dL/dalpha, alpha T) hand-off only after it (a
     // barrier apart): one region, 30 KB of LDS per workgroup in all -> 5 workgroups per CU
     __shared__ union {
@@ -266,7 +265,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         float2 qa[4][kBwdGroup][65];  // per wave: per record and pixel; +1 pad
     } s_u;
     float4* s_box = s_u.box;
-#endif
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
     const int lane = tg.lane;
@@ -298,7 +296,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         dpix1 = p.dL_dpix[plane + pid];
         dpix2 = p.dL_dpix[2 * plane + pid];
     }
-#ifndef GSD_BWD_BUTTERFLY
     float2(*qa)[65] = s_u.qa[tg.wave];
     // dL/dpixel of the four pixels of the lane's quad (DPP quad broadcasts), for phase 2 below
     float3 dpq[4];
@@ -306,7 +303,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     dpq[1] = make_float3(quad_bcast<1>(dpix0), quad_bcast<1>(dpix1), quad_bcast<1>(dpix2));
     dpq[2] = make_float3(quad_bcast<2>(dpix0), quad_bcast<2>(dpix1), quad_bcast<2>(dpix2));
     dpq[3] = make_float3(quad_bcast<3>(dpix0), quad_bcast<3>(dpix1), quad_bcast<3>(dpix2));
-#endif
     float adot = 0.f;  // accum_rec . dL/dpixel (accum_rec with last_color / last_alpha folded in)
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float kbg = -T_final * bg_dot;
@@ -334,85 +330,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
         const int m = wave_compact<true>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
-#ifndef GSD_BWD_BUTTERFLY
         lds_barrier();  // every wave is done with s_box before s_u.qa is written
-#endif
-#ifdef GSD_BWD_BUTTERFLY
-        for (int j0 = 0; j0 < m; j0 += kBwdBatch) {
-            // branch-free G / alpha of kBwdBatch records (independent: the exps overlap) ...
-            float Gs[kBwdBatch], As[kBwdBatch], Os[kBwdBatch], Dx[kBwdBatch], Dy[kBwdBatch];
-            int slot[kBwdBatch];
-#pragma unroll
-            for (int u = 0; u < kBwdBatch; ++u) {
-                slot[u] = list[min(j0 + u, m - 1)];
-                const float4 co = s_co[slot[u]];
-                As[u] = record_alpha(s_xy[slot[u]], co, pxf, pyf, Gs[u], Dx[u], Dy[u]);
-                Os[u] = co.w;
-            }
-            // ... then the sequential back-to-front recurrence (backward.cu:482-555), branch-free: a record
-            // a lane skips (past its last contributor, alpha < 1/255, or beyond the list) gets alpha = G = 0,
-            // which leaves T unchanged (1/(1-0) == 1 exactly) and zeroes its partials.
-            // accum_rec only enters through (c - accum_rec) . dL/dpixel, so the lane keeps the scalar
-            // adot = accum_rec . dL/dpixel, folded forward at the end of each record (accum_rec = alpha c +
-            // (1-alpha) accum_rec, backward.cu:516-520, dotted with dL/dpixel): one FMA instead of six ops.
-            // The mean2D / conic partials are reduced as the moments q dx, q dy, q dx^2, q dx dy, q dy^2
-            // (q = o G dL/dalpha); the flush below turns them into dL/dmean2D = (a, b; b, c) (q dx, q dy)
-            // (-W/2, -H/2) and dL/dconic = -1/2 (q dx^2, q dx dy, q dy^2) -- linear, so exact up to rounding,
-            // and 5 ops per record instead of 12.  Records 0/1 and 2/3 are folded across the wave halves as
-            // soon as each pair exists (pair32), so at most 27 partials are live.
-            float h[2][9], v[9], prev[9];
-            bool any = false;
-#pragma unroll
-            for (int u = 0; u < kBwdBatch; ++u) {
-                // gradient arithmetic has no bit-exact contract: let the compiler fuse to FMA
-#pragma clang fp contract(fast)
-                // non-short-circuit (&): straight-line selects instead of exec-mask branches.  A pixel outside
-                // the image has last_contributor 0, and a slot's list position is >= 0, so `inside` is implied.
-                const bool valid = (j0 + u < m) & (front_base - slot[u] < last_contributor) &
-                                   (As[u] >= 1.0f / 255.0f);
-                any |= valid;
-                const float alpha = valid ? As[u] : 0.f;
-                const float G = valid ? Gs[u] : 0.f;
-                const float inv1ma = fast_recip(1.f - alpha);
-                T = T * inv1ma;  // backward.cu:503 (T recovered by division)
-                const float aT = alpha * T;
-                const float4 c = s_rgb[slot[u]];
-                const float cd = c.x * dpix0 + c.y * dpix1 + c.z * dpix2;
-                const float diff = cd - adot;
-                const float dL_dalpha = diff * T + kbg * inv1ma;  // backward.cu:512-529
-                v[6] = aT * dpix0;
-                v[7] = aT * dpix1;
-                v[8] = aT * dpix2;
-                v[5] = G * dL_dalpha;
-                const float q = Os[u] * v[5];
-                v[0] = q * Dx[u];
-                v[1] = q * Dy[u];
-                v[2] = v[0] * Dx[u];
-                v[3] = v[0] * Dy[u];
-                v[4] = v[1] * Dy[u];
-                adot = fmaf(alpha, diff, adot);
-#pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    if (u & 1)
-                        h[u >> 1][k] = pair32(prev[k], v[k]);
-                    else
-                        prev[k] = v[k];
-                }
-            }
-            if (__ballot(any)) {  // wave-uniform
-                // all nine reductions first (independent: their DPP chains interleave), then one masked store
-                float r[9];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) r[k] = fin16(h[0][k], h[1][k]);
-                const int col = fin16_column(lane);
-                if ((lane & 15) == 0 && j0 + col < m) {
-                    const int dst = list[j0 + col];
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) atomicAdd(&s_acc[k][dst], r[k]);
-                }
-            }
-        }
-#else
         for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
             // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
             // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
@@ -455,7 +373,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 }
             }
             if (!__ballot(any)) continue;  // wave-uniform: no pixel took any of these records
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_handoff();
             // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
             // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i is
             // (qx0 + 4 (g & 1) + i, qy0 + (g >> 1)): dx = mx - px runs over i, dy = my - py is the lane's
@@ -480,7 +398,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float c0 = sum4(sum8(pair16(pair32(a0, a1), pair32(a2, a3))));
             const float c1 = sum4(sum8(pair16(pair32(a4, a5), pair32(C0, C1))));
             const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
-            __builtin_amdgcn_wave_barrier();  // phase-1 writes of the next group must wait for these reads
+            wave_lds_handoff();  // phase-1 writes of the next group must stay behind these reads
             if (!(lane & 12) && j0 + r < m) {
                 const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
                 atomicAdd(&s_acc[qk][rs], c0);
@@ -488,15 +406,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 if (qk == 0) atomicAdd(&s_acc[8][rs], c2);
             }
         }
-#endif
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
             const float4 co = s_co[tid];
-#ifdef GSD_BWD_BUTTERFLY
-            const float o = 1.f;
-#else
             const float o = co.w;  // the moments were summed over G dL/dalpha; q = o G dL/dalpha
-#endif
             const float m0 = s_acc[0][tid] * o, m1 = s_acc[1][tid] * o;
             s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
             s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
