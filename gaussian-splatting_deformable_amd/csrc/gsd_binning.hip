@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(int T, const uint32_
 // duplicateWithKeys (rasterizer_impl.cu:70-111), scattered straight into tile buckets.
 __global__ __launch_bounds__(256) void k_scatter_keys(BinParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= p.P) return;
+    if (idx >= p.P || over_capacity(p.k_guard, p.k_cap)) return;
     const int rad = p.radii[idx];
     if (!(rad > 0)) return;
     const float2 xy = p.means2D[idx];
@@ -124,6 +124,7 @@ __global__ __launch_bounds__(kHistThreads) void k_scatter_hist(HistParams p, con
                                                               const float* __restrict__ depths,
                                                               unsigned long long* __restrict__ bucket_keys) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_bins[];
+    if (over_capacity(p.k_guard, p.k_cap)) return;
     const int T = p.num_tiles;
     const uint32_t* row = p.hist + (size_t)blockIdx.x * T;
     for (int t = threadIdx.x; t < T; t += kHistThreads) s_bins[t] = tile_base[t] + row[t];
@@ -284,8 +285,10 @@ __device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n
 __global__ __launch_bounds__(256) void k_tile_sort(int T, const uint2* __restrict__ ranges,
                                                    unsigned long long* __restrict__ keys,
                                                    unsigned long long* __restrict__ scratch,
-                                                   uint32_t* __restrict__ point_list) {
+                                                   uint32_t* __restrict__ point_list,
+                                                   const uint32_t* __restrict__ k_guard, uint32_t k_cap) {
     __shared__ unsigned long long s[kSortCap];
+    if (over_capacity(k_guard, k_cap)) return;
     const int tile = xcd_swizzle(blockIdx.x, T);
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -332,8 +335,10 @@ void launch_scatter_keys(const BinParams& p, hipStream_t s) {
     if (p.P > 0) hipLaunchKernelGGL(k_scatter_keys, dim3((p.P + 255) / 256), dim3(256), 0, s, p);
 }
 void launch_tile_sort(int T, const uint2* ranges, unsigned long long* keys, unsigned long long* scratch,
-                      uint32_t* point_list, hipStream_t s) {
-    if (T > 0) hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, T, ranges, keys, scratch, point_list);
+                      uint32_t* point_list, hipStream_t s, const uint32_t* k_guard, uint32_t k_cap) {
+    if (T > 0)
+        hipLaunchKernelGGL(k_tile_sort, dim3(T), dim3(256), 0, s, T, ranges, keys, scratch, point_list, k_guard,
+                           k_cap);
 }
 
 }  // namespace gsd

@@ -21,6 +21,8 @@ namespace {
 
 thread_local std::string g_err;
 thread_local uint32_t* g_pinned = nullptr;  // 16 B of pinned host memory for the counter read-back
+constexpr int kMaxDevices = 64;
+thread_local hipEvent_t g_kevent[kMaxDevices] = {};  // per device: "the read-back copy has landed"
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -136,9 +138,11 @@ size_t carve_bin(void* base, size_t K, Bin* g) {
         return r;
     };
     Bin v;
+    // point_list first: the only part the backward reads, so its offset does not depend on K (a forward
+    // may carve the buffer by its capacity before K is known, gsd_rasterize_forward)
+    v.point_list = reinterpret_cast<uint32_t*>(take(K * 4));
     v.keys = reinterpret_cast<unsigned long long*>(take(K * 8));
     v.scratch = reinterpret_cast<unsigned long long*>(take(K * 8));
-    v.point_list = reinterpret_cast<uint32_t*>(take(K * 4));
     if (g) *g = v;
     return off + kAlign;
 }
@@ -262,6 +266,15 @@ size_t gsd_image_buffer_bytes(int32_t width, int32_t height) {
 }
 size_t gsd_binning_buffer_bytes(int64_t K) { return carve_bin(nullptr, (size_t)(K < 0 ? 0 : K), nullptr); }
 
+namespace {
+// the largest K whose binning layout fits in `bytes`
+int64_t binning_capacity(size_t bytes) {
+    int64_t k = (int64_t)(bytes / 20);
+    while (k > 0 && gsd_binning_buffer_bytes(k) > bytes) k -= 1 + k / 4096;
+    return k;
+}
+}  // namespace
+
 void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t K, size_t* go, size_t* io, size_t* bo) {
     // carve from a fake, 256-aligned base so the returned pointers are the offsets
     char* const base = reinterpret_cast<char*>(uintptr_t(1) << 20);
@@ -286,15 +299,10 @@ void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t K, size_
     }
 }
 
-int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, int32_t* radii,
-                              int64_t* num_rendered, void* stream) {
-    int rc = validate(a, true);
-    if (rc) return rc;
-    if (!num_rendered) return fail(GSD_ERR_ARG, "num_rendered must not be null");
-    *num_rendered = 0;
-    if (a->P == 0) return GSD_OK;
-    if (!geom_buffer || !image_buffer) return fail(GSD_ERR_STATE, "state buffers must be allocated");
-    hipStream_t s = as_stream(stream);
+// Phase 1 on the stream: preprocess, tile counts, ranges, and the copy of num_rendered (+ the error flags)
+// into pinned host memory, followed by an event the host can wait on (read_back below).  No host wait.
+static int enqueue_bin(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, int32_t* radii, hipStream_t s,
+                uint32_t** counters_dev, hipEvent_t* done) {
     Geom g;
     Img im;
     const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
@@ -335,10 +343,79 @@ int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void*
     GSD_CHECK(a->debug, s);
     if (!g_pinned) GSD_HIP(hipHostMalloc(reinterpret_cast<void**>(&g_pinned), 16, hipHostMallocDefault));
     GSD_HIP(hipMemcpyAsync(g_pinned, im.counters, 8, hipMemcpyDeviceToHost, s));
-    GSD_HIP(hipStreamSynchronize(s));
+    int dev = 0;
+    GSD_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDevices) return fail(GSD_ERR_ARG, "device ordinal out of range");
+    if (!g_kevent[dev]) GSD_HIP(hipEventCreateWithFlags(&g_kevent[dev], hipEventDisableTiming));
+    GSD_HIP(hipEventRecord(g_kevent[dev], s));
+    *counters_dev = im.counters;
+    *done = g_kevent[dev];
+    return GSD_OK;
+}
+
+// Waits for phase 1's read-back (not for anything queued after it) -> *num_rendered; the prefiltered check.
+static int read_back(const gsd_raster_args* a, hipEvent_t done, int64_t* num_rendered) {
+    GSD_HIP(hipEventSynchronize(done));
     if (a->prefiltered && (g_pinned[1] & gsd::kErrPrefiltered))
         return fail(GSD_ERR_ARG, "Point is filtered although prefiltered is set. This shouldn't happen!");
     *num_rendered = (int64_t)g_pinned[0];
+    return GSD_OK;
+}
+
+int gsd_rasterize_forward_bin(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, int32_t* radii,
+                              int64_t* num_rendered, void* stream) {
+    int rc = validate(a, true);
+    if (rc) return rc;
+    if (!num_rendered) return fail(GSD_ERR_ARG, "num_rendered must not be null");
+    *num_rendered = 0;
+    if (a->P == 0) return GSD_OK;
+    if (!geom_buffer || !image_buffer) return fail(GSD_ERR_STATE, "state buffers must be allocated");
+    uint32_t* counters = nullptr;
+    hipEvent_t done = nullptr;
+    rc = enqueue_bin(a, geom_buffer, image_buffer, radii, as_stream(stream), &counters, &done);
+    if (rc) return rc;
+    return read_back(a, done, num_rendered);
+}
+
+// Phase 2 on the stream.  With k_guard (the device copy of num_rendered) the launches are queued before
+// the host knows K: the buffer is carved for K = capacity and every kernel exits when *k_guard > K.
+static int enqueue_render(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, void* binning_buffer, int64_t K,
+                   const int32_t* radii, float* out_color, hipStream_t s, const uint32_t* k_guard) {
+    Geom g;
+    Img im;
+    Bin b;
+    const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
+    carve_geom(geom_buffer, a->P, T, &g);
+    carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
+    carve_bin(binning_buffer, (size_t)K, &b);
+    const uint32_t cap = (uint32_t)std::min<int64_t>(K, UINT32_MAX);
+    if (K > 0) {
+        if (hist_binning(T)) {
+            gsd::HistParams hp = hist_params(a, g, T);
+            hp.radii = radii ? radii : g.radii;
+            hp.k_guard = k_guard; hp.k_cap = cap;
+            timed(kScatter, s, [&] { gsd::launch_scatter_hist(hp, im.tile_cursor, g.depths, b.keys, s); });
+        } else {
+            gsd::BinParams bp{};
+            bp.P = a->P; bp.grid_x = gx; bp.grid_y = gy; bp.num_tiles = T;
+            bp.radii = radii ? radii : g.radii;
+            bp.means2D = g.means2D; bp.depths = g.depths; bp.tile_cursor = im.tile_cursor; bp.bucket_keys = b.keys;
+            bp.k_guard = k_guard; bp.k_cap = cap;
+            timed(kScatter, s, [&] { gsd::launch_scatter_keys(bp, s); });
+        }
+        GSD_CHECK(a->debug, s);
+        timed(kTileSort, s,
+              [&] { gsd::launch_tile_sort(T, im.ranges, b.keys, b.scratch, b.point_list, s, k_guard, cap); });
+        GSD_CHECK(a->debug, s);
+    }
+    gsd::RenderParams rp{};
+    rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
+    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
+    rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
+    rp.out_color = out_color;
+    rp.k_guard = k_guard; rp.k_cap = cap;
+    timed(kRenderFwd, s, [&] { gsd::launch_render_fwd(rp, s); });
+    GSD_CHECK(a->debug, s);
     return GSD_OK;
 }
 
@@ -350,52 +427,41 @@ int gsd_rasterize_forward_render(const gsd_raster_args* a, void* geom_buffer, vo
     if (a->P == 0) return GSD_OK;
     if (!geom_buffer || !image_buffer || (K > 0 && !binning_buffer) || !out_color)
         return fail(GSD_ERR_STATE, "state buffers / out_color must be allocated");
-    hipStream_t s = as_stream(stream);
-    Geom g;
-    Img im;
-    Bin b;
-    const int gx = grid_x(a), gy = grid_y(a), T = gx * gy;
-    carve_geom(geom_buffer, a->P, T, &g);
-    carve_img(image_buffer, (size_t)a->width * a->height, T, &im);
-    carve_bin(binning_buffer, (size_t)K, &b);
-    if (K > 0) {
-        if (hist_binning(T)) {
-            gsd::HistParams hp = hist_params(a, g, T);
-            hp.radii = radii ? radii : g.radii;
-            timed(kScatter, s, [&] { gsd::launch_scatter_hist(hp, im.tile_cursor, g.depths, b.keys, s); });
-        } else {
-            gsd::BinParams bp{};
-            bp.P = a->P; bp.grid_x = gx; bp.grid_y = gy; bp.num_tiles = T;
-            bp.radii = radii ? radii : g.radii;
-            bp.means2D = g.means2D; bp.depths = g.depths; bp.tile_cursor = im.tile_cursor; bp.bucket_keys = b.keys;
-            timed(kScatter, s, [&] { gsd::launch_scatter_keys(bp, s); });
-        }
-        GSD_CHECK(a->debug, s);
-        timed(kTileSort, s, [&] { gsd::launch_tile_sort(T, im.ranges, b.keys, b.scratch, b.point_list, s); });
-        GSD_CHECK(a->debug, s);
-    }
-    gsd::RenderParams rp{};
-    rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
-    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
-    rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
-    rp.out_color = out_color;
-    timed(kRenderFwd, s, [&] { gsd::launch_render_fwd(rp, s); });
-    GSD_CHECK(a->debug, s);
-    return GSD_OK;
+    return enqueue_render(a, geom_buffer, image_buffer, binning_buffer, K, radii, out_color, as_stream(stream),
+                          nullptr);
 }
 
 int gsd_rasterize_forward(const gsd_raster_args* a, void* geom_buffer, void* image_buffer, void* binning_buffer,
                           size_t binning_bytes, int32_t* radii, float* out_color, int64_t* num_rendered,
                           void* stream) {
-    int rc = gsd_rasterize_forward_bin(a, geom_buffer, image_buffer, radii, num_rendered, stream);
+    int rc = validate(a, true);
     if (rc) return rc;
+    if (!num_rendered) return fail(GSD_ERR_ARG, "num_rendered must not be null");
+    *num_rendered = 0;
     if (a->P == 0) return GSD_OK;
-    if (gsd_binning_buffer_bytes(*num_rendered) > binning_bytes) {
+    if (!geom_buffer || !image_buffer || !out_color)
+        return fail(GSD_ERR_STATE, "state buffers / out_color must be allocated");
+    hipStream_t s = as_stream(stream);
+    uint32_t* counters = nullptr;
+    hipEvent_t done = nullptr;
+    rc = enqueue_bin(a, geom_buffer, image_buffer, radii, s, &counters, &done);
+    if (rc) return rc;
+    // Phase 2 goes behind phase 1 on the stream before the host waits for num_rendered, so the device never
+    // idles on the read-back; its kernels check the device count against what the buffer holds.
+    const int64_t cap = binning_buffer ? binning_capacity(binning_bytes) : 0;
+    if (cap > 0) {
+        rc = enqueue_render(a, geom_buffer, image_buffer, binning_buffer, cap, radii, out_color, s, counters);
+        if (rc) return rc;
+    }
+    rc = read_back(a, done, num_rendered);
+    if (rc) return rc;
+    if (*num_rendered > cap || (cap == 0 && *num_rendered == 0)) {
+        if (*num_rendered == 0)  // nothing to bin: the render phase still writes the background image
+            return enqueue_render(a, geom_buffer, image_buffer, binning_buffer, 0, radii, out_color, s, nullptr);
         g_err = "binning buffer too small for num_rendered: allocate gsd_binning_buffer_bytes(num_rendered)";
         return GSD_NEED_BINNING;
     }
-    return gsd_rasterize_forward_render(a, geom_buffer, image_buffer, binning_buffer, *num_rendered, radii,
-                                        out_color, stream);
+    return GSD_OK;
 }
 
 int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const void* geom_buffer,

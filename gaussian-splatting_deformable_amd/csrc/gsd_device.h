@@ -265,6 +265,13 @@ __device__ __forceinline__ float wave_sum8(const float (&c)[8]) {
     return t;
 }
 
+// Capacity guard of a launch queued before num_rendered reached the host (gsd_rasterize_forward): true
+// when the count the tile scan wrote exceeds what the binning buffer holds -- the launch then does nothing
+// and the host re-runs it with a buffer of the right size.  One uniform (scalar) load per workgroup.
+__device__ __forceinline__ bool over_capacity(const uint32_t* k_guard, uint32_t k_cap) {
+    return k_guard != nullptr && *k_guard > k_cap;
+}
+
 // XCD-aware remap of a 1-D block index: blocks b and b+8 are dealt to the same
 // XCD (MI355X_MICROARCH.md "Workgroup dispatch"), so give each XCD a
 // contiguous run of tiles -- neighbouring tiles gather the same Gaussians and

@@ -93,6 +93,8 @@ struct BinParams {
     const float* depths;
     uint32_t* tile_cursor;
     unsigned long long* bucket_keys;
+    const uint32_t* k_guard;  // optional: skip the launch when *k_guard (num_rendered) > k_cap
+    uint32_t k_cap;
 };
 
 // LDS-histogram binning (gsd_binning.hip): block b owns Gaussians [b*chunk, (b+1)*chunk)
@@ -102,6 +104,8 @@ struct HistParams {
     const float2* means2D;
     uint32_t* hist;  // [num_blocks][num_tiles]
     uint32_t* part;  // [ceil(num_blocks / kColSeg)][num_tiles]
+    const uint32_t* k_guard;  // optional: k_scatter_hist does nothing when *k_guard (num_rendered) > k_cap
+    uint32_t k_cap;
 };
 
 struct RenderParams {
@@ -115,6 +119,8 @@ struct RenderParams {
     float* final_T;
     uint32_t* n_contrib;
     float* out_color;
+    const uint32_t* k_guard;  // optional: skip the launch when *k_guard (num_rendered) > k_cap
+    uint32_t k_cap;
 };
 
 struct RenderBwdParams {
@@ -194,7 +200,7 @@ void launch_tile_scan(int num_tiles, const uint32_t* tile_count, uint2* ranges, 
                       uint32_t* counters, hipStream_t s);
 void launch_scatter_keys(const BinParams& p, hipStream_t s);
 void launch_tile_sort(int num_tiles, const uint2* ranges, unsigned long long* keys, unsigned long long* scratch,
-                      uint32_t* point_list, hipStream_t s);
+                      uint32_t* point_list, hipStream_t s, const uint32_t* k_guard = nullptr, uint32_t k_cap = 0);
 void launch_render_fwd(const RenderParams& p, hipStream_t s);
 void launch_render_bwd(const RenderBwdParams& p, hipStream_t s);
 void launch_se3_fwd(int P, const float* twist, const float* means_in, const float* rot_in, float* means_out,

@@ -181,6 +181,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float4 s_box[kTilePix];
     __shared__ uint8_t s_list[4][kTilePix];
+    if (over_capacity(p.k_guard, p.k_cap)) return;
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
     bool done = !tg.inside;

@@ -138,7 +138,7 @@ size_t gsd_binning_buffer_bytes(int64_t num_rendered);
  * from the state buffer's first 256-B aligned address, of
  *   geom[6]  = means2D float2, conic_opacity float4, rgb float4, depths f32, radii i32, clamped u8
  *   image[6] = final_T f32, n_contrib u32, ranges uint2, tile_count u32, tile_cursor u32, counters u32
- *   bin[3]   = bucket keys u64, merge scratch u64, point_list u32                          */
+ *   bin[3]   = bucket keys u64, merge scratch u64, point_list u32 (point_list first in memory) */
 void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t num_rendered, size_t* geom_offsets,
                       size_t* image_offsets, size_t* binning_offsets);
 
@@ -157,10 +157,12 @@ int gsd_rasterize_forward_render(const gsd_raster_args* args, void* geom_buffer,
                                  float* out_color, void* stream);
 
 /* Both forward phases in one call, for a caller that allocates the binning buffer before num_rendered is
- * known (e.g. from the previous view's count plus headroom): phase 1, the num_rendered read-back, and -- when
- * binning_bytes >= gsd_binning_buffer_bytes(*num_rendered) -- phase 2 without returning to the caller in
- * between (the device idles only for the read-back, not for the caller's allocation and second call).
- * Returns GSD_NEED_BINNING (phase 1 done, *num_rendered set) when the buffer is too small. */
+ * known (e.g. from the previous view's count plus headroom).  Phase 2 is queued behind phase 1 before the
+ * host waits for the num_rendered read-back (its kernels compare the device-side count with what
+ * binning_bytes holds and do nothing when it does not fit), so the device never idles on the read-back.
+ * Returns GSD_NEED_BINNING (phase 1 done, *num_rendered set, phase 2 not done) when the buffer is too
+ * small: allocate gsd_binning_buffer_bytes(*num_rendered) and call gsd_rasterize_forward_render.  The
+ * backward only needs the buffer's point_list, which sits at an offset independent of the capacity. */
 int gsd_rasterize_forward(const gsd_raster_args* args, void* geom_buffer, void* image_buffer, void* binning_buffer,
                           size_t binning_bytes, int32_t* radii, float* out_color, int64_t* num_rendered,
                           void* stream);

@@ -46,9 +46,11 @@ def test_state_layout_is_aligned_and_disjoint():
     lib = _native.load()
     go, io, bo = (ctypes.c_size_t * 6)(), (ctypes.c_size_t * 6)(), (ctypes.c_size_t * 3)()
     lib.gsd_state_layout(1001, 333, 217, 12345, go, io, bo)
-    for arr in (list(go), list(io), list(bo)):
+    # binning: point_list first (the backward's part, at a K-independent offset), then keys, scratch
+    for arr in (list(go), list(io), [bo[2], bo[0], bo[1]]):
         assert all(o % 256 == 0 for o in arr)
         assert arr == sorted(arr) and len(set(arr)) == len(arr)
+    assert bo[2] == 0
     assert go[5] + 1001 <= lib.gsd_geom_buffer_bytes(1001, 333, 217) - 256
 
 
