@@ -48,6 +48,9 @@ struct PreprocessParams {
 // unit of a global atomic) holding dL/dmean2D x,y | dL/dconic a,b,c | dL/dopacity | dL/dcolor r,g,b.
 constexpr int kGradRec = 16;
 enum GradRecField { kRecMean2D = 0, kRecConic = 2, kRecOpacity = 5, kRecColor = 6, kRecUsed = 9 };
+// floats 9..11 of a record: the view-direction term of dL/dmean3D, left there by k_preprocess_bwd_sh for
+// k_preprocess_bwd (the two halves of the per-Gaussian backward)
+constexpr int kRecShMean = 9;
 
 struct PreprocessBwdParams {
     int P, D, M;
@@ -66,7 +69,7 @@ struct PreprocessBwdParams {
     const float* view;
     const float* proj;
     const float* campos;
-    const float* grad_rec;    // (P, kGradRec) per-Gaussian gradient records accumulated by k_render_bwd
+    float* grad_rec;          // (P, kGradRec) per-Gaussian gradient records accumulated by k_render_bwd
     float* dL_dmean2D;        // (P,3) outputs unpacked from the records (written for every Gaussian)
     float* dL_dopacity;       // (P)
     float* dL_dcolor;         // (P,3)

@@ -50,11 +50,14 @@ __device__ __forceinline__ ShStrides sh_strides(const Prm& p) {
     return ShStrides{3, 1, 3LL * (p.M - 1), 1};
 }
 
-template <int NC>
+// kSrc: which operand holds the coefficients -- -1 decided at run time, 0 shs, 1 the split operand, 2 the
+// split operand plus an offset.  A compile-time source keeps the other paths' loads out of the kernel's
+// register allocation (the offset path alone holds 96 loaded values).
+template <int NC, int kSrc = -1>
 __device__ __forceinline__ void load_sh(const float* __restrict__ shs, const float* __restrict__ dc,
                                         const float* __restrict__ rest, const float* __restrict__ off, int M,
                                         int idx, float (&s)[48], const ShStrides& st) {
-    if (shs) {
+    if (kSrc < 0 ? shs != nullptr : kSrc == 0) {
         const float* row = shs + (size_t)idx * M * 3;
 #pragma unroll
         for (int k = 0; k < NC * 3; ++k) s[k] = row[k];
@@ -78,7 +81,7 @@ __device__ __forceinline__ void load_sh(const float* __restrict__ shs, const flo
 #pragma unroll
         for (int k = 3; k < NC * 3; ++k) s[k] = r[(k - 3) * st.rest_se];
     }
-    if (off) {
+    if (kSrc < 0 ? off != nullptr : kSrc == 2) {
         const float* o = off + (size_t)idx * M * 3;
 #pragma unroll
         for (int k = 0; k < NC * 3; ++k) s[k] = s[k] + o[k];
@@ -367,23 +370,6 @@ __device__ __forceinline__ void cov3d_bwd(const float3 scale, float mod, const f
     drot.w = 2 * r * (D01 - D10) + 2 * x * (D20 + D02) + 2 * y * (D12 + D21) - 4 * z * (D11 + D00);
 }
 
-// dst[k - K0] (+)= ds[k] for k in [K0, K1)
-template <int K0, int K1>
-__device__ __forceinline__ void sink_sh(float* __restrict__ dst, const float (&ds)[48], bool acc, long long se = 1) {
-    float old[K1 - K0 > 0 ? K1 - K0 : 1];
-    if (se == 1) {  // contiguous rows: compile-time offsets
-#pragma unroll
-        for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[k - K0] : 0.f;
-#pragma unroll
-        for (int k = K0; k < K1; ++k) dst[k - K0] = old[k - K0] + ds[k];
-        return;
-    }
-#pragma unroll
-    for (int k = K0; k < K1; ++k) old[k - K0] = acc ? dst[(k - K0) * se] : 0.f;
-#pragma unroll
-    for (int k = K0; k < K1; ++k) dst[(k - K0) * se] = old[k - K0] + ds[k];
-}
-
 // SH gradient entries [from, M) x 3 of one Gaussian: the coefficients above the active degree get zero
 // gradients (and all of them for a skipped Gaussian), as in the reference's zero-initialised dL_dsh.
 // Accumulating split sinks are left untouched.
@@ -444,9 +430,20 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
 }
 
 // Gradients of a Gaussian the backward skips (radii == 0): every per-Gaussian output is written, so callers need
-// not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  Accumulating SH
-// sinks are left untouched.
-__device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx, const ShStrides& st) {
+// not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  The SH half
+// writes the d_rgb row or the SH gradient entries (accumulating SH sinks are left untouched) ...
+__device__ __forceinline__ void zero_sh_outputs(const PreprocessBwdParams& p, int idx, const ShStrides& st) {
+    if (p.d_rgb) {  // the SH gradient is assembled from the views' d_rgb rows (gsd_sh_grad_views)
+        p.d_rgb[3 * idx] = 0.f;
+        p.d_rgb[3 * idx + 1] = 0.f;
+        p.d_rgb[3 * idx + 2] = 0.f;
+        return;
+    }
+    if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0, st);
+}
+
+// ... and the geometry half everything else.
+__device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx) {
     if (p.dL_dmean2D) {
         p.dL_dmean2D[3 * idx] = 0.f;
         p.dL_dmean2D[3 * idx + 1] = 0.f;
@@ -480,22 +477,253 @@ __device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int i
         p.dL_dscales[3 * idx + 2] = 0.f;
     }
     if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p.d_rgb) {  // the SH gradient is assembled from the views' d_rgb rows (gsd_sh_grad_views)
-        p.d_rgb[3 * idx] = 0.f;
-        p.d_rgb[3 * idx + 1] = 0.f;
-        p.d_rgb[3 * idx + 2] = 0.f;
-        return;
-    }
-    if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0, st);
 }
 
-template <int DEG, bool kStr>
-__global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
+// The SH basis B_k of forward.cu:20-71 (the factor backward.cu:20-139 multiplies dL/dRGB by), k < (DEG+1)^2;
+// the same expressions as sh_channel_bwd's, so dL/dsh_k,c = B_k dL/dRGB_c to the bit.
+template <int DEG>
+__device__ __forceinline__ void sh_basis(float x, float y, float z, float (&B)[16]) {
+    B[0] = kSH0;
+    if (DEG > 0) {
+        B[1] = -kSH1 * y;
+        B[2] = kSH1 * z;
+        B[3] = -kSH1 * x;
+    }
+    if (DEG > 1) {
+        const float xx = x * x, yy = y * y, zz = z * z;
+        const float xy = x * y, yz = y * z, xz = x * z;
+        B[4] = kSH2_0 * xy;
+        B[5] = kSH2_1 * yz;
+        B[6] = kSH2_2 * (2.f * zz - xx - yy);
+        B[7] = kSH2_3 * xz;
+        B[8] = kSH2_4 * (xx - yy);
+        if (DEG > 2) {
+            B[9] = kSH3_0 * y * (3.f * xx - yy);
+            B[10] = kSH3_1 * xy * z;
+            B[11] = kSH3_2 * y * (4.f * zz - xx - yy);
+            B[12] = kSH3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+            B[13] = kSH3_4 * x * (4.f * zz - xx - yy);
+            B[14] = kSH3_5 * z * (xx - yy);
+            B[15] = kSH3_6 * x * (xx - 3.f * yy);
+        }
+    }
+}
+
+// dst[(k - K0) * se] (+)= B_k dc for coefficients k in [K0, K1), three channels each (element stride se).
+// Accumulating: every old value is loaded before the first store, so the loads issue together instead of
+// each waiting behind a store it might alias.
+template <int K0, int K1, bool kAcc>
+__device__ __forceinline__ void sink_basis(float* __restrict__ dst, const float (&B)[16], const float3 dc,
+                                           long long se) {
+    constexpr int n = K1 > K0 ? 3 * (K1 - K0) : 1;
+    float old[n];
+#pragma unroll
+    for (int e = 0; e < 3 * (K1 - K0); ++e) old[e] = kAcc ? dst[e * se] : 0.f;
+#pragma unroll
+    for (int k = K0; k < K1; ++k) {
+        const int e = 3 * (k - K0);
+        dst[e * se] = old[e] + B[k] * dc.x;
+        dst[(e + 1) * se] = old[e + 1] + B[k] * dc.y;
+        dst[(e + 2) * se] = old[e + 2] + B[k] * dc.z;
+    }
+}
+
+// The SH half of the per-Gaussian backward (backward.cu:20-139 and the view-direction term of
+// backward.cu:385-392), in its own launch ahead of k_preprocess_bwd.  Together with the projection math in
+// one kernel it needed 226 VGPRs (2 waves per SIMD) and streamed the SH rows at ~4 TB/s.  Here:
+//  - dL/dsh_k,c = B_k dL/dRGB_c is written straight from the 16 basis values (no 48-float gradient array);
+//  - the view-direction gradient sum_c dL/dRGB_c sum_k sh_k,c grad B_k is taken as sum_k w_k grad B_k with
+//    w_k = sh_k . dL/dRGB (reassociated over the three channels), so the 48 loaded coefficients fold into
+//    16 values as they arrive;
+//  - the operand source (kSrc: 0 shs, 1 split, 2 split + offset) and accumulation (kAcc) are compile-time,
+//    so no other path's loads share the register allocation.
+// The view-direction term of dL/dmean3D goes to floats 9..11 of the Gaussian's gradient record, where the
+// geometry half adds it.
+template <int DEG, bool kStr, int kSrc, bool kAcc>
+__global__ __launch_bounds__(256) void k_preprocess_bwd_sh(PreprocessBwdParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= p.P) return;
     const ShStrides st = sh_strides<kStr>(p);
+    if (!(p.radii[idx] > 0)) {
+        zero_sh_outputs(p, idx, st);
+        return;
+    }
+    float4* rec = reinterpret_cast<float4*>(p.grad_rec + (size_t)idx * kGradRec);
+    const float4 r1 = rec[1], r2 = rec[2];  // colour gradient: r1.z, r1.w, r2.x
+    constexpr int nc = (DEG + 1) * (DEG + 1);
+    float s[48];
+    load_sh<nc, kSrc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s, st);
+    const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+    const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+    const float3 dir_orig = make_float3(m.x - cam.x, m.y - cam.y, m.z - cam.z);
+    const float len = sqrtf(dot3(dir_orig, dir_orig));
+    const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    const uint8_t cl = p.clamped[idx];
+    // backward.cu:31-34: no gradient through a clamped channel
+    const float3 dc = make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r2.x * ((cl & 4) ? 0 : 1));
+    float B[16];
+    sh_basis<DEG>(dir.x, dir.y, dir.z, B);
+    if (p.d_rgb) {  // this view's factor of the SH gradient; the sinks are filled by gsd_sh_grad_views
+        p.d_rgb[3 * idx] = dc.x;
+        p.d_rgb[3 * idx + 1] = dc.y;
+        p.d_rgb[3 * idx + 2] = dc.z;
+    } else if (kSrc == 0) {
+        float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
+        sink_basis<0, nc, false>(drow, B, dc, 1);
+        for (int k = 3 * nc; k < p.M * 3; ++k) drow[k] = 0.f;
+    } else {  // split sinks: dSH/d dc = dSH/d rest = dSH/d offset = identity
+        if (p.dsh_dc) sink_basis<0, 1, kAcc>(p.dsh_dc + idx * st.dc_sg, B, dc, st.dc_se);
+        if (p.dsh_rest) sink_basis<1, nc, kAcc>(p.dsh_rest + idx * st.rest_sg, B, dc, st.rest_se);
+        if (p.dsh_off) sink_basis<0, nc, kAcc>(p.dsh_off + (size_t)idx * p.M * 3, B, dc, 1);
+        if (p.M > nc && !kAcc) zero_sh_tail(p, idx, nc, st);
+    }
+    float w[48], unused[48];
+#pragma unroll
+    for (int k = 0; k < nc; ++k) w[3 * k] = s[3 * k] * dc.x + s[3 * k + 1] * dc.y + s[3 * k + 2] * dc.z;
+    const float3 ddir = sh_channel_bwd(DEG, w, 1.f, dir.x, dir.y, dir.z, unused);
+    const float3 dmn = dnormvdv(dir_orig, ddir);
+    rec[2] = make_float4(r2.x, dmn.x, dmn.y, dmn.z);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// The SH half with coalesced HBM access (contiguous rows, M = 16: every training configuration).  One wave
+// per 64 consecutive Gaussians: their SH rows are one contiguous region per operand (dc 64 x 3, rest
+// 64 x 45, or shs / offset 64 x 48 floats), read with lane-consecutive dword loads (256 B per
+// wave-instruction) into LDS rows of 48 coefficients; each lane then works on its own row (stride 49:
+// conflict-free) and leaves the gradient in the row, and the rows go back out the same way.  The per-lane
+// kernel above reads each Gaussian's 180-B rows with one lane, 64 rows per wave-instruction (3.2 TB/s).
+constexpr int kShWave = 64;
+constexpr int kShRowStride = 49;
+
+// region rows [0, rows) x R floats at src  <->  LDS rows, columns [c0, c0 + R).  A full wave (rows = 64, all
+// but the last) has no per-element guard, so all R loads are in flight before the first LDS store (with a
+// guard per element every load sat in its own branch and waited for the previous one: 2x slower).
+template <int R, int kMode>  // kMode 0: lds = src, 1: lds += src (the offset operand)
+__device__ __forceinline__ void sh_region_load(const float* __restrict__ src, int rows, float* __restrict__ lds,
+                                               int c0) {
+    const int lane = threadIdx.x, n = rows * R;
+    float v[R];
+    if (rows == kShWave) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[i] = src[i * kShWave + lane];
+    } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[i] = i * kShWave + lane < n ? src[i * kShWave + lane] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int e = i * kShWave + lane;
+        const int g = e / R, j = e - g * R;
+        float* d = lds + g * kShRowStride + c0 + j;  // rows >= `rows` are scratch: harmless
+        *d = kMode ? *d + v[i] : v[i];
+    }
+}
+template <int R, bool kAcc>
+__device__ __forceinline__ void sh_region_store(float* __restrict__ dst, int rows, const float* __restrict__ lds,
+                                                int c0) {
+    const int lane = threadIdx.x, n = rows * R;
+    float v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int e = i * kShWave + lane;
+        const int g = e / R, j = e - g * R;
+        v[i] = lds[g * kShRowStride + c0 + j];
+    }
+    if (rows == kShWave) {
+        float old[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) old[i] = kAcc ? dst[i * kShWave + lane] : 0.f;
+#pragma unroll
+        for (int i = 0; i < R; ++i) dst[i * kShWave + lane] = old[i] + v[i];
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int e = i * kShWave + lane;
+        if (e < n) dst[e] = (kAcc ? dst[e] : 0.f) + v[i];
+    }
+}
+
+template <int DEG, int kSrc, bool kAcc>
+__global__ __launch_bounds__(kShWave) __attribute__((amdgpu_waves_per_eu(4))) void k_preprocess_bwd_sh_rows(PreprocessBwdParams p) {
+    __shared__ float rows_lds[kShWave * kShRowStride];
+    constexpr int M = 16;
+    const int g0 = blockIdx.x * kShWave, lane = threadIdx.x, idx = g0 + lane;
+    const int rows = min(kShWave, p.P - g0);
+    if (kSrc == 0) {
+        sh_region_load<3 * M, 0>(p.shs + (size_t)g0 * 3 * M, rows, rows_lds, 0);
+    } else {
+        sh_region_load<3, 0>(p.sh_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+        sh_region_load<3 * (M - 1), 0>(p.sh_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    }
+    __syncthreads();
+    if (kSrc == 2) {  // the same float add as load_sh (gaussian_renderer/__init__.py:134)
+        sh_region_load<3 * M, 1>(p.sh_off + (size_t)g0 * 3 * M, rows, rows_lds, 0);
+        __syncthreads();
+    }
+    float* row = rows_lds + lane * kShRowStride;
+    constexpr int nc = (DEG + 1) * (DEG + 1);
+    if (idx < p.P) {
+        if (!(p.radii[idx] > 0)) {
+            if (p.d_rgb) {
+                p.d_rgb[3 * idx] = 0.f;
+                p.d_rgb[3 * idx + 1] = 0.f;
+                p.d_rgb[3 * idx + 2] = 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 3 * M; ++k) row[k] = 0.f;
+        } else {
+            float4* rec = reinterpret_cast<float4*>(p.grad_rec + (size_t)idx * kGradRec);
+            const float4 r1 = rec[1], r2 = rec[2];  // colour gradient: r1.z, r1.w, r2.x
+            const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+            const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+            const float3 dir_orig = make_float3(m.x - cam.x, m.y - cam.y, m.z - cam.z);
+            const float len = sqrtf(dot3(dir_orig, dir_orig));
+            const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+            const uint8_t cl = p.clamped[idx];
+            const float3 dc =
+                make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r2.x * ((cl & 4) ? 0 : 1));
+            float w[48], unused[48];
+#pragma unroll
+            for (int k = 0; k < nc; ++k) w[3 * k] = row[3 * k] * dc.x + row[3 * k + 1] * dc.y + row[3 * k + 2] * dc.z;
+            const float3 ddir = sh_channel_bwd(DEG, w, 1.f, dir.x, dir.y, dir.z, unused);
+            const float3 dmn = dnormvdv(dir_orig, ddir);
+            rec[2] = make_float4(r2.x, dmn.x, dmn.y, dmn.z);
+            if (p.d_rgb) {  // this view's factor of the SH gradient; the sinks are filled by gsd_sh_grad_views
+                p.d_rgb[3 * idx] = dc.x;
+                p.d_rgb[3 * idx + 1] = dc.y;
+                p.d_rgb[3 * idx + 2] = dc.z;
+            } else {
+                float B[16];
+                sh_basis<DEG>(dir.x, dir.y, dir.z, B);
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    row[3 * k] = k < nc ? B[k] * dc.x : 0.f;  // zero above the active degree
+                    row[3 * k + 1] = k < nc ? B[k] * dc.y : 0.f;
+                    row[3 * k + 2] = k < nc ? B[k] * dc.z : 0.f;
+                }
+            }
+        }
+    }
+    if (p.d_rgb) return;
+    __syncthreads();
+    if (kSrc == 0) {
+        sh_region_store<3 * M, false>(p.dL_dsh + (size_t)g0 * 3 * M, rows, rows_lds, 0);
+        return;
+    }
+    if (p.dsh_dc) sh_region_store<3, kAcc>(p.dsh_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    if (p.dsh_rest) sh_region_store<3 * (M - 1), kAcc>(p.dsh_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    if (p.dsh_off) sh_region_store<3 * M, kAcc>(p.dsh_off + (size_t)g0 * 3 * M, rows, rows_lds, 0);
+}
+
+// The geometry half of the per-Gaussian backward: computeCov2DCUDA + preprocessCUDA bwd without the SH
+// (backward.cu:144-396); the view-direction term of dL/dmean3D comes from the record (k_preprocess_bwd_sh,
+// launched first; zeros when there is no SH operand).
+__global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= p.P) return;
     if (!(p.radii[idx] > 0)) {  // backward.cu:359-360 skips it; its gradients are the zeros torch::zeros holds
-        zero_outputs(p, idx, st);
+        zero_outputs(p, idx);
         return;
     }
     const Mat4 Vm = load_mat4(p.view);
@@ -521,8 +749,10 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     // the rasterizer's per-Gaussian record: unpack the API outputs (rasterize_points.cu:180-188) and use it
     const float4* rec4 = reinterpret_cast<const float4*>(p.grad_rec + (size_t)idx * kGradRec);
     const float4 r0 = rec4[0], r1 = rec4[1];
-    const float r8 = p.grad_rec[(size_t)idx * kGradRec + 8];
-    // r0 = (mean2D x, mean2D y, conic a, conic b), r1 = (conic c, opacity, color r, color g), r8 = color b
+    const float4 r2 = rec4[2];
+    const float r8 = r2.x;
+    // r0 = (mean2D x, mean2D y, conic a, conic b), r1 = (conic c, opacity, color r, color g), r2.x = color b,
+    // r2.yzw = the SH half's dL/dmean3D term
     if (p.dL_dmean2D) {
         p.dL_dmean2D[3 * idx] = r0.x;
         p.dL_dmean2D[3 * idx + 1] = r0.y;
@@ -557,43 +787,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     dm2.z = (P[8] * mw - P[11] * mul1) * d2x + (P[9] * mw - P[11] * mul2) * d2y;
     dmean = make_float3(dmean.x + dm2.x, dmean.y + dm2.y, dmean.z + dm2.z);
 
-    if (p.shs || p.sh_dc) {
-        const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
-        const float3 dir_orig = make_float3(m.x - cam.x, m.y - cam.y, m.z - cam.z);
-        const float len = sqrtf(dot3(dir_orig, dir_orig));
-        const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-        const uint8_t cl = p.clamped[idx];
-        const float3 dc = make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r8 * ((cl & 4) ? 0 : 1));
-        constexpr int nc = (DEG + 1) * (DEG + 1);
-        float s[48];
-        load_sh<nc>(p.shs, p.sh_dc, p.sh_rest, p.sh_off, p.M, idx, s, st);
-        float ds[48];
-        const float3 gx = sh_channel_bwd(DEG, s + 0, dc.x, dir.x, dir.y, dir.z, ds + 0);
-        const float3 gy = sh_channel_bwd(DEG, s + 1, dc.y, dir.x, dir.y, dir.z, ds + 1);
-        const float3 gz = sh_channel_bwd(DEG, s + 2, dc.z, dir.x, dir.y, dir.z, ds + 2);
-        if (p.d_rgb) {  // this view's factor of the SH gradient; the sinks are filled by gsd_sh_grad_views
-            p.d_rgb[3 * idx] = dc.x;
-            p.d_rgb[3 * idx + 1] = dc.y;
-            p.d_rgb[3 * idx + 2] = dc.z;
-        } else if (p.dL_dsh) {
-            float* drow = p.dL_dsh + (size_t)idx * p.M * 3;
-#pragma unroll
-            for (int k = 0; k < nc * 3; ++k) drow[k] = ds[k];
-        } else {  // split sinks: dSH/d dc = dSH/d rest = dSH/d offset = identity
-            // accumulate: every old value is loaded before the first store, so the loads issue together
-            // instead of each waiting behind a store it might alias
-            const bool acc = p.sh_accumulate != 0;
-            if (p.dsh_dc) sink_sh<0, 3>(p.dsh_dc + idx * st.dc_sg, ds, acc, st.dc_se);
-            if (p.dsh_rest) sink_sh<3, nc * 3>(p.dsh_rest + idx * st.rest_sg, ds, acc, st.rest_se);
-            if (p.dsh_off) sink_sh<0, nc * 3>(p.dsh_off + (size_t)idx * p.M * 3, ds, acc);
-        }
-        if (p.M > nc && !p.d_rgb) zero_sh_tail(p, idx, nc, st);
-        // glm::dot(dRGBdx, dL_dRGB) etc: dRGBdx = (ch0.x, ch1.x, ch2.x)
-        const float3 ddir = make_float3(gx.x * dc.x + gy.x * dc.y + gz.x * dc.z, gx.y * dc.x + gy.y * dc.y + gz.y * dc.z,
-                                        gx.z * dc.x + gy.z * dc.y + gz.z * dc.z);
-        const float3 dmn = dnormvdv(dir_orig, ddir);
-        dmean = make_float3(dmean.x + dmn.x, dmean.y + dmn.y, dmean.z + dmn.z);
-    }
+    dmean = make_float3(dmean.x + r2.y, dmean.y + r2.z, dmean.z + r2.w);  // backward.cu:390-392 (SH half)
     float3 dscale = make_float3(0.f, 0.f, 0.f);
     float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
     if (p.scales) cov3d_bwd(scale, p.scale_modifier, q, dcov, dscale, drot);
@@ -726,15 +920,38 @@ void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
     if (strided_sh(p)) launch_fwd<true>(p, s);
     else launch_fwd<false>(p, s);
 }
+template <bool kStr, int kSrc, bool kAcc>
+static void launch_bwd_sh(const PreprocessBwdParams& p, dim3 g, dim3 b, hipStream_t s) {
+    if (!kStr && p.M == 16) {  // coalesced rows (every training configuration)
+        const dim3 gw((p.P + kShWave - 1) / kShWave), bw(kShWave);
+        switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+            case 0: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<0, kSrc, kAcc>), gw, bw, 0, s, p); break;
+            case 1: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<1, kSrc, kAcc>), gw, bw, 0, s, p); break;
+            case 2: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<2, kSrc, kAcc>), gw, bw, 0, s, p); break;
+            default: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<3, kSrc, kAcc>), gw, bw, 0, s, p); break;
+        }
+        return;
+    }
+    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+        case 0: hipLaunchKernelGGL((k_preprocess_bwd_sh<0, kStr, kSrc, kAcc>), g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((k_preprocess_bwd_sh<1, kStr, kSrc, kAcc>), g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_preprocess_bwd_sh<2, kStr, kSrc, kAcc>), g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL((k_preprocess_bwd_sh<3, kStr, kSrc, kAcc>), g, b, 0, s, p); break;
+    }
+}
+// With SH: the SH half (k_preprocess_bwd_sh<DEG>) then the geometry half (degree-independent); without
+// (colors_precomp): the geometry half alone.
 template <bool kStr>
 static void launch_bwd(const PreprocessBwdParams& p, hipStream_t s) {
     const dim3 g((p.P + 255) / 256), b(256);
-    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
-        case 0: hipLaunchKernelGGL((k_preprocess_bwd<0, kStr>), g, b, 0, s, p); break;
-        case 1: hipLaunchKernelGGL((k_preprocess_bwd<1, kStr>), g, b, 0, s, p); break;
-        case 2: hipLaunchKernelGGL((k_preprocess_bwd<2, kStr>), g, b, 0, s, p); break;
-        default: hipLaunchKernelGGL((k_preprocess_bwd<3, kStr>), g, b, 0, s, p); break;
+    if (p.shs || p.sh_dc) {
+        const int src = p.shs ? 0 : (p.sh_off ? 2 : 1);
+        const bool acc = p.sh_accumulate != 0 && !p.shs;
+        if (src == 0) launch_bwd_sh<kStr, 0, false>(p, g, b, s);
+        else if (src == 1) acc ? launch_bwd_sh<kStr, 1, true>(p, g, b, s) : launch_bwd_sh<kStr, 1, false>(p, g, b, s);
+        else acc ? launch_bwd_sh<kStr, 2, true>(p, g, b, s) : launch_bwd_sh<kStr, 2, false>(p, g, b, s);
     }
+    hipLaunchKernelGGL(k_preprocess_bwd, g, b, 0, s, p);
 }
 void launch_preprocess_bwd(const PreprocessBwdParams& p, hipStream_t s) {
     if (p.P <= 0) return;
