@@ -390,9 +390,12 @@ __device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int i
 // dL/d(raw parameters) of one Gaussian from the activated-space gradients (k_activate_bwd's formulas):
 // xyz: identity; scaling: * exp(scaling); rotation: (I - u u^T) / |q| (u = q / |q|); opacity: * s (1 - s).
 __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, float3 dmean, float3 dscale,
-                                          float3 scale, float4 drot, float dopac) {
+                                          float3 scale, float4 drot, float dopac, float4 q, float raw_opac, bool vis) {
     const bool acc = p.a_accumulate != 0;
-    auto put = [acc](float* d, float v) { *d = acc ? *d + v : v; };
+    auto put = [acc, vis](float* d, float v) {  // a skipped Gaussian's gradients are zeros (+0 when accumulating)
+        v = vis ? v : 0.f;
+        *d = acc ? *d + v : v;
+    };
     if (p.a_xyz) {
         put(p.a_xyz + 3 * i, dmean.x);
         put(p.a_xyz + 3 * i + 1, dmean.y);
@@ -404,7 +407,6 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
         put(p.a_scaling + 3 * i + 2, dscale.z * scale.z);
     }
     if (p.a_rotation) {
-        const float4 q = reinterpret_cast<const float4*>(p.rotations)[i];
         const float nraw = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
         float4 gq;
         if (nraw > 1e-12f) {
@@ -416,6 +418,7 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
         } else {
             gq = make_float4(drot.x * 1e12f, drot.y * 1e12f, drot.z * 1e12f, drot.w * 1e12f);
         }
+        if (!vis) gq = make_float4(0.f, 0.f, 0.f, 0.f);
         float4* d = reinterpret_cast<float4*>(p.a_rotation) + i;
         if (acc) {
             const float4 o = *d;
@@ -424,14 +427,15 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
         *d = gq;
     }
     if (p.a_opacity) {
-        const float sg = act_opac(p.raw_opacity[i]);
+        const float sg = act_opac(raw_opac);
         put(p.a_opacity + i, dopac * sg * (1.f - sg));
     }
 }
 
 // Gradients of a Gaussian the backward skips (radii == 0): every per-Gaussian output is written, so callers need
-// not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  The SH half
-// writes the d_rgb row or the SH gradient entries (accumulating SH sinks are left untouched) ...
+// not zero-fill them (only the rasterizer's atomic accumulation targets must start at zero).  This is the SH
+// part (the d_rgb row or the SH gradient entries; accumulating SH sinks are left untouched); the geometry half
+// selects zeros for the rest.
 __device__ __forceinline__ void zero_sh_outputs(const PreprocessBwdParams& p, int idx, const ShStrides& st) {
     if (p.d_rgb) {  // the SH gradient is assembled from the views' d_rgb rows (gsd_sh_grad_views)
         p.d_rgb[3 * idx] = 0.f;
@@ -442,42 +446,6 @@ __device__ __forceinline__ void zero_sh_outputs(const PreprocessBwdParams& p, in
     if (p.shs || p.sh_dc) zero_sh_tail(p, idx, 0, st);
 }
 
-// ... and the geometry half everything else.
-__device__ __forceinline__ void zero_outputs(const PreprocessBwdParams& p, int idx) {
-    if (p.dL_dmean2D) {
-        p.dL_dmean2D[3 * idx] = 0.f;
-        p.dL_dmean2D[3 * idx + 1] = 0.f;
-        p.dL_dmean2D[3 * idx + 2] = 0.f;
-    }
-    if (p.dL_dopacity) p.dL_dopacity[idx] = 0.f;
-    if (p.dL_dcolor) {
-        p.dL_dcolor[3 * idx] = 0.f;
-        p.dL_dcolor[3 * idx + 1] = 0.f;
-        p.dL_dcolor[3 * idx + 2] = 0.f;
-    }
-    if (p.raw_act) {
-        if (!p.a_accumulate) {  // stored: zeros (accumulating: + 0 changes nothing)
-            if (p.a_xyz) for (int k = 0; k < 3; ++k) p.a_xyz[3 * idx + k] = 0.f;
-            if (p.a_scaling) for (int k = 0; k < 3; ++k) p.a_scaling[3 * idx + k] = 0.f;
-            if (p.a_rotation) reinterpret_cast<float4*>(p.a_rotation)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (p.a_opacity) p.a_opacity[idx] = 0.f;
-        }
-    } else {
-        p.dL_dmeans3D[3 * idx] = 0.f;
-        p.dL_dmeans3D[3 * idx + 1] = 0.f;
-        p.dL_dmeans3D[3 * idx + 2] = 0.f;
-    }
-    if (p.dL_dcov3D) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = 0.f;
-    }
-    if (p.dL_dscales) {
-        p.dL_dscales[3 * idx] = 0.f;
-        p.dL_dscales[3 * idx + 1] = 0.f;
-        p.dL_dscales[3 * idx + 2] = 0.f;
-    }
-    if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
 
 // The SH basis B_k of forward.cu:20-71 (the factor backward.cu:20-139 multiplies dL/dRGB by), k < (DEG+1)^2;
 // the same expressions as sh_channel_bwd's, so dL/dsh_k,c = B_k dL/dRGB_c to the bit.
@@ -722,56 +690,54 @@ __global__ __launch_bounds__(kShWave) __attribute__((amdgpu_waves_per_eu(4))) vo
 __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= p.P) return;
-    if (!(p.radii[idx] > 0)) {  // backward.cu:359-360 skips it; its gradients are the zeros torch::zeros holds
-        zero_outputs(p, idx);
-        return;
-    }
-    const Mat4 Vm = load_mat4(p.view);
-    const Mat4 Pm = load_mat4(p.proj);
+    // Every per-Gaussian load is issued up front, before the visibility test: a Gaussian the backward skips
+    // (radii == 0, backward.cu:359-360) is computed like the others and its outputs are replaced by the zeros
+    // torch::zeros holds -- one latency instead of two, and no divergent branch.
+    const bool vis = p.radii[idx] > 0;
     const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
-
-    // the 3D covariance the forward used (recomputed: cheaper than storing 24 B/G)
+    const float4* rec4 = reinterpret_cast<const float4*>(p.grad_rec + (size_t)idx * kGradRec);
+    const float4 r0 = rec4[0], r1 = rec4[1], r2 = rec4[2];
+    // r0 = (mean2D x, mean2D y, conic a, conic b), r1 = (conic c, opacity, color r, color g), r2.x = color b,
+    // r2.yzw = the SH half's dL/dmean3D term
     Cov6 c3;
     float3 scale = make_float3(0, 0, 0);
-    float4 q = make_float4(0, 0, 0, 0);
+    float4 q_in = make_float4(0, 0, 0, 0), q = q_in;
+    const float raw_opac = p.raw_act && p.a_opacity ? p.raw_opacity[idx] : 0.f;
     if (p.cov3D_precomp) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3.v[k] = p.cov3D_precomp[6 * idx + k];
     } else {
         scale = make_float3(p.scales[3 * idx], p.scales[3 * idx + 1], p.scales[3 * idx + 2]);
-        q = reinterpret_cast<const float4*>(p.rotations)[idx];
+        q_in = reinterpret_cast<const float4*>(p.rotations)[idx];
+        q = q_in;
         if (p.raw_act) {
             scale = act_scale(p.scales, idx);
-            q = act_rot(q);
+            q = act_rot(q_in);
         }
+        // the 3D covariance the forward used (recomputed: cheaper than storing 24 B/G)
         c3 = cov3d_from_scale_rot(scale, p.scale_modifier, q);
     }
+    const Mat4 Vm = load_mat4(p.view);
+    const Mat4 Pm = load_mat4(p.proj);
+    auto z = [vis](float v) { return vis ? v : 0.f; };
     // the rasterizer's per-Gaussian record: unpack the API outputs (rasterize_points.cu:180-188) and use it
-    const float4* rec4 = reinterpret_cast<const float4*>(p.grad_rec + (size_t)idx * kGradRec);
-    const float4 r0 = rec4[0], r1 = rec4[1];
-    const float4 r2 = rec4[2];
-    const float r8 = r2.x;
-    // r0 = (mean2D x, mean2D y, conic a, conic b), r1 = (conic c, opacity, color r, color g), r2.x = color b,
-    // r2.yzw = the SH half's dL/dmean3D term
     if (p.dL_dmean2D) {
-        p.dL_dmean2D[3 * idx] = r0.x;
-        p.dL_dmean2D[3 * idx + 1] = r0.y;
+        p.dL_dmean2D[3 * idx] = z(r0.x);
+        p.dL_dmean2D[3 * idx + 1] = z(r0.y);
         p.dL_dmean2D[3 * idx + 2] = 0.f;
     }
-    if (p.dL_dopacity) p.dL_dopacity[idx] = r1.y;
+    if (p.dL_dopacity) p.dL_dopacity[idx] = z(r1.y);
     if (p.dL_dcolor) {
-        p.dL_dcolor[3 * idx] = r1.z;
-        p.dL_dcolor[3 * idx + 1] = r1.w;
-        p.dL_dcolor[3 * idx + 2] = r8;
+        p.dL_dcolor[3 * idx] = z(r1.z);
+        p.dL_dcolor[3 * idx + 1] = z(r1.w);
+        p.dL_dcolor[3 * idx + 2] = z(r2.x);
     }
-    const float4 dcon4 = make_float4(r0.z, r0.w, 0.f, r1.x);
     float3 dmean;
     Cov6 dcov;
-    cov2d_bwd(m, c3, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, Vm, make_float3(dcon4.x, dcon4.y, dcon4.w), dmean,
-              dcov);
+    cov2d_bwd(m, c3, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, Vm, make_float3(r0.z, r0.w, r1.x), dmean, dcov);
     if (p.dL_dcov3D) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = dcov.v[k];
+        for (int k = 0; k < 6; ++k) p.dL_dcov3D[6 * idx + k] = z(dcov.v[k]);
     }
 
     // backward.cu:373-387 projective term from dL/dmean2D
@@ -791,8 +757,11 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     float3 dscale = make_float3(0.f, 0.f, 0.f);
     float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
     if (p.scales) cov3d_bwd(scale, p.scale_modifier, q, dcov, dscale, drot);
+    dmean = make_float3(z(dmean.x), z(dmean.y), z(dmean.z));
+    dscale = make_float3(z(dscale.x), z(dscale.y), z(dscale.z));
+    drot = make_float4(z(drot.x), z(drot.y), z(drot.z), z(drot.w));
     if (p.raw_act) {  // through the activations into the raw parameters' sinks (k_activate_bwd's formulas)
-        raw_grads(p, idx, dmean, dscale, scale, drot, r1.y);
+        raw_grads(p, idx, dmean, dscale, scale, drot, r1.y, q_in, raw_opac, vis);
         return;
     }
     p.dL_dmeans3D[3 * idx] = dmean.x;
