@@ -16,34 +16,66 @@
 
 namespace gsd {
 
-// Exclusive scan of tile_count over T tiles (one 1024-lane workgroup; T <= a few 1e5).
+// Exclusive scan of tile_count over T tiles (one 1024-lane workgroup; T <= a few 1e5): each lane owns `per`
+// consecutive tiles (held in registers up to kScanKeep), wave-level shuffle scans of the lane sums, one LDS
+// exchange of the 16 wave totals -- two barriers (an LDS Hillis-Steele over 1024 partials took 20).
+constexpr int kScanKeep = 16;
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(v, off);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(int T, const uint32_t* __restrict__ tile_count,
                                                             uint2* __restrict__ ranges, uint32_t* __restrict__ cursor,
                                                             uint32_t* __restrict__ counters) {
-    __shared__ uint32_t s_sum[kScanThreads];
-    const int tid = threadIdx.x;
+    __shared__ uint32_t s_wave[kScanThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int per = (T + kScanThreads - 1) / kScanThreads;
     const int b0 = min(T, tid * per), b1 = min(T, b0 + per);
+    uint32_t keep[kScanKeep];
     uint32_t local = 0;
-    for (int i = b0; i < b1; ++i) local += tile_count[i];
-    s_sum[tid] = local;
+    if (per <= kScanKeep) {
+#pragma unroll
+        for (int i = 0; i < kScanKeep; ++i) {
+            keep[i] = b0 + i < b1 ? tile_count[b0 + i] : 0u;
+            local += keep[i];
+        }
+    } else {
+        for (int i = b0; i < b1; ++i) local += tile_count[i];
+    }
+    const uint32_t incl = wave_incl_scan(local, lane);
+    if (lane == 63) s_wave[wid] = incl;
     __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 partials
-    for (int off = 1; off < kScanThreads; off <<= 1) {
-        const uint32_t v = tid >= off ? s_sum[tid - off] : 0u;
-        __syncthreads();
-        s_sum[tid] += v;
-        __syncthreads();
+    if (wid == 0) {
+        uint32_t v = lane < kScanThreads / 64 ? s_wave[lane] : 0u;
+        v = wave_incl_scan(v, lane);
+        if (lane < kScanThreads / 64) s_wave[lane] = v;
     }
-    uint32_t run = s_sum[tid] - local;
-    for (int i = b0; i < b1; ++i) {
-        const uint32_t c = tile_count[i];
-        // empty tiles keep (0,0) as after the reference's memset (rasterizer_impl.cu:310)
-        ranges[i] = c ? make_uint2(run, run + c) : make_uint2(0u, 0u);
-        cursor[i] = run;
-        run += c;
+    __syncthreads();
+    uint32_t run = incl - local + (wid ? s_wave[wid - 1] : 0u);
+    // empty tiles keep (0,0) as after the reference's memset (rasterizer_impl.cu:310)
+    if (per <= kScanKeep) {
+#pragma unroll
+        for (int i = 0; i < kScanKeep; ++i) {
+            if (b0 + i < b1) {
+                const uint32_t c = keep[i];
+                ranges[b0 + i] = c ? make_uint2(run, run + c) : make_uint2(0u, 0u);
+                cursor[b0 + i] = run;
+                run += c;
+            }
+        }
+    } else {
+        for (int i = b0; i < b1; ++i) {
+            const uint32_t c = tile_count[i];
+            ranges[i] = c ? make_uint2(run, run + c) : make_uint2(0u, 0u);
+            cursor[i] = run;
+            run += c;
+        }
     }
-    if (tid == kScanThreads - 1) counters[0] = s_sum[tid];
+    if (tid == kScanThreads - 1) counters[0] = s_wave[kScanThreads / 64 - 1];
 }
 
 // duplicateWithKeys (rasterizer_impl.cu:70-111), scattered straight into tile buckets.
