@@ -72,7 +72,8 @@ def pmc_traffic(kernel):
         except (OSError, ValueError):
             continue
         if kernel in d:
-            return {"hbm_bytes": d[kernel]["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
+            return {"hbm_bytes": d[kernel]["hbm_bytes"], "valu": d[kernel].get("valu"),
+                    "source": os.path.relpath(f, ROOT)}
     return None
 
 
@@ -250,6 +251,8 @@ def main():
                 if tr is not None:
                     roof["traffic"] = tr["hbm_bytes"]
                     roof["traffic_source"] = tr["source"]
+                    if tr.get("valu"):   # the bound that applies to the render kernels: VALU issue
+                        roof["valu"] = tr["valu"]
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             cpu = cpu_baseline(cfg, args.config)

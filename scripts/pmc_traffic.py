@@ -27,10 +27,22 @@ def main(src, dst):
         if "FETCH_SIZE" not in cs and "WRITE_SIZE" not in cs:
             continue
         f, w = cs.get("FETCH_SIZE", 0.0), cs.get("WRITE_SIZE", 0.0)
-        out[short(k)] = {"kernel": k, "fetch_kb": round(f, 1), "write_kb": round(w, 1),
-                         "hbm_bytes": int(round((2.0 * f + w) * 1024.0))}
+        e = {"kernel": k, "fetch_kb": round(f, 1), "write_kb": round(w, 1),
+             "hbm_bytes": int(round((2.0 * f + w) * 1024.0))}
+        if "SQ_INSTS_VALU" in cs and cs.get("GRBM_GUI_ACTIVE"):
+            # VALU issue rate: wave64 VALU instructions per SIMD-cycle over the dispatch (GRBM_GUI_ACTIVE is
+            # summed over the 8 XCDs; 1024 SIMDs).  Peak 0.5: a wave64 v_fma_f32 every 2 cycles per SIMD with
+            # more than one wave resident (MI355X_MICROARCH.md, per-instruction cycle table).
+            cyc = cs["GRBM_GUI_ACTIVE"] / 8.0
+            rate = cs["SQ_INSTS_VALU"] / (1024.0 * cyc)
+            e["valu"] = {"instructions": int(cs["SQ_INSTS_VALU"]), "cycles": int(cyc),
+                         "issue_per_simd_cycle": round(rate, 4), "peak": 0.5, "frac": round(rate / 0.5, 4)}
+            if cs.get("SQ_WAVE_CYCLES"):
+                e["valu"]["lds_issue_wait_frac"] = round(cs.get("SQ_WAIT_INST_LDS", 0.0) / cs["SQ_WAVE_CYCLES"], 4)
+        out[short(k)] = e
     out["_note"] = ("per-launch means over the profiled launches (scripts/prof_render.py, cfg 4); FETCH_SIZE x2 "
-                    "per the gfx950 calibration, WRITE_SIZE as is; gathers and atomics are uncalibrated widths")
+                    "per the gfx950 calibration, WRITE_SIZE as is; gathers and atomics are uncalibrated widths; "
+                    "valu: SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) against 0.5 per SIMD-cycle")
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
