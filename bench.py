@@ -6,9 +6,11 @@ A step = on every rank (one process per GPU): render() of that rank's view
 (activation preamble + HIP rasterizer forward), the reference's training loss
 0.8 L1 + 0.2 (1 - SSIM) against a synthetic target (train.py:529, fused HIP
 kernel), backward (HIP rasterizer backward + the fused activation backward),
-ONE RCCL all-reduce of the flat per-Gaussian gradient slab, and the
-reference's Adam step (scene/gaussian_model.py:834-864 param groups, eps
-1e-15).  Inputs live in HBM before the timed region.  ``value`` = views
+the RCCL all-reduce of the flat per-Gaussian gradient slab (the SH gradient
+exchanged as per-view dL/dRGB rows inside the backward; the rest in 32-MB
+buckets) overlapped with the reference's Adam step (scene/gaussian_model.py:
+834-864 param groups, eps 1e-15), which updates each bucket as its sum
+arrives.  Inputs live in HBM before the timed region.  ``value`` = views
 processed by all ranks / max-over-ranks wall time of the K timed steps.
 
 Also reported (rank 0): fwd+bwd ms/view (hipEvents, median over >= 100 views,
@@ -161,8 +163,10 @@ def main():
         out = render(cam, pc, pipe, bg)
         loss = l1_ssim_loss(out["render"], target, 0.2)   # train.py:529, lambda_dssim = 0.2
         loss.backward()
-        flat.allreduce()
-        opt.step(zero_grad=True)   # the Adam pass also clears the gradient slab for the next step
+        # the gradient all-reduce (RCCL, bucketed, asynchronous) overlapped with the Adam pass, which runs
+        # over each bucket as its sum arrives; a no-op collective at N = 1.  The gradient slab is marked
+        # stale for the next step instead of cleared.
+        opt.allreduce_step(zero_grad=True)
         return out
 
     # Adam moves every parameter by ~lr per step whatever the gradient, so the scene drifts from the configured

@@ -65,6 +65,30 @@ class FusedAdam(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero()
 
+    def _adam(self, a: int, b: int):
+        """gsd_adam_step over slab elements [a, b) (whole groups or parts of them) at the current step count."""
+        if b <= a:
+            return
+        g0 = self.param_groups[0]
+        beta1, beta2 = g0["betas"]
+        begins, lrs = [], []
+        for gi, g in enumerate(self.param_groups):
+            gb = self._begin[gi]
+            ge = self._begin[gi + 1] if gi + 1 < len(self.param_groups) else self.param_slab.numel()
+            if ge > a and gb < b and ge > gb:
+                begins.append(max(gb, a) - a)
+                lrs.append(float(g["lr"]))
+        lib = _native.load()
+        dev = self.param_slab.device
+        f4 = 4  # bytes per float: the range's pointers
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_adam_step(
+                b - a, ctypes.c_void_p(self.param_slab.data_ptr() + f4 * a),
+                ctypes.c_void_p(self.flat.slab.data_ptr() + f4 * a), ctypes.c_void_p(self.exp_avg.data_ptr() + f4 * a),
+                ctypes.c_void_p(self.exp_avg_sq.data_ptr() + f4 * a), len(begins),
+                (ctypes.c_int64 * len(begins))(*begins), (ctypes.c_float * len(lrs))(*lrs), self.step_count, beta1,
+                beta2, float(g0["eps"]), 0, _stream(dev)))
+
     @torch.no_grad()
     def step(self, closure=None, zero_grad: bool = False):
         """One Adam step for every group.  ``zero_grad`` then marks the gradient slab stale instead of writing
@@ -87,6 +111,29 @@ class FusedAdam(torch.optim.Optimizer):
         if zero_grad:
             self.flat.invalidate()
         return loss
+
+    @torch.no_grad()
+    def allreduce_step(self, zero_grad: bool = False, bucket_floats: int | None = None):
+        """Data-parallel step: the gradient all-reduce (FlatGrads.allreduce) and this Adam step, overlapped.
+        The all-reduce goes out in buckets on RCCL's stream; Adam runs over every range that needs no
+        reduction (the SH gradient the ranks assembled from the exchanged views) at once, and over each bucket
+        as soon as that bucket's sum is in -- the device updates bucket k while the links carry bucket k + 1.
+        The same arithmetic per element as ``allreduce(); step()``; at world size 1 it is ``step()``."""
+        from .parallel import BUCKET_FLOATS
+        ranges = self.flat.allreduce_buckets(bucket_floats or BUCKET_FLOATS)
+        self.step_count += 1
+        if len(ranges) == 1 and ranges[0][2] is None:
+            self._adam(*ranges[0][:2])
+        else:
+            for a, b, w in ranges:        # ranges with nothing to wait for first
+                if w is None:
+                    self._adam(a, b)
+            for a, b, w in ranges:
+                if w is not None:
+                    w.wait()
+                    self._adam(a, b)
+        if zero_grad:
+            self.flat.invalidate()
 
     def moments(self, p: torch.Tensor):
         """(exp_avg, exp_avg_sq) views of parameter ``p`` (shaped like ``p``)."""

@@ -60,6 +60,9 @@ def slab_view(slab, off, like=None, shape=None, coef_major=False):
 
 
 SH_VIEWS = os.environ.get("GSD_SH_VIEWS", "1") != "0"   # exchange per-view dL/dRGB instead of the SH gradient
+# all-reduce bucket (floats) of FusedAdam.allreduce_step: 8M floats = 32 MB, a few per step at 1M Gaussians, each
+# large enough for the ring to run at link rate on xGMI (GSD_BUCKET_MB overrides)
+BUCKET_FLOATS = int(float(os.environ.get("GSD_BUCKET_MB", "32")) * (1 << 20) / 4)
 
 
 def data_parallel_world() -> int:
@@ -165,14 +168,8 @@ class FlatGrads:
                 p.grad = v
                 self.stale.discard(id(p))
 
-    def allreduce(self, op=None, async_op=False):
-        """Sum the slab across ranks (no-op for world size 1): one all-reduce per contiguous run of views not
-        already summed (mark_reduced -- e.g. the SH gradient the rasterizer assembled from every view)."""
-        self.collect()
-        self.settle()
-        reduced, self.reduced = self.reduced, set()
-        if data_parallel_world() == 1:
-            return None
+    def _runs(self, reduced):
+        """Contiguous slab ranges [a, b) of the views not in ``reduced``."""
         runs, off = [], 0
         for p, v in zip(self.params, self.views):
             n = v.numel()
@@ -182,6 +179,17 @@ class FlatGrads:
                 else:
                     runs.append([off, off + n])
             off += n
+        return runs
+
+    def allreduce(self, op=None, async_op=False):
+        """Sum the slab across ranks (no-op for world size 1): one all-reduce per contiguous run of views not
+        already summed (mark_reduced -- e.g. the SH gradient the rasterizer assembled from every view)."""
+        self.collect()
+        self.settle()
+        reduced, self.reduced = self.reduced, set()
+        if data_parallel_world() == 1:
+            return None
+        runs = self._runs(reduced)
         if dist.get_backend() != "nccl" and self.slab.is_cuda:   # gloo (tests): through host memory
             for a, b in runs:
                 h = self.slab[a:b].cpu()
@@ -190,6 +198,38 @@ class FlatGrads:
             return None
         works = [dist.all_reduce(self.slab[a:b], op=op or dist.ReduceOp.SUM, async_op=async_op) for a, b in runs]
         return works if async_op else None
+
+    def allreduce_buckets(self, bucket_floats: int = BUCKET_FLOATS):
+        """The all-reduce of ``allreduce`` issued asynchronously in buckets of at most ``bucket_floats``, for
+        a consumer that works through the slab while the later buckets are still on the links
+        (FusedAdam.allreduce_step).  Returns [(a, b, work)] covering the whole slab in order: work is None for
+        a range that needs no reduction (world size 1, or views already summed) or was reduced synchronously
+        (gloo); otherwise the caller waits on it (``work.wait()`` only orders the current stream behind the
+        collective, the host does not block)."""
+        self.collect()
+        self.settle()
+        reduced, self.reduced = self.reduced, set()
+        n = self.slab.numel()
+        if data_parallel_world() == 1:
+            return [(0, n, None)]
+        out, pos = [], 0
+        nccl = dist.get_backend() == "nccl" or not self.slab.is_cuda
+        for a, b in self._runs(reduced):
+            if a > pos:
+                out.append((pos, a, None))
+            for c in range(a, b, max(1, int(bucket_floats))):
+                d = min(b, c + int(bucket_floats))
+                if nccl:
+                    out.append((c, d, dist.all_reduce(self.slab[c:d], op=dist.ReduceOp.SUM, async_op=True)))
+                else:   # gloo on device tensors (tests): through host memory, synchronously
+                    h = self.slab[c:d].cpu()
+                    dist.all_reduce(h, op=dist.ReduceOp.SUM)
+                    self.slab[c:d].copy_(h)
+                    out.append((c, d, None))
+            pos = b
+        if pos < n:
+            out.append((pos, n, None))
+        return out
 
 
 def view_stats_allreduce(visible_count: torch.Tensor, grad2d_norm_sum: torch.Tensor, max_radii: torch.Tensor):

@@ -69,3 +69,68 @@ def test_two_ranks_match_one_process(tmp_path):
         assert torch.isfinite(got).all()
         rel = float((got - want).norm() / want.norm())
         assert rel <= 1e-5, (r, rel)
+
+
+WORKER_ADAM = r'''
+import os, sys
+sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting_deformable_amd"), ROOT]
+import torch, torch.distributed as dist
+from gsd_amd import DeformableGaussians, default_pipe, render
+from gsd_amd.camera import synthetic_camera
+from gsd_amd.optim import FusedAdam
+from gsd_amd.scene import make_gaussians
+
+def step(pc, yaw):
+    cam = synthetic_camera(320, 240, yaw_deg=yaw).to("cuda:0")
+    out = render(cam, pc, default_pipe(), torch.zeros(3, device="cuda:0"))
+    w = torch.linspace(0.5, 1.5, 320, device="cuda:0")
+    (out["render"] * w).sum().backward()
+
+rank, world, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+params = make_gaussians(20_000, 320, 240, seed=22, device="cuda:0")
+pc = DeformableGaussians(params, sh_degree=3)
+opt = FusedAdam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pc.parameters())])
+for it in range(2):
+    if rank >= 0:
+        if it == 0:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[4], RANK=str(rank), WORLD_SIZE=str(world))
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        step(pc, 4.0 * rank + it)
+        opt.allreduce_step(zero_grad=True, bucket_floats=50_000)   # several buckets, partial ones included
+    else:                      # the single-process reference: both views into one slab, then a plain step
+        for r in range(world):
+            step(pc, 4.0 * r + it)
+        opt.step(zero_grad=True)
+if rank >= 0:
+    dist.destroy_process_group()
+torch.save({"p": opt.param_slab.cpu(), "m": opt.exp_avg.cpu(), "v": opt.exp_avg_sq.cpu()}, out)
+'''
+
+
+def test_two_ranks_overlapped_allreduce_adam_matches_one_process(tmp_path):
+    """FusedAdam.allreduce_step (bucketed asynchronous all-reduce, Adam per bucket as it arrives, the exchanged
+    SH gradient first) over two gloo ranks == one process summing both views and taking a plain Adam step;
+    two steps, so the second runs on moments the first left."""
+    script = tmp_path / "worker_adam.py"
+    script.write_text("ROOT = %r\n" % ROOT + WORKER_ADAM)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    port = str(29800 + os.getpid() % 150)
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), "2", str(tmp_path / f"a{r}.pt"), port], env=env)
+             for r in range(2)]
+    rcs = [p.wait(timeout=300) for p in procs]
+    assert rcs == [0, 0]
+    ref = subprocess.run([sys.executable, str(script), "-1", "2", str(tmp_path / "aref.pt"), port], env=env,
+                         timeout=300)
+    assert ref.returncode == 0
+    want = torch.load(tmp_path / "aref.pt", weights_only=True)
+    for r in range(2):
+        got = torch.load(tmp_path / f"a{r}.pt", weights_only=True)
+        for k in ("m", "v"):   # the moments are (quadratic in) the summed gradients
+            assert torch.isfinite(got[k]).all()
+            rel = float((got[k] - want[k]).norm() / want[k].norm())
+            assert rel <= 1e-5, (r, k, rel)
+        # the parameters move by ~lr m / sqrt(v); only gradients within rounding of zero may flip a sign
+        d = (got["p"] - want["p"]).abs()
+        assert float(d.max()) <= 2 * 6e-3 + 1e-6
+        assert float((d > 1e-6).float().mean()) <= 1e-4
