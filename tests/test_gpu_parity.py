@@ -182,6 +182,23 @@ def test_binning_buffer_too_small_retries(oracle_mod):
     assert _C._K_GUESS[torch.device(DEV)] > 1000
 
 
+def test_binning_capacity_boundary():
+    """Phase 2 is queued before num_rendered reaches the host, guarded by the binning buffer's capacity: buffers
+    holding a little less than, exactly, and a little more than num_rendered all give the same image, radii
+    and final count (short ones through GSD_NEED_BINNING and a second phase-2 call)."""
+    from gsd_amd import _C
+    d = scene_inputs(6_000, 640, 360, 3, seed=6, device=DEV)
+    K, color, radii, *_ = gpu_forward(d)
+    assert K > 1000
+    for want in (K - 300, K - 1, K, K + 1):
+        guess = next(g for g in range(max(1, want * 4 // 5 - 8), want * 4 // 5 + 8) if g + g // 4 >= want)
+        _C._K_GUESS[torch.device(DEV)] = guess     # the buffer holds gsd_binning_buffer_bytes(guess + guess // 4)
+        K2, color2, radii2, *_ = gpu_forward(d)
+        assert K2 == K
+        assert torch.equal(radii2, radii)
+        assert torch.equal(color2, color), want
+
+
 def test_empty_and_culled():
     d = scene_inputs(100, 64, 64, 0, seed=1, device=DEV)
     d["means3D"] = d["means3D"] * torch.tensor([1.0, 1.0, -1.0], device=DEV)   # all behind the camera
