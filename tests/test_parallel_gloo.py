@@ -108,3 +108,48 @@ def test_two_rank_sh_views_protocol(tmp_path):
     for r in range(world):
         got = np.load(tmp_path / f"rank{r}.npy")
         np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-9)
+
+
+def _worker_buckets(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd.parallel import FlatGrads, init_from_env, mark_reduced
+    r, _, w = init_from_env(backend="gloo")
+    grads = view_grads(yaw=2.0 * r)
+    params = [torch.nn.Parameter(torch.zeros(g.shape)) for g in grads]
+    fg = FlatGrads(params, device="cpu")
+    for p, g in zip(params, grads):
+        p.grad.copy_(torch.from_numpy(g))
+    # the SH gradient (params[1]) stands for one the ranks already summed (the per-view exchange): every rank
+    # holds the sum, and the bucketed all-reduce must leave it alone
+    total_sh = torch.zeros_like(params[1].grad)
+    for k in range(w):
+        total_sh += torch.from_numpy(view_grads(yaw=2.0 * k)[1])
+    params[1].grad.copy_(total_sh)
+    mark_reduced([params[1]])
+    ranges = fg.allreduce_buckets(bucket_floats=1000)    # several buckets per run, a partial one at each end
+    covered = 0
+    for a, b, work in ranges:
+        assert a == covered and b > a
+        covered = b
+        if work is not None:
+            work.wait()
+    assert covered == fg.slab.numel()
+    np.save(os.path.join(out_dir, f"brank{r}.npy"), fg.slab.numpy())
+    dist.destroy_process_group()
+
+
+def test_four_rank_bucketed_allreduce_equals_sum_of_views(tmp_path):
+    """FlatGrads.allreduce_buckets (the asynchronous, bucketed all-reduce FusedAdam.allreduce_step overlaps with
+    Adam) over four gloo ranks: the slab ranges cover it in order, and every rank ends with the sum of the four
+    single-view oracle gradients -- including the range marked as already summed, which it must not re-add."""
+    world = 4
+    mp.spawn(_worker_buckets, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = sum(np.concatenate([g.reshape(-1) for g in view_grads(2.0 * r)]) for r in range(world))
+    for r in range(world):
+        got = np.load(os.path.join(str(tmp_path), f"brank{r}.npy"))
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
