@@ -31,11 +31,12 @@ namespace gsd {
 
 
 // forward: records whose alphas are evaluated together (ILP across the exps); measured 2/3/4/6/8/16 ->
-// 4 is fastest (0.33 ms vs 0.38 at 8: fewer alphas wasted past a pixel's termination)
-#ifndef GSD_FWD_BATCH
-#define GSD_FWD_BATCH 4
-#endif
-constexpr int kBatch = GSD_FWD_BATCH;
+// 4 is fastest (0.33 ms vs 0.38 at 8: fewer alphas wasted past a pixel's termination; re-measured with the
+// uniform-skip recurrence: 2 / 4 / 8 -> 0.305 / 0.289 / 0.328 ms)
+constexpr int kBatch = 4;
+// forward culling: the alpha box only (the exact ellipse test of the backward costs the forward more than it
+// saves: 0.306 vs 0.289 ms)
+constexpr bool kFwdExactCull = false;
 constexpr int kBwdBatch = 4;  // backward: records whose alphas are evaluated together
 constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
 
@@ -212,10 +213,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        #ifndef GSD_FWD_EXACT
-#define GSD_FWD_EXACT false
-#endif
-        const int m = wave_compact<GSD_FWD_EXACT>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, tg.lane);
+        const int m = wave_compact<kFwdExactCull>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, tg.lane);
         for (int j0 = 0; j0 < m; j0 += kBatch) {
             if (!__ballot(!done)) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
