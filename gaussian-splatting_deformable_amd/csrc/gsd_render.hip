@@ -36,7 +36,6 @@ namespace gsd {
 constexpr int kBatch = 4;
 // forward culling: the alpha box only (the exact ellipse test of the backward costs the forward more than it
 // saves: 0.306 vs 0.289 ms)
-constexpr bool kFwdExactCull = false;
 constexpr int kBwdBatch = 4;  // backward: records whose alphas are evaluated together
 constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
 
@@ -112,6 +111,74 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
     return m;
 }
 
+// Forward lane groups: the wave's 8x8 quadrant as kFwdGroups rectangles of 64 / kFwdGroups pixels (2: the 8x4
+// halves, lanes 0-31 / 32-63; 4: 4x4 blocks, lanes 16 g .. 16 g + 15), each walking its own compacted record
+// list side by side with the others -- a record whose alpha box misses a group no longer occupies its lanes.
+// Measured (render_fwd, bench workload): 1 group (the whole quadrant) 0.291 ms, 2 (8x4 halves) 0.288,
+// 4 (4x4 blocks) 0.261, 8 (4x2 blocks) 0.268 -- finer groups waste fewer lanes on records that miss them, at
+// the price of distinct LDS addresses per record read and more compaction.
+constexpr int kFwdGroups = 4;
+// pixel offset of `lane` inside the quadrant, and its group's rectangle [gx0, gx0 + gw) x [gy0, gy0 + gh)
+__device__ __forceinline__ void fwd_lane_pixel(int lane, int& dx, int& dy) {
+    if (kFwdGroups == 8) {  // 4x2 blocks
+        const int g = lane >> 3;
+        dx = (g & 1) * 4 + (lane & 3);
+        dy = (g >> 1) * 2 + ((lane >> 2) & 1);
+    } else if (kFwdGroups == 4) {
+        const int g = lane >> 4;
+        dx = (g & 1) * 4 + (lane & 3);
+        dy = (g >> 1) * 4 + ((lane >> 2) & 3);
+    } else {
+        dx = lane & 7;
+        dy = lane >> 3;
+    }
+}
+__device__ __forceinline__ float4 fwd_group_rect(int g, float qx0, float qy0) {  // (x0, x1, y0, y1), inclusive
+    if (kFwdGroups == 8) {
+        const float x0 = qx0 + (float)((g & 1) * 4), y0 = qy0 + (float)((g >> 1) * 2);
+        return make_float4(x0, x0 + 3.f, y0, y0 + 1.f);
+    }
+    if (kFwdGroups == 4) {
+        const float x0 = qx0 + (float)((g & 1) * 4), y0 = qy0 + (float)((g >> 1) * 4);
+        return make_float4(x0, x0 + 3.f, y0, y0 + 3.f);
+    }
+    if (kFwdGroups == 2) return make_float4(qx0, qx0 + 7.f, qy0 + (float)(4 * g), qy0 + (float)(4 * g) + 3.f);
+    return make_float4(qx0, qx0 + 7.f, qy0, qy0 + 7.f);
+}
+
+// Compaction into one list per lane group: lists[g] receives, in increasing slot order, the slots whose alpha
+// box meets group g's rectangle.  Returns the count of `mine` (the calling lane's group) and the maximum.
+__device__ __forceinline__ int2 wave_compact_groups(const float4* __restrict__ s_box, uint8_t (*lists)[kTilePix],
+                                                    int n, float qx0, float qy0, int lane) {
+    int cnt[kFwdGroups];
+#pragma unroll
+    for (int g = 0; g < kFwdGroups; ++g) cnt[g] = 0;
+#pragma unroll
+    for (int k = 0; k < kTilePix / 64; ++k) {
+        const int t = k * 64 + lane;
+        const float4 bx = t < n ? s_box[t] : make_float4(1e30f, -1e30f, 1e30f, -1e30f);
+#pragma unroll
+        for (int g = 0; g < kFwdGroups; ++g) {
+            const float4 r = fwd_group_rect(g, qx0, qy0);
+            const bool hit = t < n && bx.y >= r.x && bx.x <= r.y && bx.w >= r.z && bx.z <= r.w;
+            const unsigned long long b = __ballot(hit);
+            if (hit)
+                lists[g][cnt[g] + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))] = (uint8_t)t;
+            cnt[g] += __popcll(b);
+        }
+    }
+    wave_lds_handoff();
+    const int me = lane / (64 / kFwdGroups);
+    int mine = cnt[0], mx = cnt[0];
+#pragma unroll
+    for (int g = 1; g < kFwdGroups; ++g) {
+        mine = me == g ? cnt[g] : mine;
+        mx = max(mx, cnt[g]);
+    }
+    return make_int2(mine, mx);
+}
+
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
 // Shared by both passes so their skip decisions are identical.  power is evaluated exactly as the
 // reference writes it (no contraction), so alpha differs from the reference only through exp:
@@ -164,15 +231,18 @@ struct TileGeom {
     float qx0, qy0;
     bool inside;
 };
-__device__ __forceinline__ TileGeom tile_geom(int num_tiles, int grid_x, int W, int H) {
+// fwd_map: the forward's lane -> pixel map (fwd_lane_pixel); else row-major 8x8 (the backward)
+__device__ __forceinline__ TileGeom tile_geom(int num_tiles, int grid_x, int W, int H, bool fwd_map = false) {
     TileGeom g;
     g.tile = xcd_swizzle(blockIdx.x, num_tiles);
     g.wave = threadIdx.x >> 6;
     g.lane = threadIdx.x & 63;
     const int x0 = (g.tile % grid_x) * kTileX + (g.wave & 1) * 8;
     const int y0 = (g.tile / grid_x) * kTileY + (g.wave >> 1) * 8;
-    g.px = x0 + (g.lane & 7);
-    g.py = y0 + (g.lane >> 3);
+    int dx = g.lane & 7, dy = g.lane >> 3;
+    if (fwd_map) fwd_lane_pixel(g.lane, dx, dy);
+    g.px = x0 + dx;
+    g.py = y0 + dy;
     g.qx0 = (float)x0;
     g.qy0 = (float)y0;
     g.inside = g.px < W && g.py < H;
@@ -184,9 +254,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float4 s_box[kTilePix];
-    __shared__ uint8_t s_list[4][kTilePix];
+    __shared__ uint8_t s_list[4][kFwdGroups][kTilePix];
     if (over_capacity(p.k_guard, p.k_cap)) return;
-    const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
+    const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);
     const int tid = threadIdx.x;
     bool done = !tg.inside;
     const uint2 rg = p.ranges[tg.tile];
@@ -196,7 +266,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     float T = 1.0f;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last_contributor = 0;
-    uint8_t* list = s_list[tg.wave];
+    uint8_t* list = s_list[tg.wave][tg.lane / (64 / kFwdGroups)];
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         // forward.cu:309-311: stop once every pixel of the tile is saturated
@@ -213,7 +283,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        const int m = wave_compact<kFwdExactCull>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, tg.lane);
+        const int2 mm = wave_compact_groups(s_box, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane);
+        const int mine = mm.x, m = mm.y;  // this lane's group's list length, the longest
         for (int j0 = 0; j0 < m; j0 += kBatch) {
             if (!__ballot(!done)) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
@@ -221,7 +292,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
             int slot[kBatch];
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
-                slot[u] = list[min(j0 + u, m - 1)];
+                slot[u] = mine > 0 ? list[min(j0 + u, mine - 1)] : 0;
                 float G, dx, dy;
                 a[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, G, dx, dy);
             }
@@ -232,7 +303,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 if (j0 + u >= m) break;
-                bool take = !done & (a[u] >= 1.0f / 255.0f);
+                bool take = !done & (j0 + u < mine) & (a[u] >= 1.0f / 255.0f);
                 if (!__ballot(take)) continue;
                 const float alpha = a[u];
                 const float test_T = T * (1 - alpha);
