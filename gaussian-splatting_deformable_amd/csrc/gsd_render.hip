@@ -13,7 +13,8 @@
 // batch, the list of records whose box meets its 8x8 quadrant and iterates
 // only those.  Records outside the list would have been skipped by every
 // lane (alpha < 1/255), so results are unchanged -- ~57% of (wave, record)
-// pairs never reach the ALUs on the bench scene.
+// pairs never reach the ALUs on the bench scene.  The forward culls per 4x4
+// pixel block (16 lanes), each block walking its own list.
 //
 // Backward: the reference issues 9 float atomicAdds per (pixel, Gaussian) pair
 // (backward.cu:523,545-554), all 256 lanes on the same address.  Here the work
@@ -34,8 +35,8 @@ namespace gsd {
 // 4 is fastest (0.33 ms vs 0.38 at 8: fewer alphas wasted past a pixel's termination; re-measured with the
 // uniform-skip recurrence: 2 / 4 / 8 -> 0.305 / 0.289 / 0.328 ms)
 constexpr int kBatch = 4;
-// forward culling: the alpha box only (the exact ellipse test of the backward costs the forward more than it
-// saves: 0.306 vs 0.289 ms)
+// (forward culling is by the alpha box only: the backward's exact ellipse test costs the forward more than it
+// saves -- 0.306 vs 0.289 ms per 8x8 quadrant, 0.366 vs 0.261 per 4x4 lane group)
 constexpr int kBwdBatch = 4;  // backward: records whose alphas are evaluated together
 constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
 
