@@ -252,9 +252,35 @@ __device__ __forceinline__ int merge_split(const unsigned long long* A, int la, 
 // keys t E .. t E + E - 1.  Of the log2(N)(log2(N)+1)/2 compare-exchange passes, those with partner distance
 // j < E stay inside a thread, E <= j < 64 E cross lanes of one wave (shuffles, no barrier), and only the
 // j >= 64 E ones (3 of 45 at N = 512) go through LDS with barriers -- instead of every pass.
+// v of lane ^ d.  For the distances of the unrolled passes (constants) as VALU cross-lane ops instead of
+// ds_bpermute (an LDS-pipe instruction plus an address, 412 of them in the 512-key network): DPP quad_perm for
+// 1 and 2, two row rotations and a select for 4 (rotating a 16-lane row by 8 is xor 8), v_permlane16/32_swap
+// and a select for 16 and 32.
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int d, int lane) {
+    switch (d) {
+        case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+        case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+        case 4: {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+            const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12c, 0xf, 0xf, false);  // row_ror:12
+            return (lane & 4) ? a : b;
+        }
+        case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+        case 16: {
+            const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            return (lane & 16) ? r[0] : r[1];
+        }
+        case 32: {
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return (lane & 32) ? r[0] : r[1];
+        }
+        default: return (uint32_t)__shfl_xor((int)v, d);
+    }
+}
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int d) {
-    const int lo = __shfl_xor((int)(uint32_t)v, d), hi = __shfl_xor((int)(uint32_t)(v >> 32), d);
-    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+    const int lane = threadIdx.x & 63;
+    const uint32_t lo = xor_lane((uint32_t)v, d, lane), hi = xor_lane((uint32_t)(v >> 32), d, lane);
+    return ((unsigned long long)hi << 32) | lo;
 }
 template <int E>
 __device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n, unsigned long long* s,
