@@ -180,6 +180,12 @@ __device__ __forceinline__ int2 wave_compact_groups(const float4* __restrict__ s
     return make_int2(mine, mx);
 }
 
+// List entries j0 .. j0 + 3 (j0 a multiple of 4) as one LDS word instead of four byte reads; entries at or past
+// `valid` are replaced by slot 0 (always staged in the current batch, so every value read through it is finite)
+__device__ __forceinline__ int list_slot(uint32_t w4, int u, int j0, int valid) {
+    return j0 + u < valid ? (int)((w4 >> (8 * u)) & 0xffu) : 0;
+}
+
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
 // Shared by both passes so their skip decisions are identical.  power is evaluated exactly as the
 // reference writes it (no contraction), so alpha differs from the reference only through exp:
@@ -255,7 +261,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float4 s_box[kTilePix];
-    __shared__ uint8_t s_list[4][kFwdGroups][kTilePix];
+    __shared__ __attribute__((aligned(4))) uint8_t s_list[4][kFwdGroups][kTilePix];
     if (over_capacity(p.k_guard, p.k_cap)) return;
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);
     const int tid = threadIdx.x;
@@ -291,9 +297,11 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
             float a[kBatch];
             int slot[kBatch];
+            static_assert(kBatch == 4, "one LDS word of list entries per batch");
+            const uint32_t w4 = *reinterpret_cast<const uint32_t*>(list + j0);
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
-                slot[u] = mine > 0 ? list[min(j0 + u, mine - 1)] : 0;
+                slot[u] = list_slot(w4, u, j0, mine);
                 float G, dx, dy;
                 a[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, G, dx, dy);
             }
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ float4 s_co[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float s_acc[9][kTilePix + 1];  // +1: a record's nine sums sit in nine different banks
-    __shared__ uint8_t s_list[4][kTilePix];
+    __shared__ __attribute__((aligned(4))) uint8_t s_list[4][kTilePix];
     // the alpha boxes are read only by the compaction, the (G dL/dalpha, alpha T) hand-off only after it (a
     // barrier apart): one region, 30 KB of LDS per workgroup in all -> 5 workgroups per CU
     __shared__ union {
@@ -419,6 +427,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
             // needed from the lane.
             bool any = false;
+            uint32_t w4 = 0;  // the group's four list entries (kBwdGroup == kBwdBatch: one sub-batch)
 #pragma unroll
             for (int sb = 0; sb < kBwdGroup / kBwdBatch; ++sb) {
                 const int jb = j0 + sb * kBwdBatch;
@@ -429,9 +438,11 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 }
                 float Gs[kBwdBatch], As[kBwdBatch];
                 int slot[kBwdBatch];
+                static_assert(kBwdBatch == 4, "one LDS word of list entries per batch");
+                w4 = *reinterpret_cast<const uint32_t*>(list + jb);
 #pragma unroll
                 for (int u = 0; u < kBwdBatch; ++u) {
-                    slot[u] = list[min(jb + u, m - 1)];
+                    slot[u] = list_slot(w4, u, jb, m);
                     float dx, dy;
                     As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u], dx, dy);
                 }
@@ -461,7 +472,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             // constant.  Sums: S0 = sum v, S1 = sum v dx, S3 = sum v dx^2, C = sum w dL/dpixel; the dy
             // moments follow as dy S0, dy S1, dy^2 S0 (backward.cu:545-554 expanded over pixels).
             const int r = lane & 3, grp = lane >> 2;
-            const int rs = list[min(j0 + r, m - 1)];
+            static_assert(kBwdGroup == kBwdBatch, "phase 2 reads the group's slots from phase 1's list word");
+            const int rs = list_slot(w4, r, j0, m);
             const float2 mxy = s_xy[rs];
             const float px0 = tg.qx0 + (float)(4 * (grp & 1));
             float dxi[4];
