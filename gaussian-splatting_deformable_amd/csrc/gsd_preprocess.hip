@@ -780,14 +780,11 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
 namespace gsd {
 
 // dL/dsh_k = sum_v B_k(dir_v) dL/dRGB_v (the per-view SH backward of backward.cu:20-139, summed over the views
-// whose masked dL/dRGB rows were exchanged).  One lane per Gaussian; the 3 (D+1)^2 sums stay in registers.
+// whose masked dL/dRGB rows were exchanged) for Gaussian idx: the 3 (D+1)^2 sums in acc.
 template <int DEG>
-__global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= p.P) return;
+__device__ __forceinline__ void sh_views_sum(const ShViewsParams& p, int idx, float (&acc)[48]) {
     constexpr int nc = (DEG + 1) * (DEG + 1);
     const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
-    float acc[48];
 #pragma unroll
     for (int k = 0; k < 48; ++k) acc[k] = 0.f;
     for (int v = 0; v < p.n_views; ++v) {
@@ -828,6 +825,16 @@ __global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
             acc[3 * k + 2] += b[k] * g.z;
         }
     }
+}
+
+// One lane per Gaussian, writing its own rows (any sink layout).
+template <int DEG>
+__global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= p.P) return;
+    constexpr int nc = (DEG + 1) * (DEG + 1);
+    float acc[48];
+    sh_views_sum<DEG>(p, idx, acc);
     const bool add = p.accumulate != 0;
     if (p.d_dc) {
         float* d = p.d_dc + idx * p.dc_sg;
@@ -856,8 +863,48 @@ __global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
     }
 }
 
+// The same with coalesced sinks (contiguous rows, M = 16): one wave per 64 Gaussians, the sums through LDS rows
+// and out as lane-consecutive region stores (the SH half of the backward's scheme).
+template <int DEG, bool kAcc>
+__global__ __launch_bounds__(kShWave) void k_sh_grad_views_rows(ShViewsParams p) {
+    __shared__ float rows_lds[kShWave * kShRowStride];
+    constexpr int M = 16, nc = (DEG + 1) * (DEG + 1);
+    const int g0 = blockIdx.x * kShWave, lane = threadIdx.x, idx = g0 + lane;
+    const int rows = min(kShWave, p.P - g0);
+    if (idx < p.P) {
+        float acc[48];
+        sh_views_sum<DEG>(p, idx, acc);
+        float* row = rows_lds + lane * kShRowStride;
+#pragma unroll
+        for (int k = 0; k < 3 * M; ++k) row[k] = k < 3 * nc ? acc[k] : 0.f;  // zero above the active degree
+    }
+    __syncthreads();
+    if (p.d_dc) sh_region_store<3, kAcc>(p.d_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    if (p.d_rest) sh_region_store<3 * (M - 1), kAcc>(p.d_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    if (p.d_off) sh_region_store<3 * M, kAcc>(p.d_off + (size_t)g0 * 3 * M, rows, rows_lds, 0);
+}
+
+template <bool kAcc>
+static void launch_sh_views_rows(const ShViewsParams& p, hipStream_t s) {
+    const dim3 g((p.P + kShWave - 1) / kShWave), b(kShWave);
+    switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+        case 0: hipLaunchKernelGGL((k_sh_grad_views_rows<0, kAcc>), g, b, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((k_sh_grad_views_rows<1, kAcc>), g, b, 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_sh_grad_views_rows<2, kAcc>), g, b, 0, s, p); break;
+        default: hipLaunchKernelGGL((k_sh_grad_views_rows<3, kAcc>), g, b, 0, s, p); break;
+    }
+}
 void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s) {
     if (p.P <= 0) return;
+#ifndef GSD_SH_VIEWS_LANE
+    const bool rows = p.M == 16 && (!p.d_dc || (p.dc_sg == 3 && p.dc_se == 1)) &&
+                      (!p.d_rest || (p.rest_sg == 3LL * (p.M - 1) && p.rest_se == 1));
+    if (rows) {
+        if (p.accumulate) launch_sh_views_rows<true>(p, s);
+        else launch_sh_views_rows<false>(p, s);
+        return;
+    }
+#endif
     const dim3 g((p.P + 255) / 256), b(256);
     switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
         case 0: hipLaunchKernelGGL(k_sh_grad_views<0>, g, b, 0, s, p); break;
