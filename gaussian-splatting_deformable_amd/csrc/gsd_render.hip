@@ -33,7 +33,7 @@ namespace gsd {
 
 // forward: records whose alphas are evaluated together (ILP across the exps); measured 2/3/4/6/8/16 ->
 // 4 is fastest (0.33 ms vs 0.38 at 8: fewer alphas wasted past a pixel's termination; re-measured with the
-// uniform-skip recurrence: 2 / 4 / 8 -> 0.305 / 0.289 / 0.328 ms)
+// uniform-skip recurrence: 2 / 4 / 8 -> 0.305 / 0.289 / 0.328 ms; with the 4x4 lane groups: 4 / 8 -> 0.252 / 0.280)
 constexpr int kBatch = 4;
 // (forward culling is by the alpha box only: the backward's exact ellipse test costs the forward more than it
 // saves -- 0.306 vs 0.289 ms per 8x8 quadrant, 0.366 vs 0.261 per 4x4 lane group)
