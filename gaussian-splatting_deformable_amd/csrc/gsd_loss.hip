@@ -74,10 +74,38 @@ __device__ __forceinline__ void stage(const float* __restrict__ a, float (*sa)[k
         }
 }
 
+// stage() for the image and the ground truth at once, interleaved as (x, y) pairs
+__device__ __forceinline__ void stage_pair(const float* __restrict__ a, const float* __restrict__ b,
+                                           f2 (*sab)[kSsimIn], int H, int W, int ox, int oy) {
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    constexpr int kRowIt = (kSsimIn + 7) / 8, kColIt = 2;
+    f2 v[kRowIt][kColIt];
+#pragma unroll
+    for (int i = 0; i < kRowIt; ++i) {
+        const int r = ty + 8 * i, gy = oy - kSsimHalo + r;
+#pragma unroll
+        for (int j = 0; j < kColIt; ++j) {
+            const int c = tx + 32 * j, gx = ox - kSsimHalo + c;
+            const bool ok = r < kSsimIn && c < kSsimIn && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const size_t o = ok ? (size_t)gy * W + gx : 0;
+            v[i][j] = ok ? f2{a[o], b[o]} : f2{0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kRowIt; ++i)
+#pragma unroll
+        for (int j = 0; j < kColIt; ++j) {
+            const int r = ty + 8 * i, c = tx + 32 * j;
+            if (r < kSsimIn && c < kSsimIn) sab[r][c] = v[i][j];
+        }
+}
+
 // Vertical 11-tap pass over the horizontal sums: output rows 2 jp and 2 jp + 1 of the thread's four take one
 // packed FMA (v_pk_fma_f32) per staged row, weights (w[m], w[m-1]) with m = t - 2 jp.  With the packed
-// horizontal pass below: k_ssim_fwd 0.0756 -> 0.0705 ms at 1080p.  The same packing in k_ssim_bwd (three
-// quantities, so one of them stays scalar) measured 0.0592 -> 0.0599 ms and is not used there.
+// horizontal pass below: k_ssim_fwd 0.0756 -> 0.0705 ms at 1080p; with x and y interleaved in LDS (one 8-B
+// read per tap, stage_pair) 0.0623 ms.  In k_ssim_bwd (three quantities, so one stays scalar) neither helps:
+// packed arithmetic 0.0592 -> 0.0599 ms; (g0, g1) interleaved in LDS 0.0595 -> 0.0600, with the packed vertical
+// pass 0.0606 -- not used there.
 template <int NQ>
 __device__ __forceinline__ void vertical_pass(const SsimArgs& p, const float (*sh)[kSsimIn][kSsimTile], int r0,
                                               int c, float (&acc)[NQ][kSsimRows]) {
@@ -111,14 +139,13 @@ __device__ __forceinline__ void vertical_pass(const SsimArgs& p, const float (*s
 __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const float* __restrict__ img,
                                                              const float* __restrict__ gt, float* __restrict__ gmaps,
                                                              float* __restrict__ partial) {
-    __shared__ float sx[kSsimIn][kSsimIn], sy[kSsimIn][kSsimIn];
+    __shared__ f2 sxy[kSsimIn][kSsimIn];  // (x, y) interleaved: one 8-B LDS read per window tap
     __shared__ float sh[5][kSsimIn][kSsimTile];  // horizontal sums of x, y, x^2, y^2, xy
     __shared__ float red[2][kSsimThreads / 64];
     const int ch = blockIdx.z;
     const int ox = blockIdx.x * kSsimTile, oy = blockIdx.y * kSsimTile;
     const size_t plane = (size_t)p.H * p.W;
-    stage(img + ch * plane, sx, p.H, p.W, ox, oy);
-    stage(gt + ch * plane, sy, p.H, p.W, ox, oy);
+    stage_pair(img + ch * plane, gt + ch * plane, sxy, p.H, p.W, ox, oy);
     __syncthreads();
     // horizontal pass: thread = (column c, row group); no integer division.  (x, y) as one packed pair: w x and
     // w y in one multiply, their sums and the squares' sums in two packed FMAs, xy scalar
@@ -128,7 +155,7 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
         float e = 0.f;
 #pragma unroll
         for (int k = 0; k < 11; ++k) {
-            const f2 v = {sx[r][c + k], sy[r][c + k]};
+            const f2 v = sxy[r][c + k];
             const f2 wv = p.w[k] * v;
             ab += wv;
             cd = __builtin_elementwise_fma(wv, v, cd);
@@ -163,7 +190,8 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
         gmaps[map + o] = p.coef_ssim * (-f * fast_rcp(d2));
         gmaps[2 * map + o] = p.coef_ssim * (2.f * n1 * inv);
         fsum += f;
-        l1sum += fabsf(sx[r + kSsimHalo][c + kSsimHalo] - sy[r + kSsimHalo][c + kSsimHalo]);
+        const f2 v = sxy[r + kSsimHalo][c + kSsimHalo];
+        l1sum += fabsf(v.x - v.y);
     }
     fsum = wave_sum(fsum);
     l1sum = wave_sum(l1sum);
