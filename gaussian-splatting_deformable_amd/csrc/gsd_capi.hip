@@ -703,30 +703,33 @@ int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, cons
 }
 
 int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
-                  const int64_t* group_begin, const float* group_lr, int64_t step, float beta1, float beta2, float eps,
-                  int32_t zero_grad, void* stream) {
-    if (n < 0 || n_groups < 1 || n_groups > gsd::kAdamMaxGroups || step < 1)
-        return fail(GSD_ERR_ARG, "adam: need n >= 0, 1 <= n_groups <= 16 and step >= 1");
+                  const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
+                  double beta2, double eps, int32_t zero_grad, void* stream) {
+    if (n < 0 || n_groups < 1 || n_groups > gsd::kAdamMaxGroups)
+        return fail(GSD_ERR_ARG, "adam: need n >= 0 and 1 <= n_groups <= 16");
     if (n == 0) return GSD_OK;
-    if (!param || !grad || !exp_avg || !exp_avg_sq || !group_begin || !group_lr)
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !group_begin || !group_lr || !group_step)
         return fail(GSD_ERR_ARG, "null pointer argument");
     gsd::AdamArgs a{};
     a.n = n;
     a.n_groups = n_groups;
     a.zero_grad = zero_grad != 0;
-    // torch/optim/adam.py: bias corrections and step size in double on the host, applied as float scalars
-    const double bc1 = 1.0 - std::pow((double)beta1, (double)step), bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    // torch/optim/adam.py _multi_tensor_adam: bias_correction1 = 1 - beta1 ** step, step_size = -(lr / bc1),
+    // bias_correction2_sqrt = bc2 ** 0.5, all Python doubles; the foreach kernels take them as float scalars
     for (int g = 0; g < n_groups; ++g) {
         if (group_begin[g] < (g ? group_begin[g - 1] : 0) || group_begin[g] > n || (g == 0 && group_begin[0] != 0))
             return fail(GSD_ERR_ARG, "adam: group_begin must start at 0 and be non-decreasing");
+        if (group_step[g] < 1) return fail(GSD_ERR_ARG, "adam: every step count must be >= 1");
+        const double bc1 = 1.0 - std::pow(beta1, (double)group_step[g]);
+        const double bc2 = 1.0 - std::pow(beta2, (double)group_step[g]);
         a.begin[g] = group_begin[g];
-        a.step_size[g] = (float)(-(double)group_lr[g] / bc1);
-        a.bc2_sqrt[g] = (float)std::sqrt(bc2);
+        a.step_size[g] = (float)(((double)group_lr[g] / bc1) * -1.0);
+        a.bc2_sqrt[g] = (float)std::pow(bc2, 0.5);  // bc2 ** 0.5
     }
-    a.w1 = 1.f - beta1;
-    a.beta2 = beta2;
-    a.omb2 = 1.f - beta2;
-    a.eps = eps;
+    a.w1 = (float)(1.0 - beta1);     // _foreach_lerp_(exp_avgs, grads, 1 - beta1)
+    a.beta2 = (float)beta2;          // _foreach_mul_(exp_avg_sqs, beta2)
+    a.omb2 = (float)(1.0 - beta2);   // _foreach_addcmul_(exp_avg_sqs, grads, grads, 1 - beta2)
+    a.eps = (float)eps;
     hipStream_t s = as_stream(stream);
     timed(kAdam, s, [&] { gsd::launch_adam(a, param, grad, exp_avg, exp_avg_sq, s); });
     GSD_CHECK(false, s);

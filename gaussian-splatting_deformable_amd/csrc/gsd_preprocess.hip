@@ -793,6 +793,9 @@ __device__ __forceinline__ void sh_views_sum(const ShViewsParams& p, int idx, fl
         const float3 g = make_float3(row[3 * idx], row[3 * idx + 1], row[3 * idx + 2]);
         const float3 d0 = make_float3(m.x - cam[0], m.y - cam[1], m.z - cam[2]);
         const float len = sqrtf(dot3(d0, d0));
+        // a view that culled this Gaussian handed over a zero row: its term is exactly zero, and is skipped
+        // rather than evaluated (a mean at that camera's centre would give a NaN basis, and NaN * 0 = NaN)
+        if ((g.x == 0.f && g.y == 0.f && g.z == 0.f) || !(len > 0.f)) continue;
         const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
         float b[16];
         b[0] = kSH0;

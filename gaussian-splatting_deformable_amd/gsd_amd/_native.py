@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -71,8 +71,8 @@ SIGNATURES = {
     "gsd_l1_ssim_workspace_bytes": (_sz, [_i32, _i32, _i32]),
     "gsd_l1_ssim": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
     "gsd_l1_ssim_backward": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _f32, _vp, _vp, _vp]),
-    "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32), _i64, _f32,
-                             _f32, _f32, _i32, _vp]),
+    "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32),
+                             ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32, _vp]),
     "gsd_densify_stats": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_knn_workspace_bytes": (_sz, [_i32]),
     "gsd_knn_mean_dist2": (_i32, [_i32, _vp, _vp, _vp, _vp]),

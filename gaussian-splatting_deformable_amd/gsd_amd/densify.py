@@ -11,6 +11,11 @@ trained by ``gsd_amd.optim.FusedAdam``:
   semantics: new points get zero moments, pruned points drop theirs, a replaced tensor gets zero moments.
   They run every ``densification_interval`` (100) views, so they stay torch ops on the GPU; the flat
   parameter / moment / gradient slabs are rebuilt once per call (``FusedAdam.rebuild``).
+- Data parallel (one view per rank, replicated Gaussians): every rank accumulates the statistics of its own
+  views; ``densify_and_prune`` first combines them across ranks (``sync_stats``: sums of the counts and
+  gradient norms, max of the radii -- what one process accumulating every view holds), and the split's normal
+  samples are drawn on rank 0 and broadcast, so every rank selects, samples and prunes identically and the
+  replicated parameters (and P) stay the same on every rank.
 """
 from __future__ import annotations
 
@@ -18,6 +23,7 @@ import torch
 
 from . import _native
 from ._C import _ptr, _stream
+from .parallel import broadcast_, data_parallel_world, view_stats_allreduce
 from .renderer import build_rotation, inverse_sigmoid
 
 _NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
@@ -52,6 +58,13 @@ class GaussianDensifier:
             _native.check(lib.gsd_densify_stats(P, _ptr(g), _ptr(r), _ptr(self.xyz_gradient_accum),
                                                 _ptr(self.xyz_gradient_accum_3vec), _ptr(self.denom),
                                                 _ptr(self.max_radii2D), _stream(g.device)))
+
+    def sync_stats(self):
+        """Combine the per-rank statistics (no-op on one rank): afterwards every rank holds the statistics of
+        all ranks' views."""
+        if data_parallel_world() > 1:
+            view_stats_allreduce(self.denom, self.xyz_gradient_accum, self.max_radii2D,
+                                 self.xyz_gradient_accum_3vec)
 
     # ---- optimizer-state surgery ----
     def _params(self):
@@ -109,7 +122,7 @@ class GaussianDensifier:
         with torch.no_grad():
             stds = pc.get_scaling[sel].repeat(N, 1)
             means = torch.zeros((stds.size(0), 3), device=pc._xyz.device)
-            samples = torch.normal(mean=means, std=stds)
+            samples = broadcast_(torch.normal(mean=means, std=stds))   # rank 0's draw on every rank
             rots = build_rotation(pc._rotation[sel]).repeat(N, 1, 1)
             new = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + pc._xyz[sel].repeat(N, 1),
                    "scaling": torch.log(pc.get_scaling[sel].repeat(N, 1) / (0.8 * N)),
@@ -120,7 +133,8 @@ class GaussianDensifier:
         self.prune_points(prune)
 
     def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size):
-        """:1219-1233."""
+        """:1219-1233 (after combining the ranks' statistics)."""
+        self.sync_stats()
         grads = self.xyz_gradient_accum / self.denom
         grads[grads.isnan()] = 0.0
         self.densify_and_clone(grads, max_grad, extent)

@@ -128,15 +128,18 @@ def load_ply(path: str, max_sh_degree: int = 3) -> GaussianParams:
 _ORDER = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
 
 
-def _adam_state_dict(optimizer, step: int):
-    """torch.optim.Adam.state_dict() layout for a FusedAdam (one entry per parameter, global indices)."""
+def _adam_state_dict(optimizer):
+    """torch.optim.Adam.state_dict() layout for a FusedAdam (global indices in group order; a parameter that
+    never got a gradient has no state entry, as in torch, and every entry carries its own step)."""
     state, groups, idx = {}, [], 0
+    steps = dict(zip((id(p) for p in optimizer._params), optimizer.steps))
     for g in optimizer.param_groups:
         ids = []
         for p in g["params"]:
-            m, v = optimizer.moments(p)
-            state[idx] = {"step": torch.tensor(float(step)), "exp_avg": m.detach().clone(),
-                          "exp_avg_sq": v.detach().clone()}
+            if steps[id(p)] > 0:
+                m, v = optimizer.moments(p)
+                state[idx] = {"step": torch.tensor(float(steps[id(p)])), "exp_avg": m.detach().clone(),
+                              "exp_avg_sq": v.detach().clone()}
             ids.append(idx)
             idx += 1
         groups.append({k: val for k, val in g.items() if k != "params"} | {"params": ids})
@@ -151,7 +154,7 @@ def capture(pc, optimizer, densifier=None, spatial_lr_scale: float = 1.0):
     denom = densifier.denom if densifier is not None else torch.zeros(P, 1, device=dev)
     return (pc.active_sh_degree, pc._xyz.detach(), pc._features_dc.detach(), pc._features_rest.detach(),
             pc._scaling.detach(), pc._rotation.detach(), pc._opacity.detach(), max_r, accum, denom,
-            _adam_state_dict(optimizer, optimizer.step_count), spatial_lr_scale)
+            _adam_state_dict(optimizer), spatial_lr_scale)
 
 
 def restore(model_args, pc, optimizer, densifier=None):
@@ -161,28 +164,31 @@ def restore(model_args, pc, optimizer, densifier=None):
     pc.active_sh_degree = int(active)
     data = {"xyz": xyz, "f_dc": f_dc, "f_rest": f_rest, "opacity": opacity, "scaling": scaling,
             "rotation": rotation}
-    named = {}
-    for g in opt_dict["param_groups"]:
-        if "name" in g and len(g["params"]) == 1:
-            named[g["name"]] = opt_dict["state"].get(g["params"][0])
-    news, ms, vs, step = [], [], [], 0
+    # the checkpoint's state per (group name, position in group) -- a multi-parameter group such as the
+    # reference's offset network keeps every entry -- with groups lacking a name matched by their index
+    saved = {}
+    for gi, g in enumerate(opt_dict["param_groups"]):
+        for pos, idx in enumerate(g["params"]):
+            saved[(g.get("name", gi), pos)] = opt_dict["state"].get(idx)
+    news, ms, vs, steps = [], [], [], []
     gauss = {id(p): n for p, n in zip([pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling,
                                        pc._rotation], _ORDER)}
-    for g in optimizer.param_groups:
-        for p in g["params"]:
+    for gi, g in enumerate(optimizer.param_groups):
+        for pos, p in enumerate(g["params"]):
             n = gauss.get(id(p))
             d = data[n].to(p.device) if n is not None else p.detach()
-            st = named.get(n) if n is not None else named.get(g.get("name"))
+            st = saved.get((n, 0)) if n is not None else saved.get((g.get("name", gi), pos))
             if st is not None and st.get("exp_avg") is not None and st["exp_avg"].shape == d.shape:
                 ms.append(st["exp_avg"].to(p.device))
                 vs.append(st["exp_avg_sq"].to(p.device))
-                step = max(step, int(float(st.get("step", 0))))
+                steps.append(int(float(st.get("step", 0))))
             else:
                 ms.append(torch.zeros_like(d))
                 vs.append(torch.zeros_like(d))
+                steps.append(0)
             news.append(d)
     optimizer.rebuild(news, ms, vs)
-    optimizer.step_count = step
+    optimizer.steps = steps
     if densifier is not None:
         densifier.max_radii2D = max_r.to(pc._xyz.device)
         densifier.xyz_gradient_accum = accum.to(pc._xyz.device)

@@ -55,59 +55,87 @@ class FusedAdam(torch.optim.Optimizer):
         self.flat = FlatGrads(ps, device=dev)
         self.exp_avg = torch.zeros_like(self.param_slab)
         self.exp_avg_sq = torch.zeros_like(self.param_slab)
-        begins, off = [], 0
-        for g in self.param_groups:
-            begins.append(off)
-            off += sum(p.numel() for p in g["params"])
-        self._begin = (ctypes.c_int64 * len(begins))(*begins)
-        self.step_count = 0
+        self._layout()
+        self.steps = [0] * len(ps)   # torch's state['step'] per parameter (0: no state yet)
+
+    def _layout(self):
+        """Slab span, group index and identity of every parameter, in slab order."""
+        self._params, self._span, self._gidx = [], [], []
+        off = 0
+        for gi, g in enumerate(self.param_groups):
+            for p in g["params"]:
+                self._params.append(p)
+                self._span.append((off, off + p.numel()))
+                self._gidx.append(gi)
+                off += p.numel()
+
+    @property
+    def step_count(self) -> int:
+        """The largest per-parameter step count (every parameter's, when all of them get gradients)."""
+        return max(self.steps, default=0)
+
+    @step_count.setter
+    def step_count(self, n: int):
+        self.steps = [int(n)] * len(self.steps)
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero()
 
-    def _adam(self, a: int, b: int):
-        """gsd_adam_step over slab elements [a, b) (whole groups or parts of them) at the current step count."""
-        if b <= a:
-            return
+    def _advance(self, missing):
+        """torch.optim.Adam skips a parameter whose grad is None and keeps state['step'] per parameter: count
+        this step for every parameter that got a gradient.  Returns their indices."""
+        active = [i for i, p in enumerate(self._params) if id(p) not in missing]
+        for i in active:
+            self.steps[i] += 1
+        return set(active)
+
+    def _adam(self, a: int, b: int, active):
+        """gsd_adam_step over slab elements [a, b) of the parameters in ``active``: one launch per contiguous
+        run of them (parameters without a gradient are left out, untouched), each run cut into segments of equal
+        (learning rate, step count), at most 16 per launch."""
+        segs = []   # [begin, end, lr, step]
+        for i, (pb, pe) in enumerate(self._span):
+            lo, hi = max(pb, a), min(pe, b)
+            if hi <= lo or i not in active:
+                continue
+            lr, st = float(self.param_groups[self._gidx[i]]["lr"]), self.steps[i]
+            if segs and segs[-1][1] == lo and segs[-1][2] == lr and segs[-1][3] == st:
+                segs[-1][1] = hi
+            else:
+                segs.append([lo, hi, lr, st])
+        runs = []
+        for sg in segs:
+            if runs and runs[-1][-1][1] == sg[0] and len(runs[-1]) < 16:
+                runs[-1].append(sg)
+            else:
+                runs.append([sg])
         g0 = self.param_groups[0]
         beta1, beta2 = g0["betas"]
-        begins, lrs = [], []
-        for gi, g in enumerate(self.param_groups):
-            gb = self._begin[gi]
-            ge = self._begin[gi + 1] if gi + 1 < len(self.param_groups) else self.param_slab.numel()
-            if ge > a and gb < b and ge > gb:
-                begins.append(max(gb, a) - a)
-                lrs.append(float(g["lr"]))
         lib = _native.load()
         dev = self.param_slab.device
-        f4 = 4  # bytes per float: the range's pointers
+        f4 = 4  # bytes per float: the run's pointers
         with torch.cuda.device(dev):
-            _native.check(lib.gsd_adam_step(
-                b - a, ctypes.c_void_p(self.param_slab.data_ptr() + f4 * a),
-                ctypes.c_void_p(self.flat.slab.data_ptr() + f4 * a), ctypes.c_void_p(self.exp_avg.data_ptr() + f4 * a),
-                ctypes.c_void_p(self.exp_avg_sq.data_ptr() + f4 * a), len(begins),
-                (ctypes.c_int64 * len(begins))(*begins), (ctypes.c_float * len(lrs))(*lrs), self.step_count, beta1,
-                beta2, float(g0["eps"]), 0, _stream(dev)))
+            for run in runs:
+                r0, r1 = run[0][0], run[-1][1]
+                k = len(run)
+                _native.check(lib.gsd_adam_step(
+                    r1 - r0, ctypes.c_void_p(self.param_slab.data_ptr() + f4 * r0),
+                    ctypes.c_void_p(self.flat.slab.data_ptr() + f4 * r0),
+                    ctypes.c_void_p(self.exp_avg.data_ptr() + f4 * r0),
+                    ctypes.c_void_p(self.exp_avg_sq.data_ptr() + f4 * r0), k,
+                    (ctypes.c_int64 * k)(*[sg[0] - r0 for sg in run]), (ctypes.c_float * k)(*[sg[2] for sg in run]),
+                    (ctypes.c_int64 * k)(*[sg[3] for sg in run]), float(beta1), float(beta2), float(g0["eps"]), 0,
+                    _stream(dev)))
 
     @torch.no_grad()
     def step(self, closure=None, zero_grad: bool = False):
-        """One Adam step for every group.  ``zero_grad`` then marks the gradient slab stale instead of writing
-        zeros (FlatGrads.invalidate): the next backward stores into it, as after torch's
-        zero_grad(set_to_none=True)."""
+        """One Adam step for every parameter that got a gradient.  ``zero_grad`` then marks the gradient slab
+        stale instead of writing zeros (FlatGrads.invalidate): the next backward stores into it, as after
+        torch's zero_grad(set_to_none=True)."""
         loss = closure() if closure is not None else None
         self.flat.collect()
-        self.flat.settle()
-        self.step_count += 1
-        g0 = self.param_groups[0]
-        beta1, beta2 = g0["betas"]
-        lrs = (ctypes.c_float * len(self.param_groups))(*[float(g["lr"]) for g in self.param_groups])
-        lib = _native.load()
-        dev = self.param_slab.device
-        with torch.cuda.device(dev):
-            _native.check(lib.gsd_adam_step(self.param_slab.numel(), _ptr(self.param_slab), _ptr(self.flat.slab),
-                                            _ptr(self.exp_avg), _ptr(self.exp_avg_sq), len(self.param_groups),
-                                            self._begin, lrs, self.step_count, beta1, beta2, float(g0["eps"]),
-                                            0, _stream(dev)))
+        active = self._advance(self.flat.settle())
+        self._adam(0, self.param_slab.numel(), active)
         if zero_grad:
             self.flat.invalidate()
         return loss
@@ -118,20 +146,19 @@ class FusedAdam(torch.optim.Optimizer):
         The all-reduce goes out in buckets on RCCL's stream; Adam runs over every range that needs no
         reduction (the SH gradient the ranks assembled from the exchanged views) at once, and over each bucket
         as soon as that bucket's sum is in -- the device updates bucket k while the links carry bucket k + 1.
-        The same arithmetic per element as ``allreduce(); step()``; at world size 1 it is ``step()``."""
+        The same arithmetic per element as ``allreduce(); step()``; at world size 1 it is ``step()``.
+        Which parameters got a gradient is decided per rank: every rank must produce gradients for the same
+        parameters (as DistributedDataParallel requires), or their step counts diverge."""
         from .parallel import BUCKET_FLOATS
         ranges = self.flat.allreduce_buckets(bucket_floats or BUCKET_FLOATS)
-        self.step_count += 1
-        if len(ranges) == 1 and ranges[0][2] is None:
-            self._adam(*ranges[0][:2])
-        else:
-            for a, b, w in ranges:        # ranges with nothing to wait for first
-                if w is None:
-                    self._adam(a, b)
-            for a, b, w in ranges:
-                if w is not None:
-                    w.wait()
-                    self._adam(a, b)
+        active = self._advance(self.flat.missing)
+        for a, b, w in ranges:        # ranges with nothing to wait for first
+            if w is None:
+                self._adam(a, b, active)
+        for a, b, w in ranges:
+            if w is not None:
+                w.wait()
+                self._adam(a, b, active)
         if zero_grad:
             self.flat.invalidate()
 
@@ -174,14 +201,10 @@ class FusedAdam(torch.optim.Optimizer):
         self.param_slab, self.exp_avg, self.exp_avg_sq = param_slab, exp_avg, exp_avg_sq
         self.flat.remove_hooks()
         self.flat = FlatGrads(ps, device=dev)
-        begins, off = [], 0
-        for g in self.param_groups:
-            begins.append(off)
-            off += sum(p.numel() for p in g["params"])
-        self._begin = (ctypes.c_int64 * len(begins))(*begins)
+        self._layout()   # per-parameter step counts carry over (the reference keeps stored_state['step'])
 
     def reset_state(self):
-        """Zero the moments and the step count (as a freshly constructed torch Adam)."""
+        """Zero the moments and the step counts (as a freshly constructed torch Adam)."""
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
-        self.step_count = 0
+        self.steps = [0] * len(self.steps)

@@ -100,6 +100,7 @@ class FlatGrads:
             self.views.append(v)
             off += p.numel()
         self.stale = set()
+        self.missing = set()   # what the last settle() found without a gradient
         self.reduced = set()   # views already summed over the ranks this step (mark_reduced)
         self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
         self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
@@ -152,13 +153,18 @@ class FlatGrads:
     def settle(self):
         """Before the gradients are consumed: views nothing wrote since ``invalidate`` hold zero gradient --
         unless no backward ran at all and the slab was written in place (gradients set by hand, e.g.
-        ``p.grad.copy_(g)``), which then stand as written."""
+        ``p.grad.copy_(g)``), which then stand as written.  Returns the ids of the parameters that got no
+        gradient (torch's ``p.grad is None`` after ``zero_grad(set_to_none=True)``): their views are zeroed (so a
+        collective sums zeros for them) but stay stale -- still "no gradient" until a producer writes them."""
         if len(self.stale) == len(self.params) and self.slab._version != getattr(self, "_version", None):
             self.stale.clear()
-            return
-        for i in list(self.stale):
+            self.missing = set()
+            return self.missing
+        for i in self.stale:
             self._view_of[i].zero_()
-        self.stale.clear()
+        self._version = self.slab._version   # the zeroing above is not a hand-written gradient
+        self.missing = set(self.stale)
+        return self.missing
 
     def collect(self):
         """Copy any .grad autograd replaced (instead of accumulating in place) back into the slab."""
@@ -232,12 +238,43 @@ class FlatGrads:
         return out
 
 
-def view_stats_allreduce(visible_count: torch.Tensor, grad2d_norm_sum: torch.Tensor, max_radii: torch.Tensor):
+def allreduce_(t: torch.Tensor, op=None) -> torch.Tensor:
+    """In-place all-reduce of ``t`` over the default group (no-op at world size 1); gloo with a device tensor
+    (the tests) goes through host memory."""
+    if data_parallel_world() == 1:
+        return t
+    op = op or dist.ReduceOp.SUM
+    if dist.get_backend() != "nccl" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    """In-place broadcast of ``t`` from rank ``src`` (no-op at world size 1)."""
+    if data_parallel_world() == 1:
+        return t
+    if dist.get_backend() != "nccl" and t.is_cuda:
+        h = t.cpu()
+        dist.broadcast(h, src)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, src)
+    return t
+
+
+def view_stats_allreduce(visible_count: torch.Tensor, grad2d_norm_sum: torch.Tensor, max_radii: torch.Tensor,
+                         grad_3vec_sum: torch.Tensor | None = None):
     """Per-view densification statistics (gaussian_model.py:1252-1257, train.py:613),
-    combined across ranks after each rank has accumulated its own view: sums for
+    combined across ranks after each rank has accumulated its own views: sums for
     the counts / norm sums, max for the radii."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(visible_count, op=dist.ReduceOp.SUM)
-        dist.all_reduce(grad2d_norm_sum, op=dist.ReduceOp.SUM)
-        dist.all_reduce(max_radii, op=dist.ReduceOp.MAX)
+    if data_parallel_world() > 1:
+        allreduce_(visible_count)
+        allreduce_(grad2d_norm_sum)
+        if grad_3vec_sum is not None:
+            allreduce_(grad_3vec_sum)
+        allreduce_(max_radii, dist.ReduceOp.MAX)
     return visible_count, grad2d_norm_sum, max_radii

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 6
+#define GSD_ABI_VERSION 7
 
 enum {
     GSD_OK = 0,
@@ -255,12 +255,16 @@ int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, cons
 
 /* One Adam step (torch.optim.Adam semantics as configured in scene/gaussian_model.py:839-856: per-group
  * learning rate, betas, eps 1e-15, no weight decay / amsgrad) over flat slabs of n floats: param, grad,
- * exp_avg, exp_avg_sq.  Group g covers elements [group_begin[g], group_begin[g+1]) (group_begin[0] = 0;
- * host arrays, n_groups <= 16) with learning rate group_lr[g]; `step` is the 1-based step count after
- * this update (bias corrections 1 - beta^step).  zero_grad != 0 also clears the gradient slab. */
+ * exp_avg, exp_avg_sq.  Segment g covers elements [group_begin[g], group_begin[g+1]) (group_begin[0] = 0;
+ * host arrays, n_groups <= 16) with learning rate group_lr[g] and its own 1-based step count group_step[g]
+ * after this update (torch keeps state['step'] per parameter: bias corrections 1 - beta^step).  The betas
+ * and eps are the Python doubles: 1 - beta1, 1 - beta2 and the bias corrections are formed in double, as
+ * torch forms them, and rounded to float once.  Elements whose parameter had no gradient this step (torch
+ * skips grad-None parameters) must be left out of [0, n) by the caller.  zero_grad != 0 also clears the
+ * gradient slab.  (ABI 7: per-segment steps, double betas.) */
 int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
-                  const int64_t* group_begin, const float* group_lr, int64_t step, float beta1, float beta2,
-                  float eps, int32_t zero_grad, void* stream);
+                  const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
+                  double beta2, double eps, int32_t zero_grad, void* stream);
 
 /* Per-view densification statistics (train.py:613-616, scene/gaussian_model.py:1252-1257): for every
  * Gaussian with radii > 0, max_radii2D = max(max_radii2D, radii); grad_accum_3vec += viewspace_grad;

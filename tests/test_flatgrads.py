@@ -57,3 +57,22 @@ def test_hand_written_gradients_stand():
     ps[1].grad.copy_(torch.ones(5, 1))
     f.settle()
     assert float(f.slab.sum()) == 20.0
+
+
+def test_settle_reports_parameters_without_gradient():
+    """settle() returns the parameters nothing wrote (torch's grad None: FusedAdam skips them and does not
+    advance their step); they stay "no gradient" until a producer writes them, also across a second settle()
+    in the same step and across steps without invalidate()."""
+    from gsd_amd.parallel import FlatGrads
+    ps = _params()
+    f = FlatGrads(ps)
+    f.slab.fill_(4.0)
+    f.invalidate()
+    (ps[0] * 3.0).sum().backward()
+    assert f.settle() == {id(ps[1])}
+    assert torch.equal(ps[1].grad, torch.zeros(5, 1))
+    assert f.settle() == {id(ps[1])}      # idempotent: its zeroing is not a hand-written gradient
+    (ps[0] * 1.0).sum().backward()        # no invalidate: ps[0] accumulates, ps[1] still has none
+    assert f.settle() == {id(ps[1])} and float(ps[0].grad.sum()) == 4.0 * 15
+    (ps[1] * 2.0).sum().backward()
+    assert f.settle() == set() and torch.equal(ps[1].grad, torch.full((5, 1), 2.0))

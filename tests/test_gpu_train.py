@@ -106,6 +106,128 @@ def test_fused_adam_matches_torch_adam():
         assert float((pa - pb).abs().max()) <= 1e-6
 
 
+def _adam_pair(seed=11):
+    """Gaussian-like groups (one parameter each) plus an offset-network group holding several parameters
+    (scene/gaussian_model.py:839-856 adds offset_model.parameters() as one group), as FusedAdam and as
+    torch.optim.Adam (foreach)."""
+    from gsd_amd.optim import FusedAdam
+    gen = torch.Generator().manual_seed(seed)
+    g_shapes = [(701, 3), (701, 15, 3), (701, 1)]
+    n_shapes = [(32, 16), (32,), (3, 32)]
+    lrs = [0.00016, 0.0025 / 20.0, 0.05]
+    init = [torch.randn(*s, generator=gen) for s in g_shapes + n_shapes]
+    a = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    b = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+
+    def groups(ps):
+        return ([{"params": [p], "lr": lr, "name": str(i)} for i, (p, lr) in enumerate(zip(ps[:3], lrs))] +
+                [{"params": ps[3:], "lr": 8e-4, "name": "offset_model"}])
+    opt_a = FusedAdam(groups(a), lr=0.0, eps=1e-15)
+    opt_b = torch.optim.Adam(groups(b), lr=0.0, eps=1e-15, foreach=True)
+    return a, b, opt_a, opt_b, gen
+
+
+def _adam_backward(ps, ws, with_net):
+    """A loss linear in every Gaussian parameter and, when ``with_net``, in the network's (autograd producers
+    only: without it the network's parameters get no gradient at all -- grad None in torch)."""
+    n = len(ps) if with_net else 3
+    sum((p * w).sum() for p, w in zip(ps[:n], ws[:n])).backward()
+
+
+def test_fused_adam_skips_parameters_without_grad():
+    """torch.optim.Adam skips a parameter whose grad is None and keeps state['step'] per parameter: the
+    offset-network group gets no gradient for its first 4 steps (the reference's DirectTemporalNeRF returns zeros
+    before iteration 3000), then its first real update uses step 1's bias corrections.  FusedAdam must leave
+    those parameters and moments untouched while they get nothing and then match torch step for step (also
+    through allreduce_step, its data-parallel entry, at world size 1)."""
+    a, b, opt_a, opt_b, gen = _adam_pair()
+    for k in range(7):
+        ws = [torch.randn(p.shape, generator=gen).to(DEV) * (10.0 ** -(k % 3)) for p in a]
+        with_net = k >= 4
+        _adam_backward(a, ws, with_net)
+        _adam_backward(b, ws, with_net)
+        if k % 2:
+            opt_a.allreduce_step(zero_grad=True)
+        else:
+            opt_a.step(zero_grad=True)
+        opt_b.step()
+        opt_b.zero_grad(set_to_none=True)
+        for i, (pa, pb) in enumerate(zip(a, b)):
+            st = opt_b.state.get(pb)
+            assert opt_a.steps[i] == (int(st["step"]) if st else 0), (k, i)
+            assert float((pa - pb).abs().max()) <= 1e-6 * max(1.0, float(pb.abs().max())), (k, i)
+            if st:
+                ma, va = opt_a.moments(pa)
+                assert float((ma - st["exp_avg"]).abs().max()) <= 1e-7 * max(1.0, float(st["exp_avg"].abs().max()))
+                assert float((va - st["exp_avg_sq"]).abs().max()) <= 1e-7 * max(1e-12, float(st["exp_avg_sq"].abs().max()))
+        if not with_net:
+            for pa in a[3:]:
+                assert all(float(m.abs().max()) == 0.0 for m in opt_a.moments(pa))
+    assert opt_a.steps == [7, 7, 7, 3, 3, 3]
+
+
+def test_checkpoint_roundtrip_multi_parameter_group(tmp_path):
+    """gsd_amd.io.capture / restore with the offset network's multi-parameter group (nonzero moments, a step
+    count of its own -- it got gradients in 2 of 5 steps): every entry comes back by (group name, position in
+    group) with its own step, the state_dict loads into torch.optim.Adam, and the restored FusedAdam and that
+    torch Adam then take the same next step."""
+    from gsd_amd import DeformableGaussians
+    from gsd_amd.io import capture, restore
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    names = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
+    lrs = [0.00016, 0.0025, 0.0025 / 20.0, 0.05, 0.005, 0.001]
+
+    def model(seed):
+        torch.manual_seed(seed)
+        pc = DeformableGaussians(make_gaussians(599, 64, 48, seed=seed, device=DEV), sh_degree=3)
+        net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3)).to(DEV)
+        ps = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+        groups = ([{"params": [p], "lr": lr, "name": n} for p, lr, n in zip(ps, lrs, names)] +
+                  [{"params": list(net.parameters()), "lr": 8e-4, "name": "offset_model"}])
+        return ps, net, FusedAdam(groups, lr=0.0, eps=1e-15), pc
+
+    def backward(ps, net, ws, x, with_net):
+        loss = sum((p * w).sum() for p, w in zip(ps, ws))
+        if with_net:
+            loss = loss + net(x).square().sum()
+        loss.backward()
+
+    ps, net, opt, pc = model(1)
+    gen = torch.Generator().manual_seed(2)
+    x = torch.randn(5, 8, generator=gen).to(DEV)
+    for k in range(5):
+        backward(ps, net, [torch.randn(p.shape, generator=gen).to(DEV) for p in ps], x, k >= 3)
+        opt.step(zero_grad=True)
+    path = str(tmp_path / "chkpnt.pth")
+    torch.save(capture(pc, opt, None, 1.0), path)
+    args = torch.load(path, weights_only=True)
+    assert [float(args[10]["state"][i]["step"]) for i in range(10)] == [5.0] * 6 + [2.0] * 4
+    ps2, net2, opt2, pc2 = model(9)
+    net2.load_state_dict(net.state_dict())   # the reference saves the network itself separately
+    restore(args, pc2, opt2)
+    assert opt2.steps == opt.steps == [5] * 6 + [2] * 4
+    for p, q in zip(ps + list(net.parameters()), ps2 + list(net2.parameters())):
+        assert torch.equal(p.detach(), q.detach())
+        for m1, m2 in zip(opt.moments(p), opt2.moments(q)):
+            assert torch.equal(m1, m2) and float(m1.abs().max()) > 0
+    # the reference's optimizer built the same way takes the checkpoint and the same next step
+    ref_ps = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    ref_net = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 3)).to(DEV)
+    ref_net.load_state_dict(net.state_dict())
+    ref = torch.optim.Adam([{"params": [p], "lr": lr, "name": n} for p, lr, n in zip(ref_ps, lrs, names)] +
+                           [{"params": list(ref_net.parameters()), "lr": 8e-4, "name": "offset_model"}],
+                           lr=0.0, eps=1e-15)
+    ref.load_state_dict(args[10])
+    ws = [torch.randn(p.shape, generator=gen).to(DEV) for p in ps]
+    backward(ps2, net2, ws, x, True)
+    backward(ref_ps, ref_net, ws, x, True)
+    opt2.step(zero_grad=True)
+    ref.step()
+    for p, q in zip(ps2 + list(net2.parameters()), ref_ps + list(ref_net.parameters())):
+        assert float((p - q).abs().max()) <= 1e-6 * max(1.0, float(q.abs().max()))
+
+
 def test_densify_and_prune_matches_reference():
     """gsd_amd.densify (fused statistics kernel + FusedAdam slab surgery) vs the line-by-line restatement of
     scene/gaussian_model.py's densification on torch.optim.Adam (oracle/densify_ref.py): statistics after three

@@ -153,3 +153,81 @@ def test_four_rank_bucketed_allreduce_equals_sum_of_views(tmp_path):
     for r in range(world):
         got = np.load(os.path.join(str(tmp_path), f"brank{r}.npy"))
         np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
+
+
+class _SlabOpt:
+    """Stand-in for FusedAdam's slab surgery interface (param_groups, moments, rebuild) on CPU tensors."""
+
+    def __init__(self, params):
+        self.param_groups = [{"params": [p]} for p in params]
+        self.m = {id(p): torch.full_like(p, 0.5) for p in params}
+        self.v = {id(p): torch.full_like(p, 0.25) for p in params}
+
+    def moments(self, p):
+        return self.m[id(p)], self.v[id(p)]
+
+    def rebuild(self, datas, ms, vs):
+        ps = [g["params"][0] for g in self.param_groups]
+        self.m, self.v = {}, {}
+        for p, d, m, v in zip(ps, datas, ms, vs):
+            p.data = d.clone()
+            self.m[id(p)], self.v[id(p)] = m.clone(), v.clone()
+
+
+def _densify_model(P=300):
+    from gsd_amd import DeformableGaussians
+    from gsd_amd.densify import GaussianDensifier
+    from gsd_amd.scene import make_gaussians
+    pc = DeformableGaussians(make_gaussians(P, 64, 48, seed=3), sh_degree=3)
+    ps = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+    with torch.no_grad():   # a spread of scales so that both clone and split select points
+        pc._scaling.add_(torch.linspace(-2.0, 1.5, P)[:, None])
+    return pc, ps, GaussianDensifier(pc, _SlabOpt(ps))
+
+
+def _rank_stats(r, P):
+    """Rank r's own-view statistics (as add_densification_stats leaves them): different visibility, gradient
+    norms and radii per rank."""
+    g = torch.Generator().manual_seed(100 + r)
+    vis = torch.rand(P, generator=g) < 0.7
+    return (vis.float()[:, None], (torch.rand(P, 1, generator=g) * 4e-4) * vis[:, None],
+            torch.randint(0, 40, (P,), generator=g).float() * vis, torch.randn(P, 3, generator=g) * vis[:, None])
+
+
+def _worker_densify(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd.parallel import init_from_env
+    r, _, w = init_from_env(backend="gloo")
+    pc, ps, dens = _densify_model()
+    dens.denom, dens.xyz_gradient_accum, dens.max_radii2D, dens.xyz_gradient_accum_3vec = _rank_stats(r, 300)
+    torch.manual_seed(1000 + r)   # different generators per rank: the split samples must come from rank 0
+    dens.densify_and_prune(2e-4, 0.005, 2.0, 30)
+    np.savez(os.path.join(out_dir, f"dens{r}.npz"), *[p.detach().numpy() for p in ps])
+    dist.destroy_process_group()
+
+
+def test_two_rank_densify_keeps_replicas_identical(tmp_path):
+    """Data-parallel densify_and_prune (2 ranks, gloo): each rank holds only its own view's statistics and its
+    own random generator; both must end with identical parameters, equal to one process holding the combined
+    statistics (sums; max of the radii) and rank 0's generator."""
+    world = 2
+    mp.spawn(_worker_densify, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = [np.load(tmp_path / f"dens{r}.npz") for r in range(world)]
+    pc, ps, dens = _densify_model()
+    st = [_rank_stats(r, 300) for r in range(world)]
+    dens.denom = st[0][0] + st[1][0]
+    dens.xyz_gradient_accum = st[0][1] + st[1][1]
+    dens.max_radii2D = torch.maximum(st[0][2], st[1][2])
+    dens.xyz_gradient_accum_3vec = st[0][3] + st[1][3]
+    torch.manual_seed(1000)
+    dens.densify_and_prune(2e-4, 0.005, 2.0, 30)
+    assert ps[0].shape[0] != 300   # the scene changed (clone / split / prune all ran)
+    for i, p in enumerate(ps):
+        a0, a1 = got[0][f"arr_{i}"], got[1][f"arr_{i}"]
+        assert np.array_equal(a0, a1), i
+        np.testing.assert_allclose(a0, p.detach().numpy(), rtol=1e-6, atol=1e-7)
