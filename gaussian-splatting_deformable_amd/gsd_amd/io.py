@@ -128,6 +128,9 @@ def load_ply(path: str, max_sh_degree: int = 3) -> GaussianParams:
 _ORDER = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
 
 
+_ADAM_DEFAULTS = dict(torch.optim.Adam([torch.zeros(1, requires_grad=True)]).defaults)
+
+
 def _adam_state_dict(optimizer):
     """torch.optim.Adam.state_dict() layout for a FusedAdam (global indices in group order; a parameter that
     never got a gradient has no state entry, as in torch, and every entry carries its own step)."""
@@ -142,7 +145,9 @@ def _adam_state_dict(optimizer):
                               "exp_avg_sq": v.detach().clone()}
             ids.append(idx)
             idx += 1
-        groups.append({k: val for k, val in g.items() if k != "params"} | {"params": ids})
+        # torch.optim.Adam's own group keys (weight_decay, amsgrad, ...) at their defaults, so the state_dict
+        # loads into it and steps there
+        groups.append(_ADAM_DEFAULTS | {k: val for k, val in g.items() if k != "params"} | {"params": ids})
     return {"state": state, "param_groups": groups}
 
 

@@ -53,6 +53,7 @@ class FusedAdam(torch.optim.Optimizer):
         # the gradient views take each parameter's memory order, so slab element i of the gradient belongs to
         # slab element i of the parameter (what the fused Adam pass pairs)
         self.flat = FlatGrads(ps, device=dev)
+        self.flat.invalidate()   # a fresh parameter has no gradient (grad None) until a backward writes one
         self.exp_avg = torch.zeros_like(self.param_slab)
         self.exp_avg_sq = torch.zeros_like(self.param_slab)
         self._layout()
@@ -201,6 +202,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.param_slab, self.exp_avg, self.exp_avg_sq = param_slab, exp_avg, exp_avg_sq
         self.flat.remove_hooks()
         self.flat = FlatGrads(ps, device=dev)
+        self.flat.invalidate()   # the reference's surgery makes new nn.Parameters: no gradient yet
         self._layout()   # per-parameter step counts carry over (the reference keeps stored_state['step'])
 
     def reset_state(self):

@@ -430,3 +430,29 @@ def test_sh_grad_views_sums_per_view_sh_gradients():
     assert rel_l2(out_dc.cpu(), sums[0].cpu()) <= 1e-5 and rel_l2(out_rest.cpu(), sums[1].cpu()) <= 1e-5
     _C.sh_grad_views(3, means, views, P, 16, d_dc=out_dc, d_rest=out_rest, accumulate=True)
     assert rel_l2(out_rest.cpu(), 2 * sums[1].cpu()) <= 1e-5
+
+
+def test_sh_grad_views_mean_at_camera_centre():
+    """A Gaussian whose mean sits exactly at one view's camera centre is culled in that view (zero dL/dRGB
+    row); its SH gradient must be the other views' sum, finite -- not NaN from that view's zero-length
+    direction times the zero row."""
+    from gsd_amd import _C
+    P = 300
+    gen = torch.Generator().manual_seed(4)
+    means = torch.randn(P, 3, generator=gen).to(DEV)
+    cams = [torch.zeros(3), torch.tensor([0.5, -0.25, 1.0])]
+    means[7] = cams[0].to(DEV)
+    rows = []
+    for v, c in enumerate(cams):
+        g = torch.randn(P, 3, generator=gen)
+        if v == 0:
+            g[7] = 0.0   # culled in the view it sits in
+        rows.append(torch.cat([g.reshape(-1), c, torch.zeros(1)]).to(DEV))
+    f_dc = torch.full((P, 1, 3), float("nan"), device=DEV)
+    f_rest = torch.full((P, 15, 3), float("nan"), device=DEV)
+    _C.sh_grad_views(3, means, torch.stack(rows), P, 16, d_dc=f_dc, d_rest=f_rest, accumulate=False)
+    assert bool(torch.isfinite(f_dc).all()) and bool(torch.isfinite(f_rest).all())
+    one = torch.full((P, 1, 3), float("nan"), device=DEV)
+    one_rest = torch.full((P, 15, 3), float("nan"), device=DEV)
+    _C.sh_grad_views(3, means, rows[1][None].contiguous(), P, 16, d_dc=one, d_rest=one_rest, accumulate=False)
+    assert torch.equal(f_dc[7], one[7]) and torch.equal(f_rest[7], one_rest[7])

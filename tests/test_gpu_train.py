@@ -158,8 +158,9 @@ def test_fused_adam_skips_parameters_without_grad():
             assert float((pa - pb).abs().max()) <= 1e-6 * max(1.0, float(pb.abs().max())), (k, i)
             if st:
                 ma, va = opt_a.moments(pa)
-                assert float((ma - st["exp_avg"]).abs().max()) <= 1e-7 * max(1.0, float(st["exp_avg"].abs().max()))
-                assert float((va - st["exp_avg_sq"]).abs().max()) <= 1e-7 * max(1e-12, float(st["exp_avg_sq"].abs().max()))
+                # torch's foreach kernels may contract to FMA: moments agree to float rounding (rel 1e-6)
+                assert float((ma - st["exp_avg"]).abs().max()) <= 1e-6 * float(st["exp_avg"].abs().max())
+                assert float((va - st["exp_avg_sq"]).abs().max()) <= 1e-6 * float(st["exp_avg_sq"].abs().max())
         if not with_net:
             for pa in a[3:]:
                 assert all(float(m.abs().max()) == 0.0 for m in opt_a.moments(pa))
