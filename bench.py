@@ -79,6 +79,9 @@ def pmc_traffic(kernel):
     return None
 
 
+FUSED_STEP = os.environ.get("GSD_FUSED_STEP", "1") != "0"
+
+
 def make_optimizer(pc):
     """training_setup (scene/gaussian_model.py:834-864) param groups, spatial_lr_scale = 1, eps 1e-15, as one
     fused HIP Adam over flat slabs (gsd_amd.optim.FusedAdam; torch.optim.Adam semantics)."""
@@ -162,11 +165,18 @@ def main():
     def step():
         out = render(cam, pc, pipe, bg)
         loss = l1_ssim_loss(out["render"], target, 0.2)   # train.py:529, lambda_dssim = 0.2
-        loss.backward()
-        # the gradient all-reduce (RCCL, bucketed, asynchronous) overlapped with the Adam pass, which runs
-        # over each bucket as its sum arrives; a no-op collective at N = 1.  The gradient slab is marked
-        # stale for the next step instead of cleared.
-        opt.allreduce_step(zero_grad=True)
+        if FUSED_STEP:
+            # backward + Adam: at N = 1 every gradient is final inside the preprocess backward, which applies
+            # the Adam step there (FusedAdam.step_in_backward, gsd_adam_epilogue); with N > 1 the gradients
+            # are summed first, and leaving the block runs allreduce_step as below
+            with opt.step_in_backward():
+                loss.backward()
+        else:
+            loss.backward()
+            # the gradient all-reduce (RCCL, bucketed, asynchronous) overlapped with the Adam pass, which runs
+            # over each bucket as its sum arrives; a no-op collective at N = 1.  The gradient slab is marked
+            # stale for the next step instead of cleared.
+            opt.allreduce_step(zero_grad=True)
         return out
 
     # Adam moves every parameter by ~lr per step whatever the gradient, so the scene drifts from the configured
@@ -179,7 +189,7 @@ def main():
             for p, s0 in zip(pc.parameters(), snapshot):
                 p.copy_(s0)
             opt.reset_state()
-        flat.zero()
+        flat.invalidate()   # as a fresh optimizer: no gradients yet
 
     for _ in range(args.warmup):
         step()

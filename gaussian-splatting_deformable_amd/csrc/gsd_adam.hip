@@ -15,15 +15,6 @@
 
 namespace gsd {
 
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float beta2, float omb2,
-                                          float step_size, float bc2_sqrt, float eps) {
-    m = w1 < 0.5f ? m + w1 * (g - m) : g - (g - m) * (1.f - w1);
-    v = v * beta2;
-    v = v + omb2 * g * g;
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p = p + step_size * (m / denom);
-}
-
 // Measured on the bench slab (59M floats, 28 B each): nontemporal loads/stores 4.9 -> 5.5 TB/s, and one quad
 // per thread (a grid covering the slab) rather than a grid-stride loop over 8192 workgroups 5.5 -> 5.8 TB/s;
 // more quads per thread per iteration (2, 4) did not help.

@@ -169,6 +169,53 @@ void set_sh_strides(Prm& p, const gsd_sh_split* sp, int M) {
     p.rest_se = rest_set ? sp->rest_stride_e : 1;
 }
 
+// gsd_adam_epilogue -> the kernels' float coefficients, formed in double as gsd_adam_step forms them; checks
+// that every fused sink is one the backward stores into with the layout the fused kernels walk.
+gsd::AdamSinkDev adam_sink(const gsd_adam_sink& k, double beta1, double beta2) {
+    gsd::AdamSinkDev d{};
+    if (!k.param) return d;
+    const double bc1 = 1.0 - std::pow(beta1, (double)k.step), bc2 = 1.0 - std::pow(beta2, (double)k.step);
+    d.p = k.param; d.m = k.exp_avg; d.v = k.exp_avg_sq;
+    d.step_size = (float)((k.lr / bc1) * -1.0);
+    d.bc2_sqrt = (float)std::pow(bc2, 0.5);
+    return d;
+}
+int adam_epilogue(const gsd_raster_args* a, const gsd_activation* act, const gsd_adam_epilogue* ad,
+                  gsd::AdamEpiDev* out) {
+    const gsd_adam_sink* all[6] = {&ad->dc, &ad->rest, &ad->xyz, &ad->scaling, &ad->rotation, &ad->opacity};
+    for (const gsd_adam_sink* k : all)
+        if (k->param && (!k->exp_avg || !k->exp_avg_sq || k->step < 1))
+            return fail(GSD_ERR_ARG, "adam epilogue: a fused sink needs both moments and a step count >= 1");
+    const gsd_sh_split* sp = a->sh_split;
+    if (ad->dc.param || ad->rest.param) {
+        if (!sp || sp->accumulate || sp->d_rgb || a->M != 16 || sp->dc_stride_g || sp->dc_stride_e ||
+            sp->rest_stride_g || sp->rest_stride_e)
+            return fail(GSD_ERR_ARG, "adam epilogue: the SH pieces need sh_split in store mode (accumulate 0, no "
+                                     "d_rgb), M = 16 and contiguous (P,K,3) layouts");
+        if ((ad->dc.param && ad->dc.param != sp->dc) || (ad->rest.param && ad->rest.param != sp->rest))
+            return fail(GSD_ERR_ARG, "adam epilogue: dc / rest params must be the sh_split pieces themselves");
+    }
+    if (ad->xyz.param || ad->scaling.param || ad->rotation.param || ad->opacity.param) {
+        if (!act || act->accumulate)
+            return fail(GSD_ERR_ARG, "adam epilogue: the raw parameters need gsd_activation in store mode");
+        if ((ad->xyz.param && ad->xyz.param != a->means3D) || (ad->scaling.param && ad->scaling.param != a->scales) ||
+            (ad->rotation.param && ad->rotation.param != a->rotations) ||
+            (ad->opacity.param && ad->opacity.param != a->opacities))
+            return fail(GSD_ERR_ARG, "adam epilogue: raw params must be the tensors the rasterizer reads");
+    }
+    out->dc = adam_sink(ad->dc, ad->beta1, ad->beta2);
+    out->rest = adam_sink(ad->rest, ad->beta1, ad->beta2);
+    out->xyz = adam_sink(ad->xyz, ad->beta1, ad->beta2);
+    out->scaling = adam_sink(ad->scaling, ad->beta1, ad->beta2);
+    out->rotation = adam_sink(ad->rotation, ad->beta1, ad->beta2);
+    out->opacity = adam_sink(ad->opacity, ad->beta1, ad->beta2);
+    out->w1 = (float)(1.0 - ad->beta1);
+    out->beta2 = (float)ad->beta2;
+    out->omb2 = (float)(1.0 - ad->beta2);
+    out->eps = (float)ad->eps;
+    return GSD_OK;
+}
+
 int validate(const gsd_raster_args* a, bool forward) {
     if (!a) return fail(GSD_ERR_ARG, "null gsd_raster_args");
     if (a->P < 0) return fail(GSD_ERR_ARG, "means3D must have dimensions (num_points, 3)");
@@ -525,6 +572,10 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
         p.raw_act = 1; p.raw_opacity = a->opacities;
         p.a_xyz = act->d_xyz; p.a_scaling = act->d_scaling; p.a_rotation = act->d_rotation;
         p.a_opacity = act->d_opacity; p.a_accumulate = act->accumulate;
+    }
+    if (const gsd_adam_epilogue* ad = a->adam) {
+        if (int e = adam_epilogue(a, act, ad, &p.adam)) return e;
+        p.adam_on = 1;
     }
     timed(kPreBwd, s, [&] { gsd::launch_preprocess_bwd(p, s); });
     GSD_CHECK(a->debug, s);

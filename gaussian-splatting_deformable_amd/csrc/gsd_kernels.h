@@ -52,6 +52,37 @@ enum GradRecField { kRecMean2D = 0, kRecConic = 2, kRecOpacity = 5, kRecColor = 
 // k_preprocess_bwd (the two halves of the per-Gaussian backward)
 constexpr int kRecShMean = 9;
 
+// The Adam step of one fused sink (gsd_adam_sink after the host's double-precision coefficients); p == nullptr:
+// not fused, the gradient goes to the sink.
+struct AdamSinkDev {
+    float* p;
+    float* m;
+    float* v;
+    float step_size, bc2_sqrt;  // -lr / (1 - beta1^t), sqrt(1 - beta2^t)
+};
+struct AdamEpiDev {
+    AdamSinkDev dc, rest, xyz, scaling, rotation, opacity;
+    float w1, beta2, omb2, eps;  // 1 - beta1, beta2, 1 - beta2, eps
+};
+
+// torch.optim.Adam's per-element update in torch's foreach order (torch/optim/adam.py _multi_tensor_adam):
+//   m = lerp(m, g, 1 - beta1); v = v * beta2 + (1 - beta2) * g * g; p += step_size * (m / (sqrt(v) / bc2 + eps))
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float beta2, float omb2,
+                                          float step_size, float bc2_sqrt, float eps) {
+    m = w1 < 0.5f ? m + w1 * (g - m) : g - (g - m) * (1.f - w1);
+    v = v * beta2;
+    v = v + omb2 * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + step_size * (m / denom);
+}
+__device__ __forceinline__ void adam_at(const AdamSinkDev& s, const AdamEpiDev& e, long long i, float g) {
+    float pp = s.p[i], mm = s.m[i], vv = s.v[i];
+    adam_elem(pp, g, mm, vv, e.w1, e.beta2, e.omb2, s.step_size, s.bc2_sqrt, e.eps);
+    s.p[i] = pp;
+    s.m[i] = mm;
+    s.v[i] = vv;
+}
+
 struct PreprocessBwdParams {
     int P, D, M;
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
@@ -87,6 +118,8 @@ struct PreprocessBwdParams {
     int a_accumulate;
     float* dL_dscales;
     float* dL_drotations;
+    int adam_on;           // fused Adam epilogue (any of its sinks set)
+    AdamEpiDev adam;
 };
 
 struct BinParams {

@@ -396,17 +396,27 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
         v = vis ? v : 0.f;
         *d = acc ? *d + v : v;
     };
-    if (p.a_xyz) {
+    // fused Adam epilogue (store mode only): the element's final gradient updates the parameter in place
+    auto upd = [&](const AdamSinkDev& sk, long long e, float v) { adam_at(sk, p.adam, e, vis ? v : 0.f); };
+    if (p.adam_on && p.adam.xyz.p) {
+        upd(p.adam.xyz, 3LL * i, dmean.x);
+        upd(p.adam.xyz, 3LL * i + 1, dmean.y);
+        upd(p.adam.xyz, 3LL * i + 2, dmean.z);
+    } else if (p.a_xyz) {
         put(p.a_xyz + 3 * i, dmean.x);
         put(p.a_xyz + 3 * i + 1, dmean.y);
         put(p.a_xyz + 3 * i + 2, dmean.z);
     }
-    if (p.a_scaling) {
+    if (p.adam_on && p.adam.scaling.p) {
+        upd(p.adam.scaling, 3LL * i, dscale.x * scale.x);
+        upd(p.adam.scaling, 3LL * i + 1, dscale.y * scale.y);
+        upd(p.adam.scaling, 3LL * i + 2, dscale.z * scale.z);
+    } else if (p.a_scaling) {
         put(p.a_scaling + 3 * i, dscale.x * scale.x);
         put(p.a_scaling + 3 * i + 1, dscale.y * scale.y);
         put(p.a_scaling + 3 * i + 2, dscale.z * scale.z);
     }
-    if (p.a_rotation) {
+    if (p.a_rotation || (p.adam_on && p.adam.rotation.p)) {
         const float nraw = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
         float4 gq;
         if (nraw > 1e-12f) {
@@ -419,14 +429,24 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
             gq = make_float4(drot.x * 1e12f, drot.y * 1e12f, drot.z * 1e12f, drot.w * 1e12f);
         }
         if (!vis) gq = make_float4(0.f, 0.f, 0.f, 0.f);
-        float4* d = reinterpret_cast<float4*>(p.a_rotation) + i;
-        if (acc) {
-            const float4 o = *d;
-            gq = make_float4(o.x + gq.x, o.y + gq.y, o.z + gq.z, o.w + gq.w);
+        if (p.adam_on && p.adam.rotation.p) {
+            upd(p.adam.rotation, 4LL * i, gq.x);
+            upd(p.adam.rotation, 4LL * i + 1, gq.y);
+            upd(p.adam.rotation, 4LL * i + 2, gq.z);
+            upd(p.adam.rotation, 4LL * i + 3, gq.w);
+        } else {
+            float4* d = reinterpret_cast<float4*>(p.a_rotation) + i;
+            if (acc) {
+                const float4 o = *d;
+                gq = make_float4(o.x + gq.x, o.y + gq.y, o.z + gq.z, o.w + gq.w);
+            }
+            *d = gq;
         }
-        *d = gq;
     }
-    if (p.a_opacity) {
+    if (p.adam_on && p.adam.opacity.p) {
+        const float sg = act_opac(raw_opac);
+        upd(p.adam.opacity, i, dopac * sg * (1.f - sg));
+    } else if (p.a_opacity) {
         const float sg = act_opac(raw_opac);
         put(p.a_opacity + i, dopac * sg * (1.f - sg));
     }
@@ -612,7 +632,46 @@ __device__ __forceinline__ void sh_region_store(float* __restrict__ dst, int row
     }
 }
 
-template <int DEG, int kSrc, bool kAcc>
+// The fused Adam step over a region (gsd_adam_epilogue): the gradient rows in LDS (columns [c0, c0 + R)) are
+// the final gradients of the region's parameter elements; each is applied to (param, exp_avg, exp_avg_sq) in
+// place -- coalesced like sh_region_store, kCh elements per lane in flight -- instead of being stored.
+template <int R>
+__device__ __forceinline__ void sh_region_adam(const AdamSinkDev& sk, const AdamEpiDev& e, long long base, int rows,
+                                               const float* __restrict__ lds, int c0) {
+    constexpr int kCh = R < 15 ? R : 15;
+    static_assert(R % kCh == 0, "whole chunks");
+    const int lane = threadIdx.x, n = rows * R;
+    float* __restrict__ P = sk.p + base;
+    float* __restrict__ Mo = sk.m + base;
+    float* __restrict__ V = sk.v + base;
+#pragma unroll
+    for (int c = 0; c < R; c += kCh) {
+        float g[kCh], pp[kCh], mm[kCh], vv[kCh];
+        bool in[kCh];
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+            const int el = (c + i) * kShWave + lane;
+            const int gi = el / R, j = el - gi * R;
+            in[i] = rows == kShWave || el < n;
+            g[i] = lds[gi * kShRowStride + c0 + j];
+            pp[i] = in[i] ? P[el] : 0.f;
+            mm[i] = in[i] ? __builtin_nontemporal_load(Mo + el) : 0.f;
+            vv[i] = in[i] ? __builtin_nontemporal_load(V + el) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+            adam_elem(pp[i], g[i], mm[i], vv[i], e.w1, e.beta2, e.omb2, sk.step_size, sk.bc2_sqrt, e.eps);
+            const int el = (c + i) * kShWave + lane;
+            if (in[i]) {
+                P[el] = pp[i];
+                __builtin_nontemporal_store(mm[i], Mo + el);
+                __builtin_nontemporal_store(vv[i], V + el);
+            }
+        }
+    }
+}
+
+template <int DEG, int kSrc, bool kAcc, bool kAdam = false>
 __global__ __launch_bounds__(kShWave) __attribute__((amdgpu_waves_per_eu(4))) void k_preprocess_bwd_sh_rows(PreprocessBwdParams p) {
     __shared__ float rows_lds[kShWave * kShRowStride];
     constexpr int M = 16;
@@ -679,8 +738,12 @@ __global__ __launch_bounds__(kShWave) __attribute__((amdgpu_waves_per_eu(4))) vo
         sh_region_store<3 * M, false>(p.dL_dsh + (size_t)g0 * 3 * M, rows, rows_lds, 0);
         return;
     }
-    if (p.dsh_dc) sh_region_store<3, kAcc>(p.dsh_dc + (size_t)g0 * 3, rows, rows_lds, 0);
-    if (p.dsh_rest) sh_region_store<3 * (M - 1), kAcc>(p.dsh_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    if (kAdam && p.adam.dc.p) sh_region_adam<3>(p.adam.dc, p.adam, (long long)g0 * 3, rows, rows_lds, 0);
+    else if (p.dsh_dc) sh_region_store<3, kAcc>(p.dsh_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    if (kAdam && p.adam.rest.p)
+        sh_region_adam<3 * (M - 1)>(p.adam.rest, p.adam, (long long)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    else if (p.dsh_rest)
+        sh_region_store<3 * (M - 1), kAcc>(p.dsh_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
     if (p.dsh_off) sh_region_store<3 * M, kAcc>(p.dsh_off + (size_t)g0 * 3 * M, rows, rows_lds, 0);
 }
 
@@ -941,6 +1004,16 @@ void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
 }
 template <bool kStr, int kSrc, bool kAcc>
 static void launch_bwd_sh(const PreprocessBwdParams& p, dim3 g, dim3 b, hipStream_t s) {
+    if (!kStr && !kAcc && kSrc != 0 && p.M == 16 && (p.adam.dc.p || p.adam.rest.p)) {  // fused Adam epilogue
+        const dim3 gw((p.P + kShWave - 1) / kShWave), bw(kShWave);
+        switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+            case 0: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<0, kSrc, false, true>), gw, bw, 0, s, p); break;
+            case 1: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<1, kSrc, false, true>), gw, bw, 0, s, p); break;
+            case 2: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<2, kSrc, false, true>), gw, bw, 0, s, p); break;
+            default: hipLaunchKernelGGL((k_preprocess_bwd_sh_rows<3, kSrc, false, true>), gw, bw, 0, s, p); break;
+        }
+        return;
+    }
     if (!kStr && p.M == 16) {  // coalesced rows (every training configuration)
         const dim3 gw((p.P + kShWave - 1) / kShWave), bw(kShWave);
         switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {

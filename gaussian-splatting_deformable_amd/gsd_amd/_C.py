@@ -204,18 +204,22 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
                                  campos, geomBuffer, R, binningBuffer, imageBuffer, debug, sh_split=None,
-                                 activation=None, raw_opacity=None):
+                                 activation=None, raw_opacity=None, adam=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196):
     -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
     With ``sh_split`` the SH gradients go to its sinks and dL_dsh is None; so is dL_dcov3D when no
     cov3D_precomp was given (the scales/rotations gradients are what such a caller uses).  With
     ``activation`` (a _native.Activation; scales / rotations and ``raw_opacity`` are then the raw parameters)
-    the parameter gradients go to its sinks and only dL_dmeans2D (and dL_dcov3D, dL_dsh) are returned."""
+    the parameter gradients go to its sinks and only dL_dmeans2D (and dL_dcov3D, dL_dsh) are returned.
+    ``adam`` (a _native.AdamEpilogue) fuses the Adam step of the SH pieces / raw parameters it names into this
+    backward: those are updated in place and their sinks are not written."""
     lib = _native.load()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))  # rasterize_points.cu:142-143
     a = _Args(background, means3D, colors, raw_opacity if activation is not None else None, scales, rotations,
               scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, sh, degree, campos,
               False, debug, sh_split, activation)
+    if adam is not None:
+        a.c.adam = ctypes.addressof(adam)
     dev, P, M = a.dev, a.P, a.M
     split = sh_split is not None
     want_cov = not split or a.cov3D is not None

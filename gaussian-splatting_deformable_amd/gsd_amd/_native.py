@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -34,6 +34,20 @@ class Activation(ctypes.Structure):
     _fields_ = [("d_xyz", _vp), ("d_scaling", _vp), ("d_rotation", _vp), ("d_opacity", _vp), ("accumulate", _i32)]
 
 
+class AdamSink(ctypes.Structure):
+    """Mirror of ``gsd_adam_sink`` (include/gsd_raster.h)."""
+
+    _fields_ = [("param", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("lr", ctypes.c_double), ("step", _i64)]
+
+
+class AdamEpilogue(ctypes.Structure):
+    """Mirror of ``gsd_adam_epilogue``: the Adam step fused into the rasterizer backward."""
+
+    _fields_ = [("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+                ("dc", AdamSink), ("rest", AdamSink), ("xyz", AdamSink), ("scaling", AdamSink),
+                ("rotation", AdamSink), ("opacity", AdamSink)]
+
+
 class RasterArgs(ctypes.Structure):
     """Mirror of ``gsd_raster_args`` (include/gsd_raster.h)."""
 
@@ -43,7 +57,7 @@ class RasterArgs(ctypes.Structure):
         ("prefiltered", _i32), ("debug", _i32),
         ("background", _vp), ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp),
         ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp), ("projmatrix", _vp),
-        ("campos", _vp), ("sh_split", _vp), ("activation", _vp),
+        ("campos", _vp), ("sh_split", _vp), ("activation", _vp), ("adam", _vp),
     ]
 
 

@@ -10,13 +10,14 @@ data-parallel all-reduce sums).  There is no CPU path.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
 
 from . import _native
 from ._C import _ptr, _stream
-from .parallel import FlatGrads, slab_view
+from .parallel import FlatGrads, data_parallel_world, slab_view
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -82,10 +83,11 @@ class FusedAdam(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero()
 
-    def _advance(self, missing):
+    def _advance(self, missing, done=frozenset()):
         """torch.optim.Adam skips a parameter whose grad is None and keeps state['step'] per parameter: count
-        this step for every parameter that got a gradient.  Returns their indices."""
-        active = [i for i, p in enumerate(self._params) if id(p) not in missing]
+        this step for every parameter that got a gradient (``done``: already stepped inside the backward).
+        Returns their indices."""
+        active = [i for i, p in enumerate(self._params) if id(p) not in missing and id(p) not in done]
         for i in active:
             self.steps[i] += 1
         return set(active)
@@ -152,7 +154,7 @@ class FusedAdam(torch.optim.Optimizer):
         parameters (as DistributedDataParallel requires), or their step counts diverge."""
         from .parallel import BUCKET_FLOATS
         ranges = self.flat.allreduce_buckets(bucket_floats or BUCKET_FLOATS)
-        active = self._advance(self.flat.missing)
+        active = self._advance(self.flat.missing, self.flat.fused)
         for a, b, w in ranges:        # ranges with nothing to wait for first
             if w is None:
                 self._adam(a, b, active)
@@ -162,6 +164,65 @@ class FusedAdam(torch.optim.Optimizer):
                 self._adam(a, b, active)
         if zero_grad:
             self.flat.invalidate()
+
+    @contextlib.contextmanager
+    def step_in_backward(self):
+        """``with opt.step_in_backward(): loss.backward()`` is ``loss.backward(); opt.allreduce_step(zero_grad=True)``
+        with the Adam step of every parameter whose gradient is final inside the rasterizer backward fused into
+        that backward (``fuse``; gsd_adam_epilogue): the gradient never goes through HBM, 8 B per float saved
+        (of the 28 B of the separate pass).  Such a gradient is final there when the rasterizer is its only
+        producer (store mode: the parameter had no gradient yet this step) and no rank sums it (world size 1).
+        The rest is stepped on leaving the block, as ``allreduce_step`` does.  Afterwards the fused parameters'
+        ``.grad`` hold no gradient (as after ``zero_grad(set_to_none=True)``); a second gradient producer for
+        one of them inside the block -- which the fused step would have missed -- raises."""
+        if self.flat.epilogue is not None:
+            raise RuntimeError("step_in_backward: already inside a step_in_backward block")
+        self.flat.epilogue = self
+        try:
+            yield self
+        except BaseException:
+            self.flat.epilogue = None
+            self.flat.fused = set()
+            raise
+        self.flat.epilogue = None
+        self.allreduce_step(zero_grad=True)
+        self.flat.fused = set()
+
+    def fuse(self, named, epi=None):
+        """Called by the rasterizer backward inside ``step_in_backward`` for sinks it is about to store into:
+        ``named`` maps gsd_adam_epilogue slots ("dc", "rest", "xyz", "scaling", "rotation", "opacity") to
+        parameters.  Counts their step now and returns ``epi`` (a _native.AdamEpilogue, created when None) with
+        their slots filled -- or ``epi`` unchanged when the step cannot be fused here (world size > 1, a
+        coefficient-major slab, a parameter this optimizer does not own or has already stepped)."""
+        if self.flat.epilogue is not self or data_parallel_world() != 1 or self.coef_major:
+            return epi
+        index = {id(p): i for i, p in enumerate(self._params)}
+        if any(id(p) not in index or id(p) in self.flat.fused for p in named.values()):
+            return epi
+        if epi is None:
+            g0 = self.param_groups[0]
+            epi = _native.AdamEpilogue(beta1=float(g0["betas"][0]), beta2=float(g0["betas"][1]),
+                                       eps=float(g0["eps"]))
+        f4 = 4
+        for slot, p in named.items():
+            i = index[id(p)]
+            self.steps[i] += 1
+            a = self._span[i][0]
+            setattr(epi, slot, _native.AdamSink(
+                param=p.data_ptr(), exp_avg=self.exp_avg.data_ptr() + f4 * a,
+                exp_avg_sq=self.exp_avg_sq.data_ptr() + f4 * a,
+                lr=float(self.param_groups[self._gidx[i]]["lr"]), step=self.steps[i]))
+            self.flat.fused.add(id(p))
+        return epi
+
+    @staticmethod
+    def fused_owner(params):
+        """The FusedAdam inside ``step_in_backward`` that owns ``params`` (through their FlatGrads), or None."""
+        flats = {id(getattr(p, "_gsd_flat", None)): getattr(p, "_gsd_flat", None) for p in params}
+        if len(flats) != 1:
+            return None
+        f = next(iter(flats.values()))
+        return getattr(f, "epilogue", None) if f is not None else None
 
     def moments(self, p: torch.Tensor):
         """(exp_avg, exp_avg_sq) views of parameter ``p`` (shaped like ``p``)."""

@@ -101,13 +101,23 @@ class FlatGrads:
             off += p.numel()
         self.stale = set()
         self.missing = set()   # what the last settle() found without a gradient
+        self.epilogue = None   # the FusedAdam inside its step_in_backward block, if any
+        self.fused = set()     # parameters that block already stepped inside the backward
         self.reduced = set()   # views already summed over the ranks this step (mark_reduced)
         self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
         self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
         self.attach()
 
+    def _fused_guard(self, ids):
+        if self.fused.intersection(ids):
+            raise RuntimeError("FlatGrads: a second gradient for a parameter whose Adam step already ran inside "
+                               "the backward (FusedAdam.step_in_backward); leave it out of that block")
+
     def _before_accumulate(self, p):
         def hook(grad):
+            if grad is None:   # a fused HIP backward wrote the .grad in place (it returns None to autograd)
+                return grad
+            self._fused_guard([id(p)])
             if id(p) in self.stale:
                 self._view_of[id(p)].zero_()
                 self.stale.discard(id(p))
@@ -141,6 +151,7 @@ class FlatGrads:
         """A fused backward is about to produce the gradients of ``params`` in place: True = add into the
         views, False = store (they were all stale).  A mix zeroes the stale ones and adds."""
         ids = [id(p) for p in params]
+        self._fused_guard(ids)
         fresh = [i for i in ids if i in self.stale]
         if fresh and len(fresh) == len(ids):
             self.stale.difference_update(ids)

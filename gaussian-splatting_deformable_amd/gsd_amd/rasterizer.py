@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from . import _C, _native, parallel
+from .optim import FusedAdam
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -151,16 +152,22 @@ class _RasterizeRaw(torch.autograd.Function):
             return (None,) * 9
         saved = ctx.saved_tensors
         xyz, scaling, rotation, opacity = saved[0], saved[1], saved[2], saved[10]
-        sinks, acc = _sinks((xyz, scaling, rotation, opacity))
+        raw = (xyz, scaling, rotation, opacity)
+        sinks, acc = _sinks(raw)
+        epi = None
         if sinks is None:
-            sinks, acc = [torch.empty_like(t) for t in (xyz, scaling, rotation, opacity)], False
+            sinks, acc = [torch.empty_like(t) for t in raw], False
             ret = sinks
         else:
             ret = [None] * 4
+            owner = FusedAdam.fused_owner(raw) if not acc else None
+            if owner is not None:   # the raw parameters' Adam step runs inside this backward
+                epi = owner.fuse(dict(zip(("xyz", "scaling", "rotation", "opacity"), raw)))
         act = _native.Activation(d_xyz=sinks[0].data_ptr(), d_scaling=sinks[1].data_ptr(),
                                  d_rotation=sinks[2].data_ptr(), d_opacity=sinks[3].data_ptr(),
                                  accumulate=int(bool(acc)))
-        g_m2d, d_dc, d_rest, _, _ = _split_sh_backward(ctx, grad_out_color, activation=act, raw_opacity=opacity)
+        g_m2d, d_dc, d_rest, _, _ = _split_sh_backward(ctx, grad_out_color, activation=act, raw_opacity=opacity,
+                                                       epi=epi, raw=raw)
         return ret[0], g_m2d, d_dc, d_rest, ret[1], ret[2], ret[3], None, None
 
 
@@ -177,10 +184,11 @@ def _save(ctx, rs, num_rendered, radii, means3D, scales, rotations, f_dc, f_rest
                           imgBuffer, opacity if opacity is not None else torch.empty(0))
 
 
-def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None):
+def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None, epi=None, raw=()):
     """Shared backward of the split-SH rasterizer paths -> (dL/dmeans2D, d_dc, d_rest, d_offset,
     (dL/dopacity, dL/dmeans3D, dL/dscales, dL/drotations)); the SH gradients are None when they went into
-    the parameters' .grad in place, the last four when ``activation`` took them."""
+    the parameters' .grad in place, the last four when ``activation`` took them.  ``epi``: the Adam epilogue
+    the caller set up for ``raw`` (FusedAdam.step_in_backward); the SH pieces join it when they can."""
     from .activate import _sinks
     rs = ctx.raster_settings
     means3D, scales, rotations, radii, f_dc, f_rest, sh_offset, geomBuffer, binningBuffer, imgBuffer, opac = \
@@ -195,6 +203,9 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None):
         return g_m2d, None, None, None, (g_op, g_m3d, g_sc, g_rot)
     if sinks is not None:
         d_dc, d_rest = sinks
+        owner = FusedAdam.fused_owner(ctx.params) if not acc else None
+        if owner is not None and f_dc.is_contiguous() and f_rest.is_contiguous():
+            epi = owner.fuse({"dc": f_dc, "rest": f_rest}, epi)
     else:
         d_dc, d_rest = torch.zeros_like(f_dc), torch.zeros_like(f_rest)
     d_off = None
@@ -204,7 +215,12 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None):
     g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
-        binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity)
+        binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity,
+        adam=epi)
+    if epi is not None:   # parameters the kernel updated in place: autograd's saved-tensor checks must see it
+        for p in (*raw, f_dc, f_rest):
+            if id(p) in p._gsd_flat.fused:
+                torch.autograd.graph.increment_version(p)
     if sinks is not None:
         d_dc = d_rest = None
     return g_m2d, d_dc, d_rest, d_off, (g_op, g_m3d, g_sc, g_rot)

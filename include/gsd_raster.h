@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 7
+#define GSD_ABI_VERSION 8
 
 enum {
     GSD_OK = 0,
@@ -98,6 +98,25 @@ typedef struct gsd_activation {
     int32_t accumulate;    /* 1 = add into the sinks, 0 = store (every Gaussian written) */
 } gsd_activation;
 
+/* Optional Adam step fused into the backward (ABI 8): torch.optim.Adam's update (the same per-element
+ * arithmetic as gsd_adam_step) applied where the backward would store a parameter's gradient -- the gradient
+ * is final there when this backward is its only producer and nothing sums it over ranks -- instead of writing
+ * it into the sink.  That is backward + step without the gradient's round trip through HBM (8 B per float).
+ * A sink with param == NULL is not fused: its gradient is written as usual.  Fusion needs the store mode
+ * (accumulate == 0) of its sink and contiguous (P,K,3) SH pieces; sh_split.d_rgb excludes the SH sinks. */
+typedef struct gsd_adam_sink {
+    float* param;          /* the parameter the rasterizer read (features_dc / _rest, _xyz, _scaling, ...) */
+    float* exp_avg;        /* Adam moments, the parameter's layout */
+    float* exp_avg_sq;
+    double lr;             /* its group's learning rate */
+    int64_t step;          /* its 1-based step count after this update */
+} gsd_adam_sink;
+typedef struct gsd_adam_epilogue {
+    double beta1, beta2, eps;
+    gsd_adam_sink dc, rest;                          /* the split SH pieces (gsd_sh_split) */
+    gsd_adam_sink xyz, scaling, rotation, opacity;   /* the raw parameters (gsd_activation) */
+} gsd_adam_epilogue;
+
 /* Raster settings + per-Gaussian inputs of one view.  Mirrors the 19 arguments
  * of _C.rasterize_gaussians (rasterize_points.cu:36-55).  Absent optional
  * inputs are NULL (the reference passes empty tensors -> nullptr). */
@@ -123,6 +142,7 @@ typedef struct gsd_raster_args {
     const float* campos;        /* (3) */
     const gsd_sh_split* sh_split; /* NULL, or the split SH operand above (then shs == NULL) */
     const gsd_activation* activation; /* NULL, or: scales / rotations / opacities are raw parameters */
+    const gsd_adam_epilogue* adam;    /* backward only: NULL, or the fused Adam step above (ABI 8) */
 } gsd_raster_args;
 
 int gsd_abi_version(void);

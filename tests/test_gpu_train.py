@@ -408,3 +408,94 @@ def test_coefficient_major_sh_layout_same_gradients():
         outs.append([p.detach().clone() for p in pc.parameters()])
     for a, b in zip(*outs):
         assert rel_l2(a, b) <= 1e-5
+
+
+def _fused_step_run(fused, net=None, steps=3, P=20_000, W=320, H=240, iteration=0):
+    """render + loss + backward + Adam for `steps` steps, with the step fused into the backward
+    (FusedAdam.step_in_backward) or as the separate pass (allreduce_step) -> parameters, moments, steps."""
+    from gsd_amd import DeformableGaussians, default_pipe, l1_ssim_loss, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    params = make_gaussians(P, W, H, seed=8, device=DEV)
+    cam = synthetic_camera(W, H).to(DEV)
+    pc = DeformableGaussians(params, sh_degree=3, offset_model=net)
+    names = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
+    lrs = [0.00016, 0.0025, 0.0025 / 20.0, 0.05, 0.005, 0.001]
+    ps = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+    groups = [{"params": [p], "lr": lr, "name": n} for p, lr, n in zip(ps, lrs, names)]
+    if net is not None:
+        groups.append({"params": list(net.parameters()), "lr": 1e-4, "name": "offset_model"})
+    opt = FusedAdam(groups, lr=0.0, eps=1e-15)
+    gt = torch.rand(3, H, W, generator=torch.Generator().manual_seed(3)).to(DEV)
+    for _ in range(steps):
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV), iteration=iteration)
+        loss = l1_ssim_loss(out["render"], gt, 0.2)
+        if fused:
+            with opt.step_in_backward():
+                loss.backward()
+        else:
+            loss.backward()
+            opt.allreduce_step(zero_grad=True)
+    return ([p.detach().clone() for p in opt._params], [m.clone() for p in opt._params for m in opt.moments(p)],
+            list(opt.steps), opt)
+
+
+def test_step_in_backward_equals_backward_then_step():
+    """FusedAdam.step_in_backward (Adam fused into the preprocess backward for the SH pieces and the raw
+    parameters: gsd_adam_epilogue) gives the parameters and moments of backward() + allreduce_step() -- the same
+    per-element arithmetic, up to the float-atomic order of the rasterizer's gradient sums -- and the same step
+    counts; no separate Adam launch remains."""
+    from gsd_amd._native import kernel_times
+    kernel_times(enable=True, reset=True)
+    a_p, a_m, a_s, opt = _fused_step_run(True)
+    kt = kernel_times(enable=False, reset=True)
+    assert "adam" not in kt and opt.flat.fused == set()
+    b_p, b_m, b_s, _ = _fused_step_run(False)
+    assert a_s == b_s == [3] * 6
+    for x, y in zip(a_p + a_m, b_p + b_m):
+        assert rel_l2(x, y) <= 1e-5
+        assert float((x - y).abs().max()) <= 1e-5 * max(1.0, float(y.abs().max()))
+
+
+def test_step_in_backward_with_offset_network():
+    """With the deformation network live (iteration past 3000): the SH pieces are fused (the offset's gradient
+    still flows to the network), the raw parameters take the separate pass (the activation preamble path),
+    the network is stepped on leaving the block -- all equal to backward() + step."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    res = []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        net = DirectTemporalNeRF().to(DEV)
+        with torch.no_grad():
+            for h in (net._time_out, net._time_out_scale, net._time_out_rot, net._time_out_shs):
+                h.weight.mul_(0.01)
+        res.append(_fused_step_run(fused, net=net, steps=2, P=6000, W=192, H=128, iteration=5000))
+    assert res[0][2] == res[1][2]
+    for x, y in zip(res[0][0] + res[0][1], res[1][0] + res[1][1]):
+        assert rel_l2(x, y) <= 1e-4
+
+
+def test_step_in_backward_rejects_second_producer():
+    """A second gradient for a parameter the block already stepped (a regulariser on _scaling: autograd sums its
+    gradient with the rasterizer's before the parameter's AccumulateGrad, after the rasterizer has run) would be
+    lost: it raises instead, whichever of the two was built first; outside the block the same loss trains."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    cam = synthetic_camera(128, 96).to(DEV)
+    for reg_first in (True, False):
+        pc = DeformableGaussians(make_gaussians(3000, 128, 96, seed=2, device=DEV), sh_degree=3)
+        opt = FusedAdam([{"params": [p], "lr": 1e-3} for p in pc.parameters()], lr=0.0, eps=1e-15)
+        reg = 1e-3 * pc._scaling.square().sum() if reg_first else None
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+        loss = out["render"].sum() + (reg if reg_first else 1e-3 * pc._scaling.square().sum())
+        with pytest.raises(RuntimeError, match="second gradient"):
+            with opt.step_in_backward():
+                loss.backward()
+        assert opt.flat.epilogue is None and not opt.flat.fused
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+        (out["render"].sum() + 1e-3 * pc._scaling.square().sum()).backward()
+        opt.allreduce_step(zero_grad=True)
+        assert all(bool(torch.isfinite(p).all()) for p in pc.parameters())
