@@ -584,7 +584,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
 
 int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
                       int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
-                      const gsd_sh_split* layout, void* stream) {
+                      const gsd_sh_split* layout, const gsd_adam_epilogue* adam, void* stream) {
     if (P < 0 || n_views < 0 || M < 1 || M < (D + 1) * (D + 1))
         return fail(GSD_ERR_ARG, "sh_grad_views: need P >= 0, n_views >= 0, M >= (D+1)^2");
     if (view_stride < 3 * (int64_t)P + 3) return fail(GSD_ERR_ARG, "sh_grad_views: view_stride < 3 P + 3");
@@ -595,6 +595,20 @@ int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const fl
     p.means3D = means3D; p.views = views; p.d_dc = d_dc; p.d_rest = d_rest; p.d_off = d_offset;
     p.accumulate = accumulate;
     set_sh_strides(p, layout, M);
+    if (adam && (adam->dc.param || adam->rest.param)) {
+        const bool contiguous = p.dc_sg == 3 && p.dc_se == 1 && p.rest_sg == 3LL * (M - 1) && p.rest_se == 1;
+        if (accumulate || M != 16 || !contiguous)
+            return fail(GSD_ERR_ARG, "sh_grad_views adam epilogue: needs accumulate 0, M = 16, contiguous pieces");
+        for (const gsd_adam_sink* k : {&adam->dc, &adam->rest})
+            if (k->param && (!k->exp_avg || !k->exp_avg_sq || k->step < 1))
+                return fail(GSD_ERR_ARG, "adam epilogue: a fused sink needs both moments and a step count >= 1");
+        p.adam.dc = adam_sink(adam->dc, adam->beta1, adam->beta2);
+        p.adam.rest = adam_sink(adam->rest, adam->beta1, adam->beta2);
+        p.adam.w1 = (float)(1.0 - adam->beta1);
+        p.adam.beta2 = (float)adam->beta2;
+        p.adam.omb2 = (float)(1.0 - adam->beta2);
+        p.adam.eps = (float)adam->eps;
+    }
     hipStream_t s = as_stream(stream);
     timed(kShViews, s, [&] { gsd::launch_sh_grad_views(p, s); });
     GSD_CHECK(false, s);

@@ -229,6 +229,7 @@ struct ShViewsParams {
     float *d_dc, *d_rest, *d_off;
     long long dc_sg, dc_se, rest_sg, rest_se;
     int accumulate;
+    AdamEpiDev adam;  // fused Adam epilogue for dc / rest (rows kernel, store mode), p == nullptr: off
 };
 void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);

@@ -945,8 +945,12 @@ __global__ __launch_bounds__(kShWave) void k_sh_grad_views_rows(ShViewsParams p)
         for (int k = 0; k < 3 * M; ++k) row[k] = k < 3 * nc ? acc[k] : 0.f;  // zero above the active degree
     }
     __syncthreads();
-    if (p.d_dc) sh_region_store<3, kAcc>(p.d_dc + (size_t)g0 * 3, rows, rows_lds, 0);
-    if (p.d_rest) sh_region_store<3 * (M - 1), kAcc>(p.d_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    if (!kAcc && p.adam.dc.p) sh_region_adam<3>(p.adam.dc, p.adam, (long long)g0 * 3, rows, rows_lds, 0);
+    else if (p.d_dc) sh_region_store<3, kAcc>(p.d_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    if (!kAcc && p.adam.rest.p)
+        sh_region_adam<3 * (M - 1)>(p.adam.rest, p.adam, (long long)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    else if (p.d_rest)
+        sh_region_store<3 * (M - 1), kAcc>(p.d_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
     if (p.d_off) sh_region_store<3 * M, kAcc>(p.d_off + (size_t)g0 * 3 * M, rows, rows_lds, 0);
 }
 

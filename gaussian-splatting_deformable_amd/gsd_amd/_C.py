@@ -248,9 +248,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot
 
 
-def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None, accumulate=False, layout=None):
+def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None, accumulate=False, layout=None,
+                  adam=None):
     """gsd_sh_grad_views: the SH gradient summed over the views whose rows views (n_views, view_stride) hold
-    [masked dL/dRGB (P*3) | campos (3) | pad] -> written into / added to the given sinks."""
+    [masked dL/dRGB (P*3) | campos (3) | pad] -> written into / added to the given sinks (or, for the pieces
+    ``adam`` (a _native.AdamEpilogue) names, their Adam step applied in place)."""
     lib = _native.load()
     dev = means3D.device
     if views.dim() != 2 or not views.is_contiguous() or views.dtype != torch.float32 or views.device != dev:
@@ -260,7 +262,8 @@ def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None
         _native.check(lib.gsd_sh_grad_views(int(P), int(D), int(M), int(views.size(0)), _ptr(m), _ptr(views),
                                             int(views.size(1)), _ptr(d_dc), _ptr(d_rest), _ptr(d_offset),
                                             int(bool(accumulate)),
-                                            None if layout is None else ctypes.byref(layout.c), _stream(dev)))
+                                            None if layout is None else ctypes.byref(layout.c),
+                                            None if adam is None else ctypes.byref(adam), _stream(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -74,7 +74,7 @@ SIGNATURES = {
     "gsd_rasterize_forward_bin": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "gsd_rasterize_forward_render": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gsd_rasterize_forward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _sz, _vp, _vp, ctypes.POINTER(_i64), _vp]),
-    "gsd_sh_grad_views": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "gsd_sh_grad_views": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
     "gsd_rasterize_backward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),

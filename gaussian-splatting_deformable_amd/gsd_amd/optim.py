@@ -188,13 +188,14 @@ class FusedAdam(torch.optim.Optimizer):
         self.allreduce_step(zero_grad=True)
         self.flat.fused = set()
 
-    def fuse(self, named, epi=None):
+    def fuse(self, named, epi=None, summed=False):
         """Called by the rasterizer backward inside ``step_in_backward`` for sinks it is about to store into:
         ``named`` maps gsd_adam_epilogue slots ("dc", "rest", "xyz", "scaling", "rotation", "opacity") to
         parameters.  Counts their step now and returns ``epi`` (a _native.AdamEpilogue, created when None) with
         their slots filled -- or ``epi`` unchanged when the step cannot be fused here (world size > 1, a
-        coefficient-major slab, a parameter this optimizer does not own or has already stepped)."""
-        if self.flat.epilogue is not self or data_parallel_world() != 1 or self.coef_major:
+        coefficient-major slab, a parameter this optimizer does not own or has already stepped).  ``summed``: the
+        caller's gradient is already the sum over every rank (the exchanged SH views), so any world size fuses."""
+        if self.flat.epilogue is not self or (data_parallel_world() != 1 and not summed) or self.coef_major:
             return epi
         index = {id(p): i for i, p in enumerate(self._params)}
         if any(id(p) not in index or id(p) in self.flat.fused for p in named.values()):

@@ -249,8 +249,15 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
         parts = [torch.empty(stride, dtype=torch.float32) for _ in range(world)]
         dist.all_gather(parts, row.cpu())
         views.copy_(torch.stack(parts))
+    epi = None
+    owner = FusedAdam.fused_owner(ctx.params) if not acc else None
+    if owner is not None and f_dc.is_contiguous() and f_rest.is_contiguous():
+        epi = owner.fuse({"dc": f_dc, "rest": f_rest}, summed=True)   # every view's sum: final on every rank
     _C.sh_grad_views(rs.sh_degree, means3D, views, P, 1 + int(f_rest.size(1)), d_dc=sinks[0], d_rest=sinks[1],
-                     accumulate=acc, layout=split)
+                     accumulate=acc, layout=split, adam=epi)
+    if epi is not None:
+        for p in (f_dc, f_rest):
+            torch.autograd.graph.increment_version(p)
     parallel.mark_reduced(ctx.params)
     return g_m2d, g_op, g_m3d, g_sc, g_rot
 

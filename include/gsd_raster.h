@@ -212,10 +212,13 @@ int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, co
  *   dL/dsh_k[c] = sum_v B_k(normalize(means3D - campos_v)) * d_rgb_v[c]    (backward.cu:20-139 per view)
  * views: n_views rows of view_stride floats, row v = [d_rgb_v (P*3) | campos_v (3)].  means3D (P,3) must be
  * the positions every view rendered (the same on every rank).  Sinks as in gsd_sh_split (any may be NULL);
- * accumulate 0 stores every entry (coefficients above degree D as zeros), 1 adds. */
+ * accumulate 0 stores every entry (coefficients above degree D as zeros), 1 adds.  adam (ABI 8): NULL, or a
+ * gsd_adam_epilogue whose dc / rest sinks are fused -- the assembled SH gradient is final here (every view
+ * summed), so with accumulate 0, M = 16 and contiguous layouts the Adam step of those pieces is applied in
+ * place instead of storing d_dc / d_rest (its other slots are ignored). */
 int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
                       int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
-                      const gsd_sh_split* layout, void* stream);
+                      const gsd_sh_split* layout, const gsd_adam_epilogue* adam, void* stream);
 
 /* Near-plane visibility test (auxiliary.h:139-164): present[i] = 1/0. */
 int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -96,8 +96,12 @@ for it in range(2):
         if it == 0:
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[4], RANK=str(rank), WORLD_SIZE=str(world))
             dist.init_process_group("gloo", rank=rank, world_size=world)
-        step(pc, 4.0 * rank + it)
-        opt.allreduce_step(zero_grad=True, bucket_floats=50_000)   # several buckets, partial ones included
+        if len(sys.argv) > 5 and sys.argv[5] == "fused":   # SH pieces stepped inside sh_grad_views
+            with opt.step_in_backward():
+                step(pc, 4.0 * rank + it)
+        else:
+            step(pc, 4.0 * rank + it)
+            opt.allreduce_step(zero_grad=True, bucket_floats=50_000)   # several buckets, partial ones included
     else:                      # the single-process reference: both views into one slab, then a plain step
         for r in range(world):
             step(pc, 4.0 * r + it)
@@ -108,16 +112,19 @@ torch.save({"p": opt.param_slab.cpu(), "m": opt.exp_avg.cpu(), "v": opt.exp_avg_
 '''
 
 
-def test_two_ranks_overlapped_allreduce_adam_matches_one_process(tmp_path):
+@pytest.mark.parametrize("mode", ["plain", "fused"])
+def test_two_ranks_overlapped_allreduce_adam_matches_one_process(tmp_path, mode):
     """FusedAdam.allreduce_step (bucketed asynchronous all-reduce, Adam per bucket as it arrives, the exchanged
     SH gradient first) over two gloo ranks == one process summing both views and taking a plain Adam step;
-    two steps, so the second runs on moments the first left."""
+    two steps, so the second runs on moments the first left.  "fused": FusedAdam.step_in_backward, whose SH
+    pieces take their Adam step inside gsd_sh_grad_views (the assembled gradient is final on every rank) and
+    whose other parameters are all-reduced and stepped on leaving the block."""
     script = tmp_path / "worker_adam.py"
     script.write_text("ROOT = %r\n" % ROOT + WORKER_ADAM)
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    port = str(29800 + os.getpid() % 150)
-    procs = [subprocess.Popen([sys.executable, str(script), str(r), "2", str(tmp_path / f"a{r}.pt"), port], env=env)
-             for r in range(2)]
+    port = str(29800 + os.getpid() % 150 + (7 if mode == "fused" else 0))
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), "2", str(tmp_path / f"a{r}.pt"), port, mode],
+                              env=env) for r in range(2)]
     rcs = [p.wait(timeout=300) for p in procs]
     assert rcs == [0, 0]
     ref = subprocess.run([sys.executable, str(script), "-1", "2", str(tmp_path / "aref.pt"), port], env=env,
