@@ -479,7 +479,8 @@ def test_step_in_backward_with_offset_network():
 def test_step_in_backward_rejects_second_producer():
     """A second gradient for a parameter the block already stepped (a regulariser on _scaling: autograd sums its
     gradient with the rasterizer's before the parameter's AccumulateGrad, after the rasterizer has run) would be
-    lost: it raises instead, whichever of the two was built first; outside the block the same loss trains."""
+    lost: it raises instead, whichever of the two was built first -- autograd's saved-tensor version check (the
+    fused kernel bumps the parameters' versions) or the FlatGrads guard; outside the block the loss trains."""
     from gsd_amd import DeformableGaussians, default_pipe, render
     from gsd_amd.camera import synthetic_camera
     from gsd_amd.optim import FusedAdam
@@ -491,7 +492,7 @@ def test_step_in_backward_rejects_second_producer():
         reg = 1e-3 * pc._scaling.square().sum() if reg_first else None
         out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
         loss = out["render"].sum() + (reg if reg_first else 1e-3 * pc._scaling.square().sum())
-        with pytest.raises(RuntimeError, match="second gradient"):
+        with pytest.raises(RuntimeError, match="second gradient|modified by an inplace operation"):
             with opt.step_in_backward():
                 loss.backward()
         assert opt.flat.epilogue is None and not opt.flat.fused
