@@ -80,8 +80,8 @@ __device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t
 // the extra test than it saves).  Returns the count.
 // Slots below t_min are skipped too (the backward's last-contributor bound).
 template <bool kExact, int RW = 8, int RH = 8>
-__device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, const float2* __restrict__ s_xy,
-                                            const float4* __restrict__ s_co, uint8_t* __restrict__ s_list, int n,
+__device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
+                                            const float4* __restrict__ s_bo, uint8_t* __restrict__ s_list, int n,
                                             float qx0, float qy0, int lane, int t_min = 0) {
     int m = 0;
 #pragma unroll
@@ -92,12 +92,14 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
             const float4 bx = s_box[t];
             hit = bx.y >= qx0 && bx.x <= qx0 + (float)(RW - 1) && bx.w >= qy0 && bx.z <= qy0 + (float)(RH - 1);
             if (kExact && hit) {
-                const float4 co = s_co[t];
+                const float4 pc = s_pc[t];
+                const float2 bo = *reinterpret_cast<const float2*>(&s_bo[t]);
+                const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
                 const float det = co.x * co.z - co.y * co.y;
                 // alpha >= 1/255  <=>  Q <= 2 ln(255 o); slack: 0.1 % + 0.05 (v_exp / v_log rounding)
                 const float tq = 2.0f * 0.69314718f * __builtin_amdgcn_logf(255.0f * co.w) * 1.001f + 0.05f;
                 if (co.x > 0.f && co.z > 0.f && det > 0.f)
-                    hit = ellipse_meets_rect(s_xy[t], co, tq, qx0, qx0 + (float)(RW - 1), qy0,
+                    hit = ellipse_meets_rect(make_float2(pc.x, pc.y), co, tq, qx0, qx0 + (float)(RW - 1), qy0,
                                              qy0 + (float)(RH - 1));
             }
         }
@@ -201,13 +203,21 @@ __device__ __forceinline__ float gauss_exp(float power) {
     return __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
 #endif
 }
-__device__ __forceinline__ float record_alpha(float2 xy, float4 co, float pxf, float pyf, float& G, float& dx,
-                                              float& dy) {
-    dx = xy.x - pxf;
-    dy = xy.y - pyf;
-    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+// The render kernels stage a record as pc = (mx, my, -a/2, -c/2) and bo = (b, o): with the halves folded into
+// the staged conic, (-a/2 dx) dx + (-c/2 dy) dy is exactly -0.5f * (a dx dx + c dy dy) (scaling by a power of
+// two commutes with rounding), so power below has the reference's bits with one multiply fewer per pair.
+__device__ __forceinline__ float4 stage_pc(float2 xy, float4 co) {
+    return make_float4(xy.x, xy.y, -0.5f * co.x, -0.5f * co.z);
+}
+// Returns min(0.99, o G); the record is skipped where power > 0 (`keep` false) or alpha < 1/255 -- the
+// callers fold both tests into their take / valid masks (NaN power passes, as in the reference).
+__device__ __forceinline__ float record_alpha(float4 pc, float2 bo, float pxf, float pyf, float& G, bool& keep) {
+    const float dx = pc.x - pxf;
+    const float dy = pc.y - pyf;
+    const float power = (pc.z * dx * dx + pc.w * dy * dy) - bo.x * dx * dy;
     G = gauss_exp(power);
-    return power > 0.0f ? 0.0f : fminf(0.99f, co.w * G);
+    keep = !(power > 0.0f);
+    return fminf(0.99f, bo.y * G);
 }
 
 // 1/d from v_rcp_f32 (1 ulp) plus one Newton step: ~0.5 ulp in 3 VALU ops instead of the ~10 of the
@@ -220,7 +230,16 @@ __device__ __forceinline__ float fast_recip(float d) {
 // Record-major accumulation of the backward (k_render_bwd phase 2): pixel I of the lane's quad contributes
 // v = G dL/dalpha and w = alpha T (read from LDS) with its dL/dpixel (DPP quad broadcast from lane I).
 struct RecordSums {
-    float S0 = 0.f, S1 = 0.f, S3 = 0.f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+    float S0, S1, S3, C0, C1, C2;
+    __device__ __forceinline__ RecordSums(float2 vw, float dx, float3 d) {
+#pragma clang fp contract(fast)
+        S0 = vw.x;
+        S1 = vw.x * dx;
+        S3 = S1 * dx;
+        C0 = vw.y * d.x;
+        C1 = vw.y * d.y;
+        C2 = vw.y * d.z;
+    }
     __device__ __forceinline__ void add(float2 vw, float dx, float3 d) {
 #pragma clang fp contract(fast)
         S0 += vw.x;
@@ -256,9 +275,10 @@ __device__ __forceinline__ TileGeom tile_geom(int num_tiles, int grid_x, int W, 
     return g;
 }
 
-__global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
-    __shared__ float2 s_xy[kTilePix];
-    __shared__ float4 s_co[kTilePix];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_fwd(RenderParams p) {
+    // staged records (stage_pc); (b, o) at an 8-B stride keeps the LDS at 8 workgroups per CU
+    __shared__ float4 s_pc[kTilePix];
+    __shared__ float2 s_bo[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float4 s_box[kTilePix];
     __shared__ __attribute__((aligned(4))) uint8_t s_list[4][kFwdGroups][kTilePix];
@@ -283,8 +303,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
             const uint32_t g = p.point_list[k];
             const float2 xy = p.means2D[g];
             const float4 co = p.conic_opacity[g];
-            s_xy[tid] = xy;
-            s_co[tid] = co;
+            s_pc[tid] = stage_pc(xy, co);
+            s_bo[tid] = make_float2(co.y, co.w);
             s_rgb[tid] = p.rgb[g];
             s_box[tid] = alpha_box(xy, co);
         }
@@ -296,23 +316,24 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
             if (!__ballot(!done)) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
             float a[kBatch];
+            bool keep[kBatch];
             int slot[kBatch];
             static_assert(kBatch == 4, "one LDS word of list entries per batch");
             const uint32_t w4 = *reinterpret_cast<const uint32_t*>(list + j0);
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
-                slot[u] = list_slot(w4, u, j0, mine);
-                float G, dx, dy;
-                a[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, G, dx, dy);
+                slot[u] = list_slot(w4, u, j0, mine);  // past the list: slot 0, staged, so its colour is finite
+                float G;
+                a[u] = record_alpha(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, G, keep[u]);
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
             // One wave-uniform branch per record (skipped when no lane takes it), the lane decisions as selects:
             // 0.300 -> 0.289 ms against a divergent branch per test (each an exec-mask save / restore); fully
-            // branch-free (no skip) was slower, 0.335 ms.  Same float operations, so the same image bits.
+            // branch-free (no skip) was slower, 0.335 ms.
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 if (j0 + u >= m) break;
-                bool take = !done & (j0 + u < mine) & (a[u] >= 1.0f / 255.0f);
+                bool take = !done & (j0 + u < mine) & keep[u] & (a[u] >= 1.0f / 255.0f);
                 if (!__ballot(take)) continue;
                 const float alpha = a[u];
                 const float test_T = T * (1 - alpha);
@@ -320,10 +341,15 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
                 done |= fin;
                 take &= !fin;
                 const float4 c = s_rgb[slot[u]];
-                const float c0 = C0 + c.x * alpha * T, c1 = C1 + c.y * alpha * T, c2 = C2 + c.z * alpha * T;
-                C0 = take ? c0 : C0;
-                C1 = take ? c1 : C1;
-                C2 = take ? c2 : C2;
+                // C += c alpha T (forward.cu:356-357) as one FMA per channel on the weight alpha T, selected to 0
+                // where the lane does not take the record (C + c * 0 == C for the finite colours of staged records;
+                // a non-finite colour would now poison C where the reference skips it): 5 VALU ops instead of 12.  Rounds
+                // differently from ((c alpha) T) by an ulp per step (image tolerance); T -- all the
+                // backward reads -- keeps the reference's operations.
+                const float wgt = take ? alpha * T : 0.f;
+                C0 = fmaf(c.x, wgt, C0);
+                C1 = fmaf(c.y, wgt, C1);
+                C2 = fmaf(c.z, wgt, C2);
                 T = take ? test_T : T;
                 last_contributor = take ? (uint32_t)(i * kTilePix + slot[u] + 1) : last_contributor;
             }
@@ -342,13 +368,14 @@ __global__ __launch_bounds__(256) void k_render_fwd(RenderParams p) {
 
 __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
-    __shared__ float2 s_xy[kTilePix];
-    __shared__ float4 s_co[kTilePix];
+    // staged records (stage_pc), all at a 16-B stride: one LDS address per record serves the three reads
+    __shared__ float4 s_pc[kTilePix];
+    __shared__ float4 s_bo[kTilePix];
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float s_acc[9][kTilePix + 1];  // +1: a record's nine sums sit in nine different banks
     __shared__ __attribute__((aligned(4))) uint8_t s_list[4][kTilePix];
     // the alpha boxes are read only by the compaction, the (G dL/dalpha, alpha T) hand-off only after it (a
-    // barrier apart): one region, 30 KB of LDS per workgroup in all -> 5 workgroups per CU
+    // barrier apart): one region, 31.2 KB of LDS per workgroup in all -> 5 workgroups per CU
     __shared__ union {
         float4 box[kTilePix];
         float2 qa[4][kBwdGroup][65];  // per wave: per record and pixel; +1 pad
@@ -407,8 +434,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float2 xy = p.means2D[g];
             const float4 co = p.conic_opacity[g];
             s_id[tid] = g;
-            s_xy[tid] = xy;
-            s_co[tid] = co;
+            s_pc[tid] = stage_pc(xy, co);
+            s_bo[tid] = make_float4(co.y, co.w, 0.f, 0.f);
             s_rgb[tid] = p.rgb[g];
             s_box[tid] = alpha_box(xy, co);
         }
@@ -418,8 +445,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         const int n = min(kTilePix, toDo);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
-        const int m = wave_compact<true>(s_box, s_xy, s_co, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
+        const int m = wave_compact<true>(s_box, s_pc, s_bo, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
         lds_barrier();  // every wave is done with s_box before s_u.qa is written
+        // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor
+        const int slot_min = front_base - last_contributor;  // slot t counts for this pixel iff t > slot_min
         for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
             // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
             // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
@@ -437,20 +466,23 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                     continue;
                 }
                 float Gs[kBwdBatch], As[kBwdBatch];
+                bool keep[kBwdBatch];
                 int slot[kBwdBatch];
                 static_assert(kBwdBatch == 4, "one LDS word of list entries per batch");
-                w4 = *reinterpret_cast<const uint32_t*>(list + jb);
+                // the list is the wave's, so its entries are wave-uniform: read once into a scalar register, the
+                // slot extraction and the bounds select run on the scalar unit, and each record costs one vector
+                // move for its LDS address (shared by its three reads)
+                w4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(list + jb));
 #pragma unroll
                 for (int u = 0; u < kBwdBatch; ++u) {
                     slot[u] = list_slot(w4, u, jb, m);
-                    float dx, dy;
-                    As[u] = record_alpha(s_xy[slot[u]], s_co[slot[u]], pxf, pyf, Gs[u], dx, dy);
+                    As[u] = record_alpha(s_pc[slot[u]], *reinterpret_cast<const float2*>(&s_bo[slot[u]]), pxf, pyf,
+                                         Gs[u], keep[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < kBwdBatch; ++u) {
 #pragma clang fp contract(fast)
-                    const bool valid = (jb + u < m) & (front_base - slot[u] < last_contributor) &
-                                       (As[u] >= 1.0f / 255.0f);
+                    const bool valid = (jb + u < m) & (slot[u] > slot_min) & keep[u] & (As[u] >= 1.0f / 255.0f);
                     any |= valid;
                     const float alpha = valid ? As[u] : 0.f;
                     const float G = valid ? Gs[u] : 0.f;
@@ -474,15 +506,15 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const int r = lane & 3, grp = lane >> 2;
             static_assert(kBwdGroup == kBwdBatch, "phase 2 reads the group's slots from phase 1's list word");
             const int rs = list_slot(w4, r, j0, m);
-            const float2 mxy = s_xy[rs];
+            const float2 mxy = make_float2(s_pc[rs].x, s_pc[rs].y);
             const float px0 = tg.qx0 + (float)(4 * (grp & 1));
             float dxi[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) dxi[i] = mxy.x - (px0 + (float)i);
             const float dy = mxy.y - (tg.qy0 + (float)(grp >> 1));
-            RecordSums acc;
+            RecordSums acc(qa[r][4 * grp], dxi[0], dpq[0]);  // started from pixel 0: no adds to zero
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc.add(qa[r][4 * grp + i], dxi[i], dpq[i]);
+            for (int i = 1; i < 4; ++i) acc.add(qa[r][4 * grp + i], dxi[i], dpq[i]);
             const float S0 = acc.S0, S1 = acc.S1, S3 = acc.S3, C0 = acc.C0, C1 = acc.C1, C2 = acc.C2;
             // the nine sums in s_acc order (kRecMean2D.. moments, opacity, colour), summed over the 16 groups
             // g (lane bits 5, 4 transposed; bits 3, 2 by row rotations): afterwards lane 4 g + r with bits 2-3
@@ -501,7 +533,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         }
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
-            const float4 co = s_co[tid];
+            const float4 pc = s_pc[tid];
+            const float2 bo = *reinterpret_cast<const float2*>(&s_bo[tid]);
+            const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
             const float o = co.w;  // the moments were summed over G dL/dalpha; q = o G dL/dalpha
             const float m0 = s_acc[0][tid] * o, m1 = s_acc[1][tid] * o;
             s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;

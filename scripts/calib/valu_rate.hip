@@ -7,7 +7,8 @@
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int MODE>
-__global__ __launch_bounds__(64) void k(float* out, int iters, float a) {
+__global__ __launch_bounds__(64) void k(float* out, int iters, float a, unsigned long long* clk) {
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     float x[8];
     f2 y[4];
     for (int i = 0; i < 8; ++i) x[i] = threadIdx.x * 0.001f + i;
@@ -43,8 +44,14 @@ __global__ __launch_bounds__(64) void k(float* out, int iters, float a) {
     for (int i = 0; i < 8; ++i) s += x[i];
     for (int i = 0; i < 4; ++i) s += y[i].x + y[i].y + (float)(sv[i] & 1);
     out[blockIdx.x * 64 + threadIdx.x] = s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // shader clock: s_memtime ticks per 100-MHz s_memrealtime tick
+        clk[0] = __builtin_amdgcn_s_memtime() - c0;
+        clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
 }
 
+static unsigned long long* g_clk;
+static double g_ghz = 2.4;
 template <int MODE>
 float run(float* out, int blocks, int iters) {
     hipEvent_t e0, e1;
@@ -53,17 +60,21 @@ float run(float* out, int blocks, int iters) {
     float ms = 0;
     for (int rep = 0; rep < 2; ++rep) {
         (void)hipEventRecord(e0);
-        hipLaunchKernelGGL(k<MODE>, dim3(blocks), dim3(64), 0, 0, out, iters, 0.999f);
+        hipLaunchKernelGGL(k<MODE>, dim3(blocks), dim3(64), 0, 0, out, iters, 0.999f, g_clk);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         (void)hipEventElapsedTime(&ms, e0, e1);
     }
+    unsigned long long c[2];
+    (void)hipMemcpy(c, g_clk, sizeof(c), hipMemcpyDeviceToHost);
+    g_ghz = c[1] ? (double)c[0] / (double)c[1] * 0.1 : 2.4;
     return ms;
 }
 
 int main() {
     float* out;
     (void)hipMalloc(&out, 1 << 26);
+    (void)hipMalloc(&g_clk, 16);
     const int iters = 4096;
     const char* names[14] = {"v_fma_f32", "v_exp_f32", "v_add_f32_dpp", "v_pk_fma_f32", "v_permlane32_swap",
                              "v_rcp_f32", "v_mul_f32", "v_cndmask_b32 vcc", "v_cndmask_b32 sgpr", "v_max_f32",
@@ -89,7 +100,8 @@ int main() {
                 default: ms = run<13>(out, blocks, iters); break;
             }
             const double n_instr = (double)wps * iters * (mode == 3 || mode == 4 ? 4 : 8);
-            printf("%-20s waves/SIMD %d: %.2f cycles per wave-instruction per SIMD (%.3f ms)\n", names[mode], wps,
+            printf("%-20s waves/SIMD %d: %.2f cycles per wave-instruction per SIMD at the measured %.2f GHz "
+                   "(%.2f at 2.4 GHz; %.3f ms)\n", names[mode], wps, ms * 1e-3 * g_ghz * 1e9 / n_instr, g_ghz,
                    ms * 1e-3 * 2.4e9 / n_instr, ms);
         }
     }
