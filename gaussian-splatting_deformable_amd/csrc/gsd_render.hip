@@ -26,6 +26,8 @@
 // one record over 4 pixels each and a short transposed butterfly finishes it;
 // the sums go to LDS accumulators and, after each 256-record batch, to HBM as
 // one set of global atomics per (Gaussian, tile) instance.
+#include <type_traits>
+
 #include "gsd_kernels.h"
 
 namespace gsd {
@@ -224,33 +226,12 @@ __device__ __forceinline__ float record_alpha(float4 pc, float2 bo, float pxf, f
 // correctly rounded division sequence.
 __device__ __forceinline__ float fast_recip(float d) {
     float r = __builtin_amdgcn_rcpf(d);
+#ifdef GSD_BARE_RCP
+    return r;
+#else
     return fmaf(fmaf(-d, r, 1.0f), r, r);
+#endif
 }
-
-// Record-major accumulation of the backward (k_render_bwd phase 2): pixel I of the lane's quad contributes
-// v = G dL/dalpha and w = alpha T (read from LDS) with its dL/dpixel (DPP quad broadcast from lane I).
-struct RecordSums {
-    float S0, S1, S3, C0, C1, C2;
-    __device__ __forceinline__ RecordSums(float2 vw, float dx, float3 d) {
-#pragma clang fp contract(fast)
-        S0 = vw.x;
-        S1 = vw.x * dx;
-        S3 = S1 * dx;
-        C0 = vw.y * d.x;
-        C1 = vw.y * d.y;
-        C2 = vw.y * d.z;
-    }
-    __device__ __forceinline__ void add(float2 vw, float dx, float3 d) {
-#pragma clang fp contract(fast)
-        S0 += vw.x;
-        const float t = vw.x * dx;
-        S1 += t;
-        S3 = fmaf(t, dx, S3);
-        C0 = fmaf(vw.y, d.x, C0);
-        C1 = fmaf(vw.y, d.y, C1);
-        C2 = fmaf(vw.y, d.z, C2);
-    }
-};
 
 struct TileGeom {
     int tile, wave, lane, px, py;
@@ -422,9 +403,14 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     float adot = 0.f;  // accum_rec . dL/dpixel (accum_rec with last_color / last_alpha folded in)
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float kbg = -T_final * bg_dot;
+    const bool any_bg = __ballot(kbg != 0.f) != 0;  // wave-uniform
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
+    // phase 2: tile-local origin of the lane's half-row of four pixels; the flush's tile origin
+    const float ph2_ox = (float)(8 * (tg.wave & 1) + 4 * ((lane >> 2) & 1));
+    const float ph2_oy = (float)(8 * (tg.wave >> 1) + (lane >> 3));
+    const float tile_x0 = (float)((tg.tile % p.grid_x) * kTileX), tile_y0 = (float)((tg.tile / p.grid_x) * kTileY);
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         lds_barrier();
@@ -449,100 +435,126 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         lds_barrier();  // every wave is done with s_box before s_u.qa is written
         // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor
         const int slot_min = front_base - last_contributor;  // slot t counts for this pixel iff t > slot_min
-        for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
-            // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
-            // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
-            // v = G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
-            // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
-            // needed from the lane.
-            bool any = false;
-            uint32_t w4 = 0;  // the group's four list entries (kBwdGroup == kBwdBatch: one sub-batch)
-#pragma unroll
-            for (int sb = 0; sb < kBwdGroup / kBwdBatch; ++sb) {
-                const int jb = j0 + sb * kBwdBatch;
-                if (sb > 0 && jb >= m) {  // wave-uniform: the tail of the list
-#pragma unroll
-                    for (int u = 0; u < kBwdBatch; ++u) qa[sb * kBwdBatch + u][lane] = make_float2(0.f, 0.f);
-                    continue;
+        // the group loop twice: with the background term of dL/dalpha and, where it is 0 for every pixel of
+        // the wave (a black background: the default of train.py), without its multiply-add
+        auto walk = [&](auto with_bg) {
+            constexpr bool kBg = decltype(with_bg)::value;
+            for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
+                // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
+                // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
+                // v = G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
+                // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
+                // needed from the lane.
+                bool any = false;
+                uint32_t w4 = 0;  // the group's four list entries (kBwdGroup == kBwdBatch: one sub-batch)
+    #pragma unroll
+                for (int sb = 0; sb < kBwdGroup / kBwdBatch; ++sb) {
+                    const int jb = j0 + sb * kBwdBatch;
+                    if (sb > 0 && jb >= m) {  // wave-uniform: the tail of the list
+    #pragma unroll
+                        for (int u = 0; u < kBwdBatch; ++u) qa[sb * kBwdBatch + u][lane] = make_float2(0.f, 0.f);
+                        continue;
+                    }
+                    float Gs[kBwdBatch], As[kBwdBatch];
+                    bool keep[kBwdBatch];
+                    int slot[kBwdBatch];
+                    static_assert(kBwdBatch == 4, "one LDS word of list entries per batch");
+                    // the list is the wave's, so its entries are wave-uniform: read once into a scalar register, the
+                    // slot extraction and the bounds select run on the scalar unit, and each record costs one vector
+                    // move for its LDS address (shared by its three reads)
+                    w4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(list + jb));
+    #pragma unroll
+                    for (int u = 0; u < kBwdBatch; ++u) {
+                        slot[u] = list_slot(w4, u, jb, m);
+                        As[u] = record_alpha(s_pc[slot[u]], *reinterpret_cast<const float2*>(&s_bo[slot[u]]), pxf, pyf,
+                                             Gs[u], keep[u]);
+                    }
+    #pragma unroll
+                    for (int u = 0; u < kBwdBatch; ++u) {
+    #pragma clang fp contract(fast)
+                        const bool valid = (jb + u < m) & (slot[u] > slot_min) & keep[u] & (As[u] >= 1.0f / 255.0f);
+                        any |= valid;
+                        const float alpha = valid ? As[u] : 0.f;
+                        const float G = valid ? Gs[u] : 0.f;
+                        const float inv1ma = fast_recip(1.f - alpha);
+                        T = T * inv1ma;  // backward.cu:503 (T recovered by division)
+                        const float4 c = s_rgb[slot[u]];
+                        const float cd = fmaf(c.z, dpix2, fmaf(c.y, dpix1, c.x * dpix0));
+                        const float diff = cd - adot;
+                        // backward.cu:512-529 (kbg = 0: fmaf(diff, T, -0) is diff * T, bit for bit)
+                        const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
+                        qa[sb * kBwdBatch + u][lane] = make_float2(G * dL_dalpha, alpha * T);
+                        adot = fmaf(alpha, diff, adot);
+                    }
                 }
-                float Gs[kBwdBatch], As[kBwdBatch];
-                bool keep[kBwdBatch];
-                int slot[kBwdBatch];
-                static_assert(kBwdBatch == 4, "one LDS word of list entries per batch");
-                // the list is the wave's, so its entries are wave-uniform: read once into a scalar register, the
-                // slot extraction and the bounds select run on the scalar unit, and each record costs one vector
-                // move for its LDS address (shared by its three reads)
-                w4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(list + jb));
-#pragma unroll
-                for (int u = 0; u < kBwdBatch; ++u) {
-                    slot[u] = list_slot(w4, u, jb, m);
-                    As[u] = record_alpha(s_pc[slot[u]], *reinterpret_cast<const float2*>(&s_bo[slot[u]]), pxf, pyf,
-                                         Gs[u], keep[u]);
+                if (!__ballot(any)) continue;  // wave-uniform: no pixel took any of these records
+                wave_lds_handoff();
+                // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
+                // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i sits at tile-local
+                // (ox + i, oy), ox = 8 (wave & 1) + 4 (g & 1), oy = 8 (wave >> 1) + (g >> 1).  The lane sums raw
+                // moments of v in tile-local pixel coordinates -- S0 = sum v, Mx = sum v x, Mxx = sum v x^2 and the
+                // y moments from its constant oy -- and C = sum w dL/dpixel; the flush turns them into the
+                // mean-centred sums of backward.cu:545-554 (sum v dx = (mx - x0) S0 - Mx, ...).  No record data
+                // is read here, and the in-row sums use the constant offsets i: 19 VALU ops for the quad's four
+                // pixels instead of 27 plus 9 for the per-record offsets.
+                const int r = lane & 3, grp = lane >> 2;
+                static_assert(kBwdGroup == kBwdBatch, "phase 2 reads the group's slots from phase 1's list word");
+                const float2 q0 = qa[r][4 * grp], q1 = qa[r][4 * grp + 1], q2 = qa[r][4 * grp + 2],
+                             q3 = qa[r][4 * grp + 3];
+                float S0, Mx, Mxx, My, Mxy, Myy, C0, C1, C2;
+                {
+    #pragma clang fp contract(fast)
+                    S0 = (q0.x + q1.x) + (q2.x + q3.x);
+                    const float X1 = fmaf(3.f, q3.x, fmaf(2.f, q2.x, q1.x));  // sum v i
+                    const float X2 = fmaf(9.f, q3.x, fmaf(4.f, q2.x, q1.x));  // sum v i^2
+                    Mx = fmaf(ph2_ox, S0, X1);
+                    Mxx = fmaf(ph2_ox, Mx + X1, X2);                            // ox^2 S0 + 2 ox X1 + X2
+                    My = ph2_oy * S0;
+                    Myy = ph2_oy * My;
+                    Mxy = ph2_oy * Mx;
+                    C0 = fmaf(q3.y, dpq[3].x, fmaf(q2.y, dpq[2].x, fmaf(q1.y, dpq[1].x, q0.y * dpq[0].x)));
+                    C1 = fmaf(q3.y, dpq[3].y, fmaf(q2.y, dpq[2].y, fmaf(q1.y, dpq[1].y, q0.y * dpq[0].y)));
+                    C2 = fmaf(q3.y, dpq[3].z, fmaf(q2.y, dpq[2].z, fmaf(q1.y, dpq[1].z, q0.y * dpq[0].z)));
                 }
-#pragma unroll
-                for (int u = 0; u < kBwdBatch; ++u) {
-#pragma clang fp contract(fast)
-                    const bool valid = (jb + u < m) & (slot[u] > slot_min) & keep[u] & (As[u] >= 1.0f / 255.0f);
-                    any |= valid;
-                    const float alpha = valid ? As[u] : 0.f;
-                    const float G = valid ? Gs[u] : 0.f;
-                    const float inv1ma = fast_recip(1.f - alpha);
-                    T = T * inv1ma;  // backward.cu:503 (T recovered by division)
-                    const float4 c = s_rgb[slot[u]];
-                    const float cd = fmaf(c.z, dpix2, fmaf(c.y, dpix1, c.x * dpix0));
-                    const float diff = cd - adot;
-                    const float dL_dalpha = fmaf(diff, T, kbg * inv1ma);  // backward.cu:512-529
-                    qa[sb * kBwdBatch + u][lane] = make_float2(G * dL_dalpha, alpha * T);
-                    adot = fmaf(alpha, diff, adot);
+                // the nine sums in s_acc order, summed over the 16 groups g (lane bits 5, 4 transposed; bits 3, 2
+                // by row rotations): afterwards lane 4 g + r with bits 2-3 clear holds record r's total of quantity
+                // (bit 5) + 2 (bit 4) [+ 4 for c1, 8 for c2]
+                const float c0 = sum4(sum8(pair16(pair32(Mx, My), pair32(Mxx, Mxy))));
+                const float c1 = sum4(sum8(pair16(pair32(Myy, S0), pair32(C0, C1))));
+                const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
+                const int rs = list_slot(w4, r, j0, m);
+                wave_lds_handoff();  // phase-1 writes of the next group must stay behind these reads
+                if (!(lane & 12) && j0 + r < m) {
+                    const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
+                    atomicAdd(&s_acc[qk][rs], c0);
+                    atomicAdd(&s_acc[4 + qk][rs], c1);
+                    if (qk == 0) atomicAdd(&s_acc[8][rs], c2);
                 }
             }
-            if (!__ballot(any)) continue;  // wave-uniform: no pixel took any of these records
-            wave_lds_handoff();
-            // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
-            // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i is
-            // (qx0 + 4 (g & 1) + i, qy0 + (g >> 1)): dx = mx - px runs over i, dy = my - py is the lane's
-            // constant.  Sums: S0 = sum v, S1 = sum v dx, S3 = sum v dx^2, C = sum w dL/dpixel; the dy
-            // moments follow as dy S0, dy S1, dy^2 S0 (backward.cu:545-554 expanded over pixels).
-            const int r = lane & 3, grp = lane >> 2;
-            static_assert(kBwdGroup == kBwdBatch, "phase 2 reads the group's slots from phase 1's list word");
-            const int rs = list_slot(w4, r, j0, m);
-            const float2 mxy = make_float2(s_pc[rs].x, s_pc[rs].y);
-            const float px0 = tg.qx0 + (float)(4 * (grp & 1));
-            float dxi[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dxi[i] = mxy.x - (px0 + (float)i);
-            const float dy = mxy.y - (tg.qy0 + (float)(grp >> 1));
-            RecordSums acc(qa[r][4 * grp], dxi[0], dpq[0]);  // started from pixel 0: no adds to zero
-#pragma unroll
-            for (int i = 1; i < 4; ++i) acc.add(qa[r][4 * grp + i], dxi[i], dpq[i]);
-            const float S0 = acc.S0, S1 = acc.S1, S3 = acc.S3, C0 = acc.C0, C1 = acc.C1, C2 = acc.C2;
-            // the nine sums in s_acc order (kRecMean2D.. moments, opacity, colour), summed over the 16 groups
-            // g (lane bits 5, 4 transposed; bits 3, 2 by row rotations): afterwards lane 4 g + r with bits 2-3
-            // clear holds record r's total of quantity (bit 5) + 2 (bit 4) [+ 4 for c1, 8 for c2]
-            const float a0 = S1, a1 = dy * S0, a2 = S3, a3 = dy * S1, a4 = dy * dy * S0, a5 = S0;
-            const float c0 = sum4(sum8(pair16(pair32(a0, a1), pair32(a2, a3))));
-            const float c1 = sum4(sum8(pair16(pair32(a4, a5), pair32(C0, C1))));
-            const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
-            wave_lds_handoff();  // phase-1 writes of the next group must stay behind these reads
-            if (!(lane & 12) && j0 + r < m) {
-                const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
-                atomicAdd(&s_acc[qk][rs], c0);
-                atomicAdd(&s_acc[4 + qk][rs], c1);
-                if (qk == 0) atomicAdd(&s_acc[8][rs], c2);
-            }
-        }
+        };
+        if (any_bg)
+            walk(std::true_type{});
+        else
+            walk(std::false_type{});
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
             const float4 pc = s_pc[tid];
             const float2 bo = *reinterpret_cast<const float2*>(&s_bo[tid]);
             const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
             const float o = co.w;  // the moments were summed over G dL/dalpha; q = o G dL/dalpha
-            const float m0 = s_acc[0][tid] * o, m1 = s_acc[1][tid] * o;
+            // raw tile-local moments (phase 2) -> sums over dx = mx - x, dy = my - y
+            const float S0 = s_acc[5][tid], Mx = s_acc[0][tid], My = s_acc[1][tid];
+            const float mxt = pc.x - tile_x0, myt = pc.y - tile_y0;
+            const float Sdx = fmaf(mxt, S0, -Mx), Sdy = fmaf(myt, S0, -My);
+            const float Sdxx = fmaf(mxt, fmaf(mxt, S0, -2.f * Mx), s_acc[2][tid]);
+            const float Sdxy = fmaf(mxt, Sdy, fmaf(-myt, Mx, s_acc[3][tid]));
+            const float Sdyy = fmaf(myt, fmaf(myt, S0, -2.f * My), s_acc[4][tid]);
+            const float m0 = Sdx * o, m1 = Sdy * o;
             s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
             s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
-            s_acc[2][tid] *= -0.5f * o;
-            s_acc[3][tid] *= -0.5f * o;
-            s_acc[4][tid] *= -0.5f * o;
+            s_acc[2][tid] = Sdxx * (-0.5f * o);
+            s_acc[3][tid] = Sdxy * (-0.5f * o);
+            s_acc[4][tid] = Sdyy * (-0.5f * o);
         }
         lds_barrier();
         // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,
