@@ -150,6 +150,10 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Ballot of a bool straight from its lane mask.  HIP's __ballot(int) converts the bool to an int and back,
+// which the compiler emits as v_cndmask 0/1 + v_cmp_ne (two VALU ops per ballot in the render loops).
+__device__ __forceinline__ unsigned long long wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 // Four-column variant: returns, in every lane l, the 64-lane total of column (l >> 4).

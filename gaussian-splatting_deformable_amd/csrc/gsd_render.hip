@@ -105,7 +105,7 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
                                              qy0 + (float)(RH - 1));
             }
         }
-        const unsigned long long mask = __ballot(hit);
+        const unsigned long long mask = wave_ballot(hit);
         if (hit) {
             const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
             s_list[m + below] = (uint8_t)t;
@@ -166,7 +166,7 @@ __device__ __forceinline__ int2 wave_compact_groups(const float4* __restrict__ s
         for (int g = 0; g < kFwdGroups; ++g) {
             const float4 r = fwd_group_rect(g, qx0, qy0);
             const bool hit = t < n && bx.y >= r.x && bx.x <= r.y && bx.w >= r.z && bx.z <= r.w;
-            const unsigned long long b = __ballot(hit);
+            const unsigned long long b = wave_ballot(hit);
             if (hit)
                 lists[g][cnt[g] + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))] = (uint8_t)t;
@@ -266,7 +266,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     if (over_capacity(p.k_guard, p.k_cap)) return;
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);
     const int tid = threadIdx.x;
-    bool done = !tg.inside;
+    // `done` (the pixel has saturated, or lies outside the image) as the wave's lane mask: the per-record
+    // decisions below are lane masks combined on the scalar unit and used as select masks
+    // (__builtin_amdgcn_inverse_ballot_w64), so no bool is materialised in a vector register
+    unsigned long long done_m = wave_ballot(!tg.inside);
     const uint2 rg = p.ranges[tg.tile];
     const int rounds = ((int)(rg.y - rg.x) + kTilePix - 1) / kTilePix;
     int toDo = (int)(rg.y - rg.x);
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         // forward.cu:309-311: stop once every pixel of the tile is saturated
-        if (__syncthreads_count(done) == kTilePix) break;
+        if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(done_m)) == kTilePix) break;
         const int k = (int)rg.x + i * kTilePix + tid;
         if (k < (int)rg.y) {
             const uint32_t g = p.point_list[k];
@@ -294,16 +297,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         const int2 mm = wave_compact_groups(s_box, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane);
         const int mine = mm.x, m = mm.y;  // this lane's group's list length, the longest
         for (int j0 = 0; j0 < m; j0 += kBatch) {
-            if (!__ballot(!done)) break;  // every pixel of this wave has saturated
+            if (done_m == ~0ull) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
             float a[kBatch];
             bool keep[kBatch];
             int slot[kBatch];
             static_assert(kBatch == 4, "one LDS word of list entries per batch");
             const uint32_t w4 = *reinterpret_cast<const uint32_t*>(list + j0);
+            unsigned long long in_m[kBatch];  // lanes whose group list holds entry j0 + u
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
-                slot[u] = list_slot(w4, u, j0, mine);  // past the list: slot 0, staged, so its colour is finite
+                in_m[u] = wave_ballot(j0 + u < mine);
+                // past the list: slot 0, staged, so its colour is finite
+                slot[u] = __builtin_amdgcn_inverse_ballot_w64(in_m[u]) ? (int)((w4 >> (8 * u)) & 0xffu) : 0;
                 float G;
                 a[u] = record_alpha(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, G, keep[u]);
             }
@@ -314,13 +320,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 if (j0 + u >= m) break;
-                bool take = !done & (j0 + u < mine) & keep[u] & (a[u] >= 1.0f / 255.0f);
-                if (!__ballot(take)) continue;
+                unsigned long long take_m = ~done_m & in_m[u] & wave_ballot(keep[u]) &
+                                            wave_ballot(a[u] >= 1.0f / 255.0f);
+                if (!take_m) continue;
                 const float alpha = a[u];
                 const float test_T = T * (1 - alpha);
-                const bool fin = take & (test_T < 0.0001f);
-                done |= fin;
-                take &= !fin;
+                const unsigned long long fin_m = take_m & wave_ballot(test_T < 0.0001f);
+                done_m |= fin_m;
+                take_m &= ~fin_m;
+                const bool take = __builtin_amdgcn_inverse_ballot_w64(take_m);
                 const float4 c = s_rgb[slot[u]];
                 // C += c alpha T (forward.cu:356-357) as one FMA per channel on the weight alpha T, selected to 0
                 // where the lane does not take the record (C + c * 0 == C for the finite colours of staged records;
@@ -403,7 +411,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     float adot = 0.f;  // accum_rec . dL/dpixel (accum_rec with last_color / last_alpha folded in)
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float kbg = -T_final * bg_dot;
-    const bool any_bg = __ballot(kbg != 0.f) != 0;  // wave-uniform
+    const bool any_bg = wave_ballot(kbg != 0.f) != 0;  // wave-uniform
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
@@ -445,13 +453,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 // v = G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
                 // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
                 // needed from the lane.
-                bool any = false;
+                unsigned long long any_m = 0;  // lanes that took any record of the group
                 uint32_t w4 = 0;  // the group's four list entries (kBwdGroup == kBwdBatch: one sub-batch)
-    #pragma unroll
+#pragma unroll
                 for (int sb = 0; sb < kBwdGroup / kBwdBatch; ++sb) {
                     const int jb = j0 + sb * kBwdBatch;
                     if (sb > 0 && jb >= m) {  // wave-uniform: the tail of the list
-    #pragma unroll
+#pragma unroll
                         for (int u = 0; u < kBwdBatch; ++u) qa[sb * kBwdBatch + u][lane] = make_float2(0.f, 0.f);
                         continue;
                     }
@@ -463,17 +471,20 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                     // slot extraction and the bounds select run on the scalar unit, and each record costs one vector
                     // move for its LDS address (shared by its three reads)
                     w4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(list + jb));
-    #pragma unroll
+#pragma unroll
                     for (int u = 0; u < kBwdBatch; ++u) {
                         slot[u] = list_slot(w4, u, jb, m);
                         As[u] = record_alpha(s_pc[slot[u]], *reinterpret_cast<const float2*>(&s_bo[slot[u]]), pxf, pyf,
                                              Gs[u], keep[u]);
                     }
-    #pragma unroll
+#pragma unroll
                     for (int u = 0; u < kBwdBatch; ++u) {
-    #pragma clang fp contract(fast)
-                        const bool valid = (jb + u < m) & (slot[u] > slot_min) & keep[u] & (As[u] >= 1.0f / 255.0f);
-                        any |= valid;
+#pragma clang fp contract(fast)
+                        const unsigned long long valid_m = (jb + u < m ? ~0ull : 0ull) &
+                                                           wave_ballot(slot[u] > slot_min) & wave_ballot(keep[u]) &
+                                                           wave_ballot(As[u] >= 1.0f / 255.0f);
+                        any_m |= valid_m;
+                        const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
                         const float alpha = valid ? As[u] : 0.f;
                         const float G = valid ? Gs[u] : 0.f;
                         const float inv1ma = fast_recip(1.f - alpha);
@@ -487,7 +498,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                         adot = fmaf(alpha, diff, adot);
                     }
                 }
-                if (!__ballot(any)) continue;  // wave-uniform: no pixel took any of these records
+                if (!any_m) continue;  // wave-uniform: no pixel took any of these records
                 wave_lds_handoff();
                 // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
                 // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i sits at tile-local
@@ -503,7 +514,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                              q3 = qa[r][4 * grp + 3];
                 float S0, Mx, Mxx, My, Mxy, Myy, C0, C1, C2;
                 {
-    #pragma clang fp contract(fast)
+#pragma clang fp contract(fast)
                     S0 = (q0.x + q1.x) + (q2.x + q3.x);
                     const float X1 = fmaf(3.f, q3.x, fmaf(2.f, q2.x, q1.x));  // sum v i
                     const float X2 = fmaf(9.f, q3.x, fmaf(4.f, q2.x, q1.x));  // sum v i^2
