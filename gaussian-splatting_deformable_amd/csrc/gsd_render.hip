@@ -51,8 +51,10 @@ __device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
     if (!(lo >= 0.999f)) return make_float4(1e30f, -1e30f, 1e30f, -1e30f);  // alpha < 1/255 everywhere (or NaN)
     if (!(det > 0.0f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f); // degenerate: never cull
     const float t = 2.0f * 0.69314718f * __builtin_amdgcn_logf(lo);     // 2 ln(255 o), v_log_f32 = log2
-    const float ex = sqrtf(fmaxf(t, 0.f) * c / det) * 1.001f + 0.02f;
-    const float ey = sqrtf(fmaxf(t, 0.f) * a / det) * 1.001f + 0.02f;
+    // hardware sqrt / reciprocal (1 ulp): far inside the 0.1 % inflation
+    const float rdet = __builtin_amdgcn_rcpf(det);
+    const float ex = __builtin_amdgcn_sqrtf(fmaxf(t, 0.f) * c * rdet) * 1.001f + 0.02f;
+    const float ey = __builtin_amdgcn_sqrtf(fmaxf(t, 0.f) * a * rdet) * 1.001f + 0.02f;
     if (!(ex < 1e30f) || !(ey < 1e30f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
     return make_float4(xy.x - ex, xy.x + ex, xy.y - ey, xy.y + ey);
 }
@@ -61,8 +63,10 @@ __device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
 // Q(d) = a dx^2 + 2 b dx dy + c dy^2 (positive definite: a, c > 0, det > 0).  Q is convex, so its minimum
 // over the rectangle is 0 when the centre is inside, else it lies on an edge; on an edge x = const the
 // minimiser is dy* = -b dx / c clamped to the edge (and symmetrically).  Conservative by `slack`.
-__device__ __forceinline__ float edge_min_x(float a, float b, float c, float dx, float dy0, float dy1) {
-    const float dy = fminf(fmaxf(-b * dx / c, dy0), dy1);
+// The minimiser is taken with the hardware reciprocal of c (1 ulp): an inexact dy* only moves the evaluated
+// point along the edge by ~1e-7 relative, which raises Q by a second-order amount far inside the test's slack.
+__device__ __forceinline__ float edge_min_x(float a, float b, float c, float rc, float dx, float dy0, float dy1) {
+    const float dy = fminf(fmaxf(-b * dx * rc, dy0), dy1);
     return a * dx * dx + 2.f * b * dx * dy + c * dy * dy;
 }
 __device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t, float x0, float x1, float y0,
@@ -70,8 +74,9 @@ __device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t
     const float dx0 = x0 - xy.x, dx1 = x1 - xy.x, dy0 = y0 - xy.y, dy1 = y1 - xy.y;
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // centre inside
     const float a = co.x, b = co.y, c = co.z;
-    float q = fminf(edge_min_x(a, b, c, dx0, dy0, dy1), edge_min_x(a, b, c, dx1, dy0, dy1));
-    q = fminf(q, fminf(edge_min_x(c, b, a, dy0, dx0, dx1), edge_min_x(c, b, a, dy1, dx0, dx1)));
+    const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
+    float q = fminf(edge_min_x(a, b, c, rc, dx0, dy0, dy1), edge_min_x(a, b, c, rc, dx1, dy0, dy1));
+    q = fminf(q, fminf(edge_min_x(c, b, a, ra, dy0, dx0, dx1), edge_min_x(c, b, a, ra, dy1, dx0, dx1)));
     return !(q > t);  // NaN-safe: keeps the record
 }
 
