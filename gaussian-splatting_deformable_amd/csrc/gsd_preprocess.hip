@@ -389,34 +389,38 @@ __device__ __forceinline__ void zero_sh_tail(const PreprocessBwdParams& p, int i
 
 // dL/d(raw parameters) of one Gaussian from the activated-space gradients (k_activate_bwd's formulas):
 // xyz: identity; scaling: * exp(scaling); rotation: (I - u u^T) / |q| (u = q / |q|); opacity: * s (1 - s).
+// With the fused Adam epilogue (adam_row != nullptr) the final gradients of the parameters that have an Adam sink
+// go to the lane's LDS row (columns: xyz 0-2, scaling 3-5, rotation 6-9, opacity 10), from which the wave
+// applies the step to its 64 Gaussians' contiguous regions (k_preprocess_bwd).
+constexpr int kGeoCol[4] = {0, 3, 6, 10};
 __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, float3 dmean, float3 dscale,
-                                          float3 scale, float4 drot, float dopac, float4 q, float raw_opac, bool vis) {
+                                          float3 scale, float4 drot, float dopac, float4 q, float raw_opac, bool vis,
+                                          float* __restrict__ adam_row) {
     const bool acc = p.a_accumulate != 0;
     auto put = [acc, vis](float* d, float v) {  // a skipped Gaussian's gradients are zeros (+0 when accumulating)
         v = vis ? v : 0.f;
         *d = acc ? *d + v : v;
     };
-    // fused Adam epilogue (store mode only): the element's final gradient updates the parameter in place
-    auto upd = [&](const AdamSinkDev& sk, long long e, float v) { adam_at(sk, p.adam, e, vis ? v : 0.f); };
-    if (p.adam_on && p.adam.xyz.p) {
-        upd(p.adam.xyz, 3LL * i, dmean.x);
-        upd(p.adam.xyz, 3LL * i + 1, dmean.y);
-        upd(p.adam.xyz, 3LL * i + 2, dmean.z);
+    auto upd = [&](int col, float v) { adam_row[col] = vis ? v : 0.f; };
+    if (adam_row && p.adam.xyz.p) {
+        upd(kGeoCol[0], dmean.x);
+        upd(kGeoCol[0] + 1, dmean.y);
+        upd(kGeoCol[0] + 2, dmean.z);
     } else if (p.a_xyz) {
         put(p.a_xyz + 3 * i, dmean.x);
         put(p.a_xyz + 3 * i + 1, dmean.y);
         put(p.a_xyz + 3 * i + 2, dmean.z);
     }
-    if (p.adam_on && p.adam.scaling.p) {
-        upd(p.adam.scaling, 3LL * i, dscale.x * scale.x);
-        upd(p.adam.scaling, 3LL * i + 1, dscale.y * scale.y);
-        upd(p.adam.scaling, 3LL * i + 2, dscale.z * scale.z);
+    if (adam_row && p.adam.scaling.p) {
+        upd(kGeoCol[1], dscale.x * scale.x);
+        upd(kGeoCol[1] + 1, dscale.y * scale.y);
+        upd(kGeoCol[1] + 2, dscale.z * scale.z);
     } else if (p.a_scaling) {
         put(p.a_scaling + 3 * i, dscale.x * scale.x);
         put(p.a_scaling + 3 * i + 1, dscale.y * scale.y);
         put(p.a_scaling + 3 * i + 2, dscale.z * scale.z);
     }
-    if (p.a_rotation || (p.adam_on && p.adam.rotation.p)) {
+    if (p.a_rotation || (adam_row && p.adam.rotation.p)) {
         const float nraw = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
         float4 gq;
         if (nraw > 1e-12f) {
@@ -429,11 +433,11 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
             gq = make_float4(drot.x * 1e12f, drot.y * 1e12f, drot.z * 1e12f, drot.w * 1e12f);
         }
         if (!vis) gq = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p.adam_on && p.adam.rotation.p) {
-            upd(p.adam.rotation, 4LL * i, gq.x);
-            upd(p.adam.rotation, 4LL * i + 1, gq.y);
-            upd(p.adam.rotation, 4LL * i + 2, gq.z);
-            upd(p.adam.rotation, 4LL * i + 3, gq.w);
+        if (adam_row && p.adam.rotation.p) {
+            upd(kGeoCol[2], gq.x);
+            upd(kGeoCol[2] + 1, gq.y);
+            upd(kGeoCol[2] + 2, gq.z);
+            upd(kGeoCol[2] + 3, gq.w);
         } else {
             float4* d = reinterpret_cast<float4*>(p.a_rotation) + i;
             if (acc) {
@@ -443,9 +447,9 @@ __device__ __forceinline__ void raw_grads(const PreprocessBwdParams& p, int i, f
             *d = gq;
         }
     }
-    if (p.adam_on && p.adam.opacity.p) {
+    if (adam_row && p.adam.opacity.p) {
         const float sg = act_opac(raw_opac);
-        upd(p.adam.opacity, i, dopac * sg * (1.f - sg));
+        upd(kGeoCol[3], dopac * sg * (1.f - sg));
     } else if (p.a_opacity) {
         const float sg = act_opac(raw_opac);
         put(p.a_opacity + i, dopac * sg * (1.f - sg));
@@ -635,12 +639,12 @@ __device__ __forceinline__ void sh_region_store(float* __restrict__ dst, int row
 // The fused Adam step over a region (gsd_adam_epilogue): the gradient rows in LDS (columns [c0, c0 + R)) are
 // the final gradients of the region's parameter elements; each is applied to (param, exp_avg, exp_avg_sq) in
 // place -- coalesced like sh_region_store, kCh elements per lane in flight -- instead of being stored.
-template <int R>
+template <int R, int RS = kShRowStride>
 __device__ __forceinline__ void sh_region_adam(const AdamSinkDev& sk, const AdamEpiDev& e, long long base, int rows,
-                                               const float* __restrict__ lds, int c0) {
+                                               const float* __restrict__ lds, int c0, int lane = threadIdx.x) {
     constexpr int kCh = R < 15 ? R : 15;
     static_assert(R % kCh == 0, "whole chunks");
-    const int lane = threadIdx.x, n = rows * R;
+    const int n = rows * R;
     float* __restrict__ P = sk.p + base;
     float* __restrict__ Mo = sk.m + base;
     float* __restrict__ V = sk.v + base;
@@ -653,7 +657,7 @@ __device__ __forceinline__ void sh_region_adam(const AdamSinkDev& sk, const Adam
             const int el = (c + i) * kShWave + lane;
             const int gi = el / R, j = el - gi * R;
             in[i] = rows == kShWave || el < n;
-            g[i] = lds[gi * kShRowStride + c0 + j];
+            g[i] = lds[gi * RS + c0 + j];
             pp[i] = in[i] ? P[el] : 0.f;
             mm[i] = in[i] ? __builtin_nontemporal_load(Mo + el) : 0.f;
             vv[i] = in[i] ? __builtin_nontemporal_load(V + el) : 0.f;
@@ -750,9 +754,9 @@ __global__ __launch_bounds__(kShWave) __attribute__((amdgpu_waves_per_eu(4))) vo
 // The geometry half of the per-Gaussian backward: computeCov2DCUDA + preprocessCUDA bwd without the SH
 // (backward.cu:144-396); the view-direction term of dL/dmean3D comes from the record (k_preprocess_bwd_sh,
 // launched first; zeros when there is no SH operand).
-__global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= p.P) return;
+// One Gaussian of the geometry half; with the fused Adam epilogue its final raw-parameter gradients go to
+// adam_row instead (raw_grads).
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams& p, int idx, float* adam_row) {
     // Every per-Gaussian load is issued up front, before the visibility test: a Gaussian the backward skips
     // (radii == 0, backward.cu:359-360) is computed like the others and its outputs are replaced by the zeros
     // torch::zeros holds -- one latency instead of two, and no divergent branch.
@@ -824,7 +828,7 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
     dscale = make_float3(z(dscale.x), z(dscale.y), z(dscale.z));
     drot = make_float4(z(drot.x), z(drot.y), z(drot.z), z(drot.w));
     if (p.raw_act) {  // through the activations into the raw parameters' sinks (k_activate_bwd's formulas)
-        raw_grads(p, idx, dmean, dscale, scale, drot, r1.y, q_in, raw_opac, vis);
+        raw_grads(p, idx, dmean, dscale, scale, drot, r1.y, q_in, raw_opac, vis, adam_row);
         return;
     }
     p.dL_dmeans3D[3 * idx] = dmean.x;
@@ -836,6 +840,34 @@ __global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
         p.dL_dscales[3 * idx + 2] = dscale.z;
     }
     if (p.dL_drotations) reinterpret_cast<float4*>(p.dL_drotations)[idx] = drot;
+}
+
+// The geometry half, one lane per Gaussian.  With the fused Adam epilogue (gsd_adam_epilogue) each wave then
+// steps its 64 Gaussians' xyz / scaling / rotation / opacity as contiguous regions: lane-consecutive dword
+// accesses to (param, exp_avg, exp_avg_sq), the gradients read from the lanes' LDS rows (sh_region_adam), in
+// place of one lane reading and writing its own 3- or 4-float rows at a 12- / 16-B lane stride.
+constexpr int kGeoRowStride = 11;  // odd: the lanes' row writes are bank-conflict free
+__global__ __launch_bounds__(256) void k_preprocess_bwd(PreprocessBwdParams p) {
+    __shared__ float s_geo[256 / kShWave][kShWave * kGeoRowStride];
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (!p.adam_on) {
+        if (idx < p.P) preprocess_bwd_one(p, idx, nullptr);
+        return;
+    }
+    const int lane = threadIdx.x & (kShWave - 1);
+    const float* rows_lds = s_geo[threadIdx.x / kShWave];
+    if (idx < p.P) preprocess_bwd_one(p, idx, s_geo[threadIdx.x / kShWave] + lane * kGeoRowStride);
+    wave_lds_handoff();
+    const int g0 = idx - lane, rows = min(kShWave, p.P - g0);
+    if (rows <= 0) return;
+    if (p.adam.xyz.p)
+        sh_region_adam<3, kGeoRowStride>(p.adam.xyz, p.adam, 3LL * g0, rows, rows_lds, kGeoCol[0], lane);
+    if (p.adam.scaling.p)
+        sh_region_adam<3, kGeoRowStride>(p.adam.scaling, p.adam, 3LL * g0, rows, rows_lds, kGeoCol[1], lane);
+    if (p.adam.rotation.p)
+        sh_region_adam<4, kGeoRowStride>(p.adam.rotation, p.adam, 4LL * g0, rows, rows_lds, kGeoCol[2], lane);
+    if (p.adam.opacity.p)
+        sh_region_adam<1, kGeoRowStride>(p.adam.opacity, p.adam, (long long)g0, rows, rows_lds, kGeoCol[3], lane);
 }
 
 }  // namespace gsd

@@ -420,10 +420,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
-    // phase 2: tile-local origin of the lane's half-row of four pixels; the flush's tile origin
-    const float ph2_ox = (float)(8 * (tg.wave & 1) + 4 * ((lane >> 2) & 1));
-    const float ph2_oy = (float)(8 * (tg.wave >> 1) + (lane >> 3));
-    const float tile_x0 = (float)((tg.tile % p.grid_x) * kTileX), tile_y0 = (float)((tg.tile / p.grid_x) * kTileY);
+    // phase 2: the first pixel of the lane's half-row of four
+    const float ph2_x0 = tg.qx0 + (float)(4 * ((lane >> 2) & 1)), ph2_y0 = tg.qy0 + (float)(lane >> 3);
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         lds_barrier();
@@ -506,28 +504,32 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 if (!any_m) continue;  // wave-uniform: no pixel took any of these records
                 wave_lds_handoff();
                 // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
-                // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i sits at tile-local
-                // (ox + i, oy), ox = 8 (wave & 1) + 4 (g & 1), oy = 8 (wave >> 1) + (g >> 1).  The lane sums raw
-                // moments of v in tile-local pixel coordinates -- S0 = sum v, Mx = sum v x, Mxx = sum v x^2 and the
-                // y moments from its constant oy -- and C = sum w dL/dpixel; the flush turns them into the
-                // mean-centred sums of backward.cu:545-554 (sum v dx = (mx - x0) S0 - Mx, ...).  No record data
-                // is read here, and the in-row sums use the constant offsets i: 19 VALU ops for the quad's four
-                // pixels instead of 27 plus 9 for the per-record offsets.
+                // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i sits at (x0 + i, y0),
+                // x0 = qx0 + 4 (g & 1), y0 = qy0 + (g >> 1); relative to the record's mean ex = x0 - mx, ey = y0 - my.
+                // With S0 = sum v, X1 = sum v i, X2 = sum v i^2 (constant offsets i): sum v (x - mx) = ex S0 + X1,
+                // sum v (x - mx)^2 = ex (ex S0 + X1) + ex X1 + X2, the y sums from the lane's constant ey, and
+                // C = sum w dL/dpixel.  The reference's dx = mx - x (backward.cu:545-554) flips the first moments' sign
+                // (the flush).  19 VALU ops for the four pixels' sums instead of 27, and no per-pixel offsets.  (Raw
+                // tile-local moments centred only in the flush need no record read here, but the centring cancels:
+                // the float-atomic order noise of the sums grew to ~1e-4 relative.)
                 const int r = lane & 3, grp = lane >> 2;
                 static_assert(kBwdGroup == kBwdBatch, "phase 2 reads the group's slots from phase 1's list word");
+                const int rs = list_slot(w4, r, j0, m);
+                const float4 mrec = s_pc[rs];
                 const float2 q0 = qa[r][4 * grp], q1 = qa[r][4 * grp + 1], q2 = qa[r][4 * grp + 2],
                              q3 = qa[r][4 * grp + 3];
                 float S0, Mx, Mxx, My, Mxy, Myy, C0, C1, C2;
                 {
 #pragma clang fp contract(fast)
+                    const float ex = ph2_x0 - mrec.x, ey = ph2_y0 - mrec.y;
                     S0 = (q0.x + q1.x) + (q2.x + q3.x);
                     const float X1 = fmaf(3.f, q3.x, fmaf(2.f, q2.x, q1.x));  // sum v i
                     const float X2 = fmaf(9.f, q3.x, fmaf(4.f, q2.x, q1.x));  // sum v i^2
-                    Mx = fmaf(ph2_ox, S0, X1);
-                    Mxx = fmaf(ph2_ox, Mx + X1, X2);                            // ox^2 S0 + 2 ox X1 + X2
-                    My = ph2_oy * S0;
-                    Myy = ph2_oy * My;
-                    Mxy = ph2_oy * Mx;
+                    Mx = fmaf(ex, S0, X1);                                      // sum v (x - mx)
+                    Mxx = fmaf(ex, Mx + X1, X2);                                // sum v (x - mx)^2
+                    My = ey * S0;
+                    Myy = ey * My;
+                    Mxy = ey * Mx;
                     C0 = fmaf(q3.y, dpq[3].x, fmaf(q2.y, dpq[2].x, fmaf(q1.y, dpq[1].x, q0.y * dpq[0].x)));
                     C1 = fmaf(q3.y, dpq[3].y, fmaf(q2.y, dpq[2].y, fmaf(q1.y, dpq[1].y, q0.y * dpq[0].y)));
                     C2 = fmaf(q3.y, dpq[3].z, fmaf(q2.y, dpq[2].z, fmaf(q1.y, dpq[1].z, q0.y * dpq[0].z)));
@@ -538,7 +540,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                 const float c0 = sum4(sum8(pair16(pair32(Mx, My), pair32(Mxx, Mxy))));
                 const float c1 = sum4(sum8(pair16(pair32(Myy, S0), pair32(C0, C1))));
                 const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
-                const int rs = list_slot(w4, r, j0, m);
                 wave_lds_handoff();  // phase-1 writes of the next group must stay behind these reads
                 if (!(lane & 12) && j0 + r < m) {
                     const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
@@ -558,19 +559,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float2 bo = *reinterpret_cast<const float2*>(&s_bo[tid]);
             const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
             const float o = co.w;  // the moments were summed over G dL/dalpha; q = o G dL/dalpha
-            // raw tile-local moments (phase 2) -> sums over dx = mx - x, dy = my - y
-            const float S0 = s_acc[5][tid], Mx = s_acc[0][tid], My = s_acc[1][tid];
-            const float mxt = pc.x - tile_x0, myt = pc.y - tile_y0;
-            const float Sdx = fmaf(mxt, S0, -Mx), Sdy = fmaf(myt, S0, -My);
-            const float Sdxx = fmaf(mxt, fmaf(mxt, S0, -2.f * Mx), s_acc[2][tid]);
-            const float Sdxy = fmaf(mxt, Sdy, fmaf(-myt, Mx, s_acc[3][tid]));
-            const float Sdyy = fmaf(myt, fmaf(myt, S0, -2.f * My), s_acc[4][tid]);
-            const float m0 = Sdx * o, m1 = Sdy * o;
+            // phase 2 summed the first moments over x - mx, y - my: the reference's dx = mx - x flips them
+            const float m0 = -s_acc[0][tid] * o, m1 = -s_acc[1][tid] * o;
             s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
             s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
-            s_acc[2][tid] = Sdxx * (-0.5f * o);
-            s_acc[3][tid] = Sdxy * (-0.5f * o);
-            s_acc[4][tid] = Sdyy * (-0.5f * o);
+            s_acc[2][tid] *= -0.5f * o;
+            s_acc[3][tid] *= -0.5f * o;
+            s_acc[4][tid] *= -0.5f * o;
         }
         lds_barrier();
         // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,
