@@ -142,6 +142,8 @@ def main():
     from gsd_amd.scene import CONFIGS, make_gaussians
 
     rank, local, world = init_from_env()
+    if os.environ.get("GSD_DIST_BACKEND") == "gloo":   # rehearsal of the N > 1 path on fewer GPUs
+        local %= max(1, torch.cuda.device_count())
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]

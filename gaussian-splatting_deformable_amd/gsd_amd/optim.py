@@ -183,6 +183,7 @@ class FusedAdam(torch.optim.Optimizer):
         except BaseException:
             self.flat.epilogue = None
             self.flat.fused = set()
+            self.flat.drain_early()
             raise
         self.flat.epilogue = None
         self.allreduce_step(zero_grad=True)
@@ -215,6 +216,19 @@ class FusedAdam(torch.optim.Optimizer):
                 lr=float(self.param_groups[self._gidx[i]]["lr"]), step=self.steps[i]))
             self.flat.fused.add(id(p))
         return epi
+
+    def reduce_early(self, params) -> bool:
+        """Called by the data-parallel rasterizer backward inside ``step_in_backward`` once it has stored the final
+        per-rank gradients of ``params``: their all-reduce starts now (FlatGrads.early_allreduce), to run on the
+        links while the device finishes the backward; ``allreduce_step`` then waits on it instead of issuing it.
+        Inside the block a second producer of these gradients raises (it would miss the sum)."""
+        if self.flat.epilogue is not self or data_parallel_world() == 1:
+            return False
+        index = {id(p) for p in self._params}
+        if any(id(p) not in index or id(p) in self.flat.fused or id(p) in self.flat.early_ids for p in params):
+            return False
+        self.flat.early_allreduce(params)
+        return True
 
     @staticmethod
     def fused_owner(params):

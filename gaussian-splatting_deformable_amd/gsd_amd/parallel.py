@@ -30,6 +30,9 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
+        # GSD_DIST_BACKEND=gloo: rehearse the data-parallel path with every rank on one GPU (gloo through host
+        # memory; bench.py then maps LOCAL_RANK onto the devices present)
+        backend = backend or os.environ.get("GSD_DIST_BACKEND") or None
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
@@ -104,12 +107,14 @@ class FlatGrads:
         self.epilogue = None   # the FusedAdam inside its step_in_backward block, if any
         self.fused = set()     # parameters that block already stepped inside the backward
         self.reduced = set()   # views already summed over the ranks this step (mark_reduced)
+        self.early = []        # [(a, b, work)]: all-reduces issued inside the backward (early_allreduce)
+        self.early_ids = set()
         self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
         self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
         self.attach()
 
     def _fused_guard(self, ids):
-        if self.fused.intersection(ids):
+        if self.fused.intersection(ids) or self.early_ids.intersection(ids):
             raise RuntimeError("FlatGrads: a second gradient for a parameter whose Adam step already ran inside "
                                "the backward (FusedAdam.step_in_backward); leave it out of that block")
 
@@ -136,6 +141,7 @@ class FlatGrads:
             p._gsd_flat = self
 
     def zero(self):
+        self.drain_early()
         self.slab.zero_()
         self.stale.clear()
         self.reduced = set()
@@ -143,6 +149,7 @@ class FlatGrads:
 
     def invalidate(self):
         """Mark every view stale (no memory traffic): the next gradient producer stores instead of adding."""
+        self.drain_early()
         self.stale = {id(p) for p in self.params}
         self.reduced = set()
         self._version = self.slab._version
@@ -185,6 +192,37 @@ class FlatGrads:
                 p.grad = v
                 self.stale.discard(id(p))
 
+    def early_allreduce(self, params, bucket_floats: int = BUCKET_FLOATS):
+        """Start the all-reduce of ``params``' views now, from inside the backward that produced their final
+        per-rank gradients (FusedAdam.step_in_backward guards them against a second producer), so that it runs
+        on the links while the device computes what is left of the backward.  The views count as reduced for
+        this step; allreduce / allreduce_buckets hand their works to the consumer instead of reducing again."""
+        if data_parallel_world() == 1:
+            return
+        ids = {id(p) for p in params}
+        if not ids <= set(self._view_of) or ids & self.early_ids:
+            raise RuntimeError("early_allreduce: parameters not in this slab, or already reduced this step")
+        keep = [p for p in self.params if id(p) not in ids]
+        nccl = dist.get_backend() == "nccl" or not self.slab.is_cuda
+        for a, b in self._runs({id(p) for p in keep}):
+            for c in range(a, b, max(1, int(bucket_floats))):
+                d = min(b, c + int(bucket_floats))
+                if nccl:
+                    self.early.append((c, d, dist.all_reduce(self.slab[c:d], op=dist.ReduceOp.SUM, async_op=True)))
+                else:   # gloo on device tensors (tests): through host memory, synchronously
+                    h = self.slab[c:d].cpu()
+                    dist.all_reduce(h, op=dist.ReduceOp.SUM)
+                    self.slab[c:d].copy_(h)
+                    self.early.append((c, d, None))
+        self.early_ids |= ids
+
+    def drain_early(self):
+        """Order the current stream behind any early all-reduce still in flight and forget them."""
+        for _, _, w in self.early:
+            if w is not None:
+                w.wait()
+        self.early, self.early_ids = [], set()
+
     def _runs(self, reduced):
         """Contiguous slab ranges [a, b) of the views not in ``reduced``."""
         runs, off = [], 0
@@ -203,9 +241,14 @@ class FlatGrads:
         already summed (mark_reduced -- e.g. the SH gradient the rasterizer assembled from every view)."""
         self.collect()
         self.settle()
-        reduced, self.reduced = self.reduced, set()
+        reduced, self.reduced = self.reduced | self.early_ids, set()
+        early = [w for _, _, w in self.early if w is not None]
+        self.early, self.early_ids = [], set()
         if data_parallel_world() == 1:
             return None
+        if not async_op:
+            for w in early:
+                w.wait()
         runs = self._runs(reduced)
         if dist.get_backend() != "nccl" and self.slab.is_cuda:   # gloo (tests): through host memory
             for a, b in runs:
@@ -214,7 +257,7 @@ class FlatGrads:
                 self.slab[a:b].copy_(h)
             return None
         works = [dist.all_reduce(self.slab[a:b], op=op or dist.ReduceOp.SUM, async_op=async_op) for a, b in runs]
-        return works if async_op else None
+        return early + works if async_op else None
 
     def allreduce_buckets(self, bucket_floats: int = BUCKET_FLOATS):
         """The all-reduce of ``allreduce`` issued asynchronously in buckets of at most ``bucket_floats``, for
@@ -225,24 +268,28 @@ class FlatGrads:
         collective, the host does not block)."""
         self.collect()
         self.settle()
-        reduced, self.reduced = self.reduced, set()
+        reduced, self.reduced = self.reduced | self.early_ids, set()
+        early, self.early, self.early_ids = self.early, [], set()
         n = self.slab.numel()
         if data_parallel_world() == 1:
             return [(0, n, None)]
-        out, pos = [], 0
+        work = list(early)   # ranges whose all-reduce went out inside the backward (early_allreduce)
         nccl = dist.get_backend() == "nccl" or not self.slab.is_cuda
         for a, b in self._runs(reduced):
-            if a > pos:
-                out.append((pos, a, None))
             for c in range(a, b, max(1, int(bucket_floats))):
                 d = min(b, c + int(bucket_floats))
                 if nccl:
-                    out.append((c, d, dist.all_reduce(self.slab[c:d], op=dist.ReduceOp.SUM, async_op=True)))
+                    work.append((c, d, dist.all_reduce(self.slab[c:d], op=dist.ReduceOp.SUM, async_op=True)))
                 else:   # gloo on device tensors (tests): through host memory, synchronously
                     h = self.slab[c:d].cpu()
                     dist.all_reduce(h, op=dist.ReduceOp.SUM)
                     self.slab[c:d].copy_(h)
-                    out.append((c, d, None))
+                    work.append((c, d, None))
+        out, pos = [], 0
+        for a, b, w in sorted(work, key=lambda t: t[0]):
+            if a > pos:
+                out.append((pos, a, None))
+            out.append((a, b, w))
             pos = b
         if pos < n:
             out.append((pos, n, None))

@@ -199,7 +199,8 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None, e
     if ctx.sh_views and world > 1 and sinks is not None and offset is None and parallel.SH_VIEWS:
         g_m2d, g_op, g_m3d, g_sc, g_rot = _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations,
                                                              radii, f_dc, f_rest, geomBuffer, binningBuffer,
-                                                             imgBuffer, sinks, acc, world, activation, raw_opacity)
+                                                             imgBuffer, sinks, acc, world, activation, raw_opacity,
+                                                             raw=raw)
         return g_m2d, None, None, None, (g_op, g_m3d, g_sc, g_rot)
     if sinks is not None:
         d_dc, d_rest = sinks
@@ -227,10 +228,13 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None, e
 
 
 def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radii, f_dc, f_rest, geomBuffer,
-                       binningBuffer, imgBuffer, sinks, acc, world, activation=None, raw_opacity=None):
+                       binningBuffer, imgBuffer, sinks, acc, world, activation=None, raw_opacity=None, raw=()):
     """Data-parallel backward of the split-SH rasterizer with the SH gradient exchanged per view: this rank's
     row [masked dL/dRGB (P*3) | campos (3) | pad] is all-gathered and every rank runs gsd_sh_grad_views over
-    all rows into its SH sinks, which FlatGrads then leaves out of the gradient all-reduce."""
+    all rows into its SH sinks, which FlatGrads then leaves out of the gradient all-reduce.  Inside
+    FusedAdam.step_in_backward the raw parameters' gradients (``raw``, stored by this backward) are final per
+    rank here: their all-reduce goes out right behind the all-gather (FusedAdam.reduce_early) and runs on the
+    links while the device assembles and steps the SH gradient."""
     import torch.distributed as dist
     P, dev = int(f_dc.size(0)), f_dc.device
     stride = 3 * P + 4
@@ -243,12 +247,19 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
         binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity)
     views = torch.empty(world, stride, dtype=torch.float32, device=dev)
+    gathered = None
     if dist.get_backend() == "nccl":   # RCCL: one all_gather into the (world, stride) buffer
-        dist.all_gather_into_tensor(views, row)
+        gathered = dist.all_gather_into_tensor(views, row, async_op=True)
     else:                              # gloo (tests): through host memory
         parts = [torch.empty(stride, dtype=torch.float32) for _ in range(world)]
         dist.all_gather(parts, row.cpu())
         views.copy_(torch.stack(parts))
+    if raw and activation is not None and not activation.accumulate:
+        owner = FusedAdam.fused_owner(raw)
+        if owner is not None:
+            owner.reduce_early(raw)    # queued behind the all-gather on RCCL's stream
+    if gathered is not None:
+        gathered.wait()                # the compute stream waits for the gather only
     epi = None
     owner = FusedAdam.fused_owner(ctx.params) if not acc else None
     if owner is not None and f_dc.is_contiguous() and f_rest.is_contiguous():

@@ -110,7 +110,7 @@ def test_two_rank_sh_views_protocol(tmp_path):
         np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-9)
 
 
-def _worker_buckets(rank, world, port, out_dir):
+def _worker_buckets(rank, world, port, out_dir, early=False):
     import sys
     for p in (PKG, ROOT):
         if p not in sys.path:
@@ -131,7 +131,15 @@ def _worker_buckets(rank, world, port, out_dir):
         total_sh += torch.from_numpy(view_grads(yaw=2.0 * k)[1])
     params[1].grad.copy_(total_sh)
     mark_reduced([params[1]])
+    if early:   # the raw parameters' all-reduce started inside the backward (FusedAdam.reduce_early)
+        fg.early_allreduce([params[2], params[0]], bucket_floats=700)
+        try:    # a second producer for an early-reduced gradient would miss the sum: refused
+            fg.claim([params[0]])
+            raise AssertionError("claim of an early-reduced parameter did not raise")
+        except RuntimeError:
+            pass
     ranges = fg.allreduce_buckets(bucket_floats=1000)    # several buckets per run, a partial one at each end
+    assert not fg.early and not fg.early_ids
     covered = 0
     for a, b, work in ranges:
         assert a == covered and b > a
@@ -139,7 +147,7 @@ def _worker_buckets(rank, world, port, out_dir):
         if work is not None:
             work.wait()
     assert covered == fg.slab.numel()
-    np.save(os.path.join(out_dir, f"brank{r}.npy"), fg.slab.numpy())
+    np.save(os.path.join(out_dir, f"{'e' if early else 'b'}rank{r}.npy"), fg.slab.numpy())
     dist.destroy_process_group()
 
 
@@ -152,6 +160,19 @@ def test_four_rank_bucketed_allreduce_equals_sum_of_views(tmp_path):
     want = sum(np.concatenate([g.reshape(-1) for g in view_grads(2.0 * r)]) for r in range(world))
     for r in range(world):
         got = np.load(os.path.join(str(tmp_path), f"brank{r}.npy"))
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
+
+
+def test_four_rank_early_allreduce_then_buckets(tmp_path):
+    """FlatGrads.early_allreduce (issued inside the data-parallel backward for the raw parameters, then handed
+    to allreduce_buckets) over four gloo ranks: two non-adjacent parameters go out early in their own buckets,
+    the rest in allreduce_buckets' -- every element summed exactly once, the ranges covering the slab in order,
+    and a second producer of an early-reduced gradient refused."""
+    world = 4
+    mp.spawn(_worker_buckets, args=(world, _free_port(), str(tmp_path), True), nprocs=world, join=True)
+    want = sum(np.concatenate([g.reshape(-1) for g in view_grads(2.0 * r)]) for r in range(world))
+    for r in range(world):
+        got = np.load(os.path.join(str(tmp_path), f"erank{r}.npy"))
         np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-7)
 
 
