@@ -297,7 +297,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

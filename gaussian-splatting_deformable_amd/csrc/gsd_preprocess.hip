@@ -751,6 +751,117 @@ __global__ __launch_bounds__(kShWave) __attribute__((amdgpu_waves_per_eu(4))) vo
     if (p.dsh_off) sh_region_store<3 * M, kAcc>(p.dsh_off + (size_t)g0 * 3 * M, rows, rows_lds, 0);
 }
 
+// The SH half with the fused Adam step for the split operand without an offset (the bench / training path:
+// store mode, M = 16).  The SH parameters stay in the LDS rows they were staged into, and each lane leaves its
+// Gaussian's 16 basis values and masked dL/dRGB in a short LDS row; the Adam pass then forms each gradient element
+// B_k dL/dRGB_c from those (the product k_preprocess_bwd_sh_rows stores in its gradient rows, bit for bit) and
+// takes the parameter from LDS.  k_preprocess_bwd_sh_rows<.., kAdam> re-reads the parameter from global memory
+// instead, and that re-read missed L2: FETCH_SIZE showed ~200 MB more than the algorithmic reads per step at 1M
+// Gaussians (scripts/prof_step.py PMC pass), one 192-B SH row per Gaussian.
+constexpr int kBasisStride = 19;  // 16 basis values + dL/dRGB (3): odd, so the per-lane row writes are conflict-free
+template <int R, int C0>
+__device__ __forceinline__ float basis_grad(const float* __restrict__ bas, int el, int& gi, int& col) {
+    gi = el / R;
+    col = C0 + (el - gi * R);
+    const int k = col / 3, ch = col - 3 * k;
+    return bas[gi * kBasisStride + k] * bas[gi * kBasisStride + 16 + ch];
+}
+template <int R, int C0>
+__device__ __forceinline__ void sh_region_adam_basis(const AdamSinkDev& sk, const AdamEpiDev& e, long long base,
+                                                     int rows, const float* __restrict__ prm,
+                                                     const float* __restrict__ bas) {
+    constexpr int kCh = R < 15 ? R : 15;
+    static_assert(R % kCh == 0, "whole chunks");
+    const int lane = threadIdx.x, n = rows * R;
+    float* __restrict__ P = sk.p + base;
+    float* __restrict__ Mo = sk.m + base;
+    float* __restrict__ V = sk.v + base;
+#pragma unroll
+    for (int c = 0; c < R; c += kCh) {
+        float g[kCh], pp[kCh], mm[kCh], vv[kCh];
+        bool in[kCh];
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+            const int el = (c + i) * kShWave + lane;
+            int gi, col;
+            g[i] = basis_grad<R, C0>(bas, el, gi, col);
+            pp[i] = prm[gi * kShRowStride + col];
+            in[i] = rows == kShWave || el < n;
+            mm[i] = in[i] ? __builtin_nontemporal_load(Mo + el) : 0.f;
+            vv[i] = in[i] ? __builtin_nontemporal_load(V + el) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+            adam_elem(pp[i], g[i], mm[i], vv[i], e.w1, e.beta2, e.omb2, sk.step_size, sk.bc2_sqrt, e.eps);
+            const int el = (c + i) * kShWave + lane;
+            if (in[i]) {
+                P[el] = pp[i];
+                __builtin_nontemporal_store(mm[i], Mo + el);
+                __builtin_nontemporal_store(vv[i], V + el);
+            }
+        }
+    }
+}
+template <int R, int C0>
+__device__ __forceinline__ void sh_region_store_basis(float* __restrict__ dst, int rows, const float* __restrict__ bas) {
+    const int lane = threadIdx.x, n = rows * R;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int el = i * kShWave + lane;
+        int gi, col;
+        const float g = basis_grad<R, C0>(bas, el, gi, col);
+        if (rows == kShWave || el < n) dst[el] = g;
+    }
+}
+
+template <int DEG>
+__global__ __launch_bounds__(kShWave) void k_preprocess_bwd_sh_adam(PreprocessBwdParams p) {
+    __shared__ float rows_lds[kShWave * kShRowStride];   // the SH parameters (dc | rest) of the 64 Gaussians
+    __shared__ float basis_lds[kShWave * kBasisStride];  // per Gaussian: B_0..B_15, masked dL/dRGB
+    constexpr int nc = (DEG + 1) * (DEG + 1);
+    const int g0 = blockIdx.x * kShWave, lane = threadIdx.x, idx = g0 + lane;
+    const int rows = min(kShWave, p.P - g0);
+    sh_region_load<3, 0>(p.sh_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    sh_region_load<45, 0>(p.sh_rest + (size_t)g0 * 45, rows, rows_lds, 3);
+    __syncthreads();
+    const float* row = rows_lds + lane * kShRowStride;
+    float B[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) B[k] = 0.f;  // zero above the active degree, and for skipped Gaussians
+    float3 dc = make_float3(0.f, 0.f, 0.f);
+    if (idx < p.P && p.radii[idx] > 0) {
+        float4* rec = reinterpret_cast<float4*>(p.grad_rec + (size_t)idx * kGradRec);
+        const float4 r1 = rec[1], r2 = rec[2];  // colour gradient: r1.z, r1.w, r2.x
+        const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+        const float3 cam = make_float3(p.campos[0], p.campos[1], p.campos[2]);
+        const float3 dir_orig = make_float3(m.x - cam.x, m.y - cam.y, m.z - cam.z);
+        const float len = sqrtf(dot3(dir_orig, dir_orig));
+        const float3 dir = make_float3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+        const uint8_t cl = p.clamped[idx];
+        dc = make_float3(r1.z * ((cl & 1) ? 0 : 1), r1.w * ((cl & 2) ? 0 : 1), r2.x * ((cl & 4) ? 0 : 1));
+        float w[48], unused[48];
+#pragma unroll
+        for (int k = 0; k < nc; ++k) w[3 * k] = row[3 * k] * dc.x + row[3 * k + 1] * dc.y + row[3 * k + 2] * dc.z;
+        const float3 ddir = sh_channel_bwd(DEG, w, 1.f, dir.x, dir.y, dir.z, unused);
+        const float3 dmn = dnormvdv(dir_orig, ddir);
+        rec[2] = make_float4(r2.x, dmn.x, dmn.y, dmn.z);
+        sh_basis<DEG>(dir.x, dir.y, dir.z, B);
+    }
+    float* brow = basis_lds + lane * kBasisStride;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) brow[k] = k < nc ? B[k] : 0.f;
+    brow[16] = dc.x;
+    brow[17] = dc.y;
+    brow[18] = dc.z;
+    __syncthreads();
+    if (p.adam.dc.p) sh_region_adam_basis<3, 0>(p.adam.dc, p.adam, (long long)g0 * 3, rows, rows_lds, basis_lds);
+    else if (p.dsh_dc) sh_region_store_basis<3, 0>(p.dsh_dc + (size_t)g0 * 3, rows, basis_lds);
+    if (p.adam.rest.p)
+        sh_region_adam_basis<45, 3>(p.adam.rest, p.adam, (long long)g0 * 45, rows, rows_lds, basis_lds);
+    else if (p.dsh_rest)
+        sh_region_store_basis<45, 3>(p.dsh_rest + (size_t)g0 * 45, rows, basis_lds);
+}
+
 // The geometry half of the per-Gaussian backward: computeCov2DCUDA + preprocessCUDA bwd without the SH
 // (backward.cu:144-396); the view-direction term of dL/dmean3D comes from the record (k_preprocess_bwd_sh,
 // launched first; zeros when there is no SH operand).
@@ -1040,6 +1151,16 @@ void launch_preprocess_fwd(const PreprocessParams& p, hipStream_t s) {
 }
 template <bool kStr, int kSrc, bool kAcc>
 static void launch_bwd_sh(const PreprocessBwdParams& p, dim3 g, dim3 b, hipStream_t s) {
+    if (!kStr && !kAcc && kSrc == 1 && p.M == 16 && (p.adam.dc.p || p.adam.rest.p)) {  // fused Adam, params in LDS
+        const dim3 gw((p.P + kShWave - 1) / kShWave), bw(kShWave);
+        switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+            case 0: hipLaunchKernelGGL(k_preprocess_bwd_sh_adam<0>, gw, bw, 0, s, p); break;
+            case 1: hipLaunchKernelGGL(k_preprocess_bwd_sh_adam<1>, gw, bw, 0, s, p); break;
+            case 2: hipLaunchKernelGGL(k_preprocess_bwd_sh_adam<2>, gw, bw, 0, s, p); break;
+            default: hipLaunchKernelGGL(k_preprocess_bwd_sh_adam<3>, gw, bw, 0, s, p); break;
+        }
+        return;
+    }
     if (!kStr && !kAcc && kSrc != 0 && p.M == 16 && (p.adam.dc.p || p.adam.rest.p)) {  // fused Adam epilogue
         const dim3 gw((p.P + kShWave - 1) / kShWave), bw(kShWave);
         switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {

@@ -19,7 +19,7 @@
 // Backward: the reference issues 9 float atomicAdds per (pixel, Gaussian) pair
 // (backward.cu:523,545-554), all 256 lanes on the same address.  Here the work
 // per record is split in two phases.  Pixel-major: each lane replays its pixel
-// back to front and hands two numbers per record to LDS, G dL/dalpha and
+// back to front and hands two numbers per record to LDS, o G dL/dalpha and
 // alpha T.  Record-major: every one of the record's nine sums (dL/dmean2D,
 // dL/dconic, dL/dopacity, dL/dcolor) is a dot product of those two with
 // per-pixel factors (the pixel offsets and dL/dpixel), so a quad of lanes sums
@@ -157,10 +157,9 @@ __device__ __forceinline__ float4 fwd_group_rect(int g, float qx0, float qy0) { 
 }
 
 // Compaction into one list per lane group: lists[g] receives, in increasing slot order, the slots whose alpha
-// box meets group g's rectangle.  Returns the count of `mine` (the calling lane's group) and the maximum.
-__device__ __forceinline__ int2 wave_compact_groups(const float4* __restrict__ s_box, uint8_t (*lists)[kTilePix],
-                                                    int n, float qx0, float qy0, int lane) {
-    int cnt[kFwdGroups];
+// box meets group g's rectangle; cnt[g] its length (wave-uniform: popcounts of ballots, scalar registers).
+__device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s_box, uint8_t (*lists)[kTilePix],
+                                                    int n, float qx0, float qy0, int lane, int (&cnt)[kFwdGroups]) {
 #pragma unroll
     for (int g = 0; g < kFwdGroups; ++g) cnt[g] = 0;
 #pragma unroll
@@ -179,14 +178,6 @@ __device__ __forceinline__ int2 wave_compact_groups(const float4* __restrict__ s
         }
     }
     wave_lds_handoff();
-    const int me = lane / (64 / kFwdGroups);
-    int mine = cnt[0], mx = cnt[0];
-#pragma unroll
-    for (int g = 1; g < kFwdGroups; ++g) {
-        mine = me == g ? cnt[g] : mine;
-        mx = max(mx, cnt[g]);
-    }
-    return make_int2(mine, mx);
 }
 
 // List entries j0 .. j0 + 3 (j0 a multiple of 4) as one LDS word instead of four byte reads; entries at or past
@@ -296,11 +287,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             s_bo[tid] = make_float2(co.y, co.w);
             s_rgb[tid] = p.rgb[g];
             s_box[tid] = alpha_box(xy, co);
+        } else {  // slots past the tile's list: finite zeros (the walk below reads list bytes past a group's end)
+            s_pc[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            s_bo[tid] = make_float2(0.f, 0.f);
+            s_rgb[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
-        const int2 mm = wave_compact_groups(s_box, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane);
-        const int mine = mm.x, m = mm.y;  // this lane's group's list length, the longest
+        int cnt[kFwdGroups];  // the groups' list lengths (scalar)
+        wave_compact_groups(s_box, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane, cnt);
+        int m = cnt[0], mine = cnt[0];  // the longest; the calling lane's group's
+#pragma unroll
+        for (int g = 1; g < kFwdGroups; ++g) {
+            m = max(m, cnt[g]);
+            mine = tg.lane / (64 / kFwdGroups) == g ? cnt[g] : mine;
+        }
         for (int j0 = 0; j0 < m; j0 += kBatch) {
             if (done_m == ~0ull) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
@@ -309,12 +310,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             int slot[kBatch];
             static_assert(kBatch == 4, "one LDS word of list entries per batch");
             const uint32_t w4 = *reinterpret_cast<const uint32_t*>(list + j0);
-            unsigned long long in_m[kBatch];  // lanes whose group list holds entry j0 + u
+            // lanes whose group list holds entry j0 + u, built on the scalar unit from the groups' lengths.  A lane
+            // past its group's list reads whatever byte lies there -- a slot of this batch's staging, so every
+            // value read through it is finite -- and never takes it (the mask); no per-lane bounds select.
+            unsigned long long in_m[kBatch];
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
+#ifdef GSD_FWD_SCALAR_MASK
+                in_m[u] = 0;
+#pragma unroll
+                for (int g = 0; g < kFwdGroups; ++g)
+                    in_m[u] |= j0 + u < cnt[g] ? (~0ull >> (64 - 64 / kFwdGroups)) << (g * (64 / kFwdGroups)) : 0ull;
+#else
                 in_m[u] = wave_ballot(j0 + u < mine);
-                // past the list: slot 0, staged, so its colour is finite
-                slot[u] = __builtin_amdgcn_inverse_ballot_w64(in_m[u]) ? (int)((w4 >> (8 * u)) & 0xffu) : 0;
+#endif
+                slot[u] = (int)((w4 >> (8 * u)) & 0xffu);
                 float G;
                 a[u] = record_alpha(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, G, keep[u]);
             }
@@ -453,7 +463,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
                 // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
                 // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
-                // v = G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
+                // v = o G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
                 // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
                 // needed from the lane.
                 unsigned long long any_m = 0;  // lanes that took any record of the group
@@ -466,7 +476,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                         for (int u = 0; u < kBwdBatch; ++u) qa[sb * kBwdBatch + u][lane] = make_float2(0.f, 0.f);
                         continue;
                     }
-                    float Gs[kBwdBatch], As[kBwdBatch];
+                    float OGs[kBwdBatch];
                     bool keep[kBwdBatch];
                     int slot[kBwdBatch];
                     static_assert(kBwdBatch == 4, "one LDS word of list entries per batch");
@@ -477,19 +487,24 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
 #pragma unroll
                     for (int u = 0; u < kBwdBatch; ++u) {
                         slot[u] = list_slot(w4, u, jb, m);
-                        As[u] = record_alpha(s_pc[slot[u]], *reinterpret_cast<const float2*>(&s_bo[slot[u]]), pxf, pyf,
-                                             Gs[u], keep[u]);
+                        float G;
+                        const float2 bo = *reinterpret_cast<const float2*>(&s_bo[slot[u]]);
+                        record_alpha(s_pc[slot[u]], bo, pxf, pyf, G, keep[u]);
+                        OGs[u] = bo.y * G;  // o G: alpha before the 0.99 clamp (the same product)
                     }
 #pragma unroll
                     for (int u = 0; u < kBwdBatch; ++u) {
 #pragma clang fp contract(fast)
+                        // alpha = min(0.99, o G) >= 1/255 <=> !(o G < 1/255), NaN included (fminf(0.99, NaN) = 0.99)
                         const unsigned long long valid_m = (jb + u < m ? ~0ull : 0ull) &
                                                            wave_ballot(slot[u] > slot_min) & wave_ballot(keep[u]) &
-                                                           wave_ballot(As[u] >= 1.0f / 255.0f);
+                                                           wave_ballot(!(OGs[u] < 1.0f / 255.0f));
                         any_m |= valid_m;
                         const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
-                        const float alpha = valid ? As[u] : 0.f;
-                        const float G = valid ? Gs[u] : 0.f;
+                        // one select: o G zeroed where the lane skips the record gives alpha = 0 (T unchanged) and
+                        // a zero hand-off; the hand-off carries q = o G dL/dalpha (the flush no longer scales by o)
+                        const float og = valid ? OGs[u] : 0.f;
+                        const float alpha = fminf(0.99f, og);
                         const float inv1ma = fast_recip(1.f - alpha);
                         T = T * inv1ma;  // backward.cu:503 (T recovered by division)
                         const float4 c = s_rgb[slot[u]];
@@ -497,7 +512,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                         const float diff = cd - adot;
                         // backward.cu:512-529 (kbg = 0: fmaf(diff, T, -0) is diff * T, bit for bit)
                         const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
-                        qa[sb * kBwdBatch + u][lane] = make_float2(G * dL_dalpha, alpha * T);
+                        qa[sb * kBwdBatch + u][lane] = make_float2(og * dL_dalpha, alpha * T);
                         adot = fmaf(alpha, diff, adot);
                     }
                 }
@@ -558,14 +573,15 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float4 pc = s_pc[tid];
             const float2 bo = *reinterpret_cast<const float2*>(&s_bo[tid]);
             const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
-            const float o = co.w;  // the moments were summed over G dL/dalpha; q = o G dL/dalpha
+            const float o = co.w;  // the sums are over q = o G dL/dalpha; dL/dopacity = sum G dL/dalpha = S0 / o
             // phase 2 summed the first moments over x - mx, y - my: the reference's dx = mx - x flips them
-            const float m0 = -s_acc[0][tid] * o, m1 = -s_acc[1][tid] * o;
+            const float m0 = -s_acc[0][tid], m1 = -s_acc[1][tid];
             s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
             s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
-            s_acc[2][tid] *= -0.5f * o;
-            s_acc[3][tid] *= -0.5f * o;
-            s_acc[4][tid] *= -0.5f * o;
+            s_acc[2][tid] *= -0.5f;
+            s_acc[3][tid] *= -0.5f;
+            s_acc[4][tid] *= -0.5f;
+            s_acc[5][tid] = o > 0.f ? s_acc[5][tid] / o : 0.f;  // o = 0: alpha = 0, the record never took a pixel
         }
         lds_barrier();
         // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,

@@ -23,7 +23,7 @@ import torch
 
 from . import _native
 from ._C import _ptr, _stream
-from .parallel import broadcast_, data_parallel_world, view_stats_allreduce
+from .parallel import broadcast_, dp_active, view_stats_allreduce
 from .renderer import build_rotation, inverse_sigmoid
 
 _NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
@@ -62,7 +62,7 @@ class GaussianDensifier:
     def sync_stats(self):
         """Combine the per-rank statistics (no-op on one rank): afterwards every rank holds the statistics of
         all ranks' views."""
-        if data_parallel_world() > 1:
+        if dp_active():
             view_stats_allreduce(self.denom, self.xyz_gradient_accum, self.max_radii2D,
                                  self.xyz_gradient_accum_3vec)
 

@@ -17,7 +17,7 @@ import torch
 
 from . import _native
 from ._C import _ptr, _stream
-from .parallel import FlatGrads, data_parallel_world, slab_view
+from .parallel import FlatGrads, dp_active, slab_view
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -196,7 +196,7 @@ class FusedAdam(torch.optim.Optimizer):
         their slots filled -- or ``epi`` unchanged when the step cannot be fused here (world size > 1, a
         coefficient-major slab, a parameter this optimizer does not own or has already stepped).  ``summed``: the
         caller's gradient is already the sum over every rank (the exchanged SH views), so any world size fuses."""
-        if self.flat.epilogue is not self or (data_parallel_world() != 1 and not summed) or self.coef_major:
+        if self.flat.epilogue is not self or (dp_active() and not summed) or self.coef_major:
             return epi
         index = {id(p): i for i, p in enumerate(self._params)}
         if any(id(p) not in index or id(p) in self.flat.fused for p in named.values()):
@@ -222,7 +222,7 @@ class FusedAdam(torch.optim.Optimizer):
         per-rank gradients of ``params``: their all-reduce starts now (FlatGrads.early_allreduce), to run on the
         links while the device finishes the backward; ``allreduce_step`` then waits on it instead of issuing it.
         Inside the block a second producer of these gradients raises (it would miss the sum)."""
-        if self.flat.epilogue is not self or data_parallel_world() == 1:
+        if self.flat.epilogue is not self or not dp_active():
             return False
         index = {id(p) for p in self._params}
         if any(id(p) not in index or id(p) in self.flat.fused or id(p) in self.flat.early_ids for p in params):

@@ -29,7 +29,10 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or DP_ONE_RANK) and not dist.is_initialized():
+        if world == 1:   # GSD_DP_ONE_RANK without a launcher: a one-rank group on this host
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29571"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         # GSD_DIST_BACKEND=gloo: rehearse the data-parallel path with every rank on one GPU (gloo through host
         # memory; bench.py then maps LOCAL_RANK onto the devices present)
         backend = backend or os.environ.get("GSD_DIST_BACKEND") or None
@@ -68,9 +71,23 @@ SH_VIEWS = os.environ.get("GSD_SH_VIEWS", "1") != "0"   # exchange per-view dL/d
 BUCKET_FLOATS = int(float(os.environ.get("GSD_BUCKET_MB", "32")) * (1 << 20) / 4)
 
 
+# GSD_DP_ONE_RANK=1: a one-rank process group still takes the data-parallel path (the SH-view all-gather, the
+# early and bucketed all-reduces), so that path -- RCCL's streams and asynchronous works included -- runs on a
+# one-GPU box (tests/test_gpu_multiview.py::test_one_rank_rccl_matches_single_process)
+DP_ONE_RANK = os.environ.get("GSD_DP_ONE_RANK", "0") == "1"
+
+
 def data_parallel_world() -> int:
     """World size of the default process group (1 without torch.distributed)."""
     return dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def dp_active() -> bool:
+    """Whether the data-parallel path runs: a process group of more than one rank, or of one with
+    GSD_DP_ONE_RANK=1."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or DP_ONE_RANK
 
 
 def mark_reduced(params):
@@ -197,7 +214,7 @@ class FlatGrads:
         per-rank gradients (FusedAdam.step_in_backward guards them against a second producer), so that it runs
         on the links while the device computes what is left of the backward.  The views count as reduced for
         this step; allreduce / allreduce_buckets hand their works to the consumer instead of reducing again."""
-        if data_parallel_world() == 1:
+        if not dp_active():
             return
         ids = {id(p) for p in params}
         if not ids <= set(self._view_of) or ids & self.early_ids:
@@ -244,7 +261,7 @@ class FlatGrads:
         reduced, self.reduced = self.reduced | self.early_ids, set()
         early = [w for _, _, w in self.early if w is not None]
         self.early, self.early_ids = [], set()
-        if data_parallel_world() == 1:
+        if not dp_active():
             return None
         if not async_op:
             for w in early:
@@ -271,7 +288,7 @@ class FlatGrads:
         reduced, self.reduced = self.reduced | self.early_ids, set()
         early, self.early, self.early_ids = self.early, [], set()
         n = self.slab.numel()
-        if data_parallel_world() == 1:
+        if not dp_active():
             return [(0, n, None)]
         work = list(early)   # ranges whose all-reduce went out inside the backward (early_allreduce)
         nccl = dist.get_backend() == "nccl" or not self.slab.is_cuda
@@ -299,7 +316,7 @@ class FlatGrads:
 def allreduce_(t: torch.Tensor, op=None) -> torch.Tensor:
     """In-place all-reduce of ``t`` over the default group (no-op at world size 1); gloo with a device tensor
     (the tests) goes through host memory."""
-    if data_parallel_world() == 1:
+    if not dp_active():
         return t
     op = op or dist.ReduceOp.SUM
     if dist.get_backend() != "nccl" and t.is_cuda:
@@ -313,7 +330,7 @@ def allreduce_(t: torch.Tensor, op=None) -> torch.Tensor:
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     """In-place broadcast of ``t`` from rank ``src`` (no-op at world size 1)."""
-    if data_parallel_world() == 1:
+    if not dp_active():
         return t
     if dist.get_backend() != "nccl" and t.is_cuda:
         h = t.cpu()
@@ -329,7 +346,7 @@ def view_stats_allreduce(visible_count: torch.Tensor, grad2d_norm_sum: torch.Ten
     """Per-view densification statistics (gaussian_model.py:1252-1257, train.py:613),
     combined across ranks after each rank has accumulated its own views: sums for
     the counts / norm sums, max for the radii."""
-    if data_parallel_world() > 1:
+    if dp_active():
         allreduce_(visible_count)
         allreduce_(grad2d_norm_sum)
         if grad_3vec_sum is not None:

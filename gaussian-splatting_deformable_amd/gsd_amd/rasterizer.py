@@ -196,7 +196,7 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None, e
     sinks, acc = _sinks(ctx.params)
     offset = sh_offset if ctx.has_offset else None
     world = parallel.data_parallel_world()
-    if ctx.sh_views and world > 1 and sinks is not None and offset is None and parallel.SH_VIEWS:
+    if ctx.sh_views and parallel.dp_active() and sinks is not None and offset is None and parallel.SH_VIEWS:
         g_m2d, g_op, g_m3d, g_sc, g_rot = _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations,
                                                              radii, f_dc, f_rest, geomBuffer, binningBuffer,
                                                              imgBuffer, sinks, acc, world, activation, raw_opacity,

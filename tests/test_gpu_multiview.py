@@ -141,3 +141,60 @@ def test_two_ranks_overlapped_allreduce_adam_matches_one_process(tmp_path, mode)
         d = (got["p"] - want["p"]).abs()
         assert float(d.max()) <= 2 * 6e-3 + 1e-6
         assert float((d > 1e-6).float().mean()) <= 1e-4
+
+
+WORKER_ONE_RANK = r'''
+import os, sys
+sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting_deformable_amd"), ROOT]
+import torch, torch.distributed as dist
+from gsd_amd import DeformableGaussians, default_pipe, render
+from gsd_amd.camera import synthetic_camera
+from gsd_amd.optim import FusedAdam
+from gsd_amd.parallel import dp_active, init_from_env
+from gsd_amd.scene import make_gaussians
+
+rank, local, world = init_from_env()
+torch.cuda.set_device(0)
+assert dp_active() == (os.environ.get("GSD_DP_ONE_RANK") == "1")
+if dp_active():
+    assert dist.get_backend() == "nccl" and world == 1
+params = make_gaussians(20_000, 320, 240, seed=23, device="cuda:0")
+pc = DeformableGaussians(params, sh_degree=3)
+opt = FusedAdam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(pc.parameters())])
+w = torch.linspace(0.5, 1.5, 320, device="cuda:0")
+for it in range(3):
+    cam = synthetic_camera(320, 240, yaw_deg=3.0 * it).to("cuda:0")
+    with opt.step_in_backward():
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device="cuda:0"))
+        (out["render"] * w).sum().backward()
+torch.cuda.synchronize()
+if dist.is_initialized():
+    dist.destroy_process_group()
+torch.save({"p": opt.param_slab.cpu(), "m": opt.exp_avg.cpu(), "v": opt.exp_avg_sq.cpu()}, sys.argv[1])
+'''
+
+
+def test_one_rank_rccl_matches_single_process(tmp_path):
+    """GSD_DP_ONE_RANK=1: a one-rank RCCL group takes the whole data-parallel path of bench.py's step -- the
+    SH-view all_gather_into_tensor, gsd_sh_grad_views with the fused SH Adam, the early all-reduce of the raw
+    parameters inside the backward and the bucketed allreduce_step on leaving the block -- with real RCCL
+    collectives and their stream ordering, on one GPU.  Three steps must match the single-process path."""
+    script = tmp_path / "worker_one.py"
+    script.write_text("ROOT = %r\n" % ROOT + WORKER_ONE_RANK)
+    port = str(29400 + os.getpid() % 150)
+    base = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "GSD_DP_ONE_RANK")}
+    env_dp = dict(base, HSA_ENABLE_IPC_MODE_LEGACY="0", GSD_DP_ONE_RANK="1", MASTER_ADDR="127.0.0.1",
+                  MASTER_PORT=port, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r1 = subprocess.run([sys.executable, str(script), str(tmp_path / "dp.pt")], env=env_dp, timeout=300)
+    assert r1.returncode == 0
+    r2 = subprocess.run([sys.executable, str(script), str(tmp_path / "ref.pt")], env=dict(base), timeout=300)
+    assert r2.returncode == 0
+    got = torch.load(tmp_path / "dp.pt", weights_only=True)
+    want = torch.load(tmp_path / "ref.pt", weights_only=True)
+    for k in ("m", "v"):
+        assert torch.isfinite(got[k]).all()
+        rel = float((got[k] - want[k]).norm() / want[k].norm())
+        assert rel <= 1e-5, (k, rel)
+    d = (got["p"] - want["p"]).abs()
+    assert float(d.max()) <= 2 * 1.8e-2 + 1e-6
+    assert float((d > 1e-6).float().mean()) <= 1e-4
