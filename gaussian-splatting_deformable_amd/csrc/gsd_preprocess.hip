@@ -246,19 +246,25 @@ __device__ __forceinline__ void cov2d_bwd(const float3 mean, const Cov6& c3, flo
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     // T[col][row] accessors
     const float T00 = T.c[0].x, T01 = T.c[0].y, T02 = T.c[0].z, T10 = T.c[1].x, T11 = T.c[1].y, T12 = T.c[1].z;
-    if (denom2inv != 0) {
-        dL_da = denom2inv * (-c * c * dc.x + 2 * b * c * dc.y + (denom - a * c) * dc.z);
-        dL_dc = denom2inv * (-a * a * dc.z + 2 * a * b * dc.y + (denom - a * c) * dc.x);
-        dL_db = denom2inv * 2 * (b * c * dc.x - (denom + 2 * b * b) * dc.y + a * b * dc.z);
-        dcov.v[0] = (T00 * T00 * dL_da + T00 * T10 * dL_db + T10 * T10 * dL_dc);
-        dcov.v[3] = (T01 * T01 * dL_da + T01 * T11 * dL_db + T11 * T11 * dL_dc);
-        dcov.v[5] = (T02 * T02 * dL_da + T02 * T12 * dL_db + T12 * T12 * dL_dc);
-        dcov.v[1] = 2 * T00 * T01 * dL_da + (T00 * T11 + T01 * T10) * dL_db + 2 * T10 * T11 * dL_dc;
-        dcov.v[2] = 2 * T00 * T02 * dL_da + (T00 * T12 + T02 * T10) * dL_db + 2 * T10 * T12 * dL_dc;
-        dcov.v[4] = 2 * T02 * T01 * dL_da + (T01 * T12 + T02 * T11) * dL_db + 2 * T11 * T12 * dL_dc;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) dcov.v[i] = 0;
+    // backward.cu:204-228: everything stays 0 when denom2inv == 0 -- as selects, not a branch (the branch made the
+    // compiler keep dcov in scratch memory)
+    const bool inv_ok = denom2inv != 0;
+    dL_da = inv_ok ? denom2inv * (-c * c * dc.x + 2 * b * c * dc.y + (denom - a * c) * dc.z) : 0.f;
+    dL_dc = inv_ok ? denom2inv * (-a * a * dc.z + 2 * a * b * dc.y + (denom - a * c) * dc.x) : 0.f;
+    dL_db = inv_ok ? denom2inv * 2 * (b * c * dc.x - (denom + 2 * b * b) * dc.y + a * b * dc.z) : 0.f;
+    {
+        const float v0 = (T00 * T00 * dL_da + T00 * T10 * dL_db + T10 * T10 * dL_dc);
+        const float v3 = (T01 * T01 * dL_da + T01 * T11 * dL_db + T11 * T11 * dL_dc);
+        const float v5 = (T02 * T02 * dL_da + T02 * T12 * dL_db + T12 * T12 * dL_dc);
+        const float v1 = 2 * T00 * T01 * dL_da + (T00 * T11 + T01 * T10) * dL_db + 2 * T10 * T11 * dL_dc;
+        const float v2 = 2 * T00 * T02 * dL_da + (T00 * T12 + T02 * T10) * dL_db + 2 * T10 * T12 * dL_dc;
+        const float v4 = 2 * T02 * T01 * dL_da + (T01 * T12 + T02 * T11) * dL_db + 2 * T11 * T12 * dL_dc;
+        dcov.v[0] = inv_ok ? v0 : 0.f;
+        dcov.v[1] = inv_ok ? v1 : 0.f;
+        dcov.v[2] = inv_ok ? v2 : 0.f;
+        dcov.v[3] = inv_ok ? v3 : 0.f;
+        dcov.v[4] = inv_ok ? v4 : 0.f;
+        dcov.v[5] = inv_ok ? v5 : 0.f;
     }
     // Vrk[col][row]
     const float V00 = V.c[0].x, V01 = V.c[0].y, V02 = V.c[0].z, V10 = V.c[1].x, V11 = V.c[1].y, V12 = V.c[1].z,

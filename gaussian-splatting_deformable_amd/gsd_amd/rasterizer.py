@@ -227,6 +227,20 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None, e
     return g_m2d, d_dc, d_rest, d_off, (g_op, g_m3d, g_sc, g_rot)
 
 
+_VIEWS_ROW = {}
+
+
+def _views_row(P, dev):
+    """This rank's exchange row [d_rgb (P*3) | campos (3) | 0] (rasterizer._backward_sh_views), kept per (P, device):
+    the compute stream waits for each step's all-gather before it writes the row again."""
+    key = (P, str(dev))
+    row = _VIEWS_ROW.get(key)
+    if row is None:
+        _VIEWS_ROW.clear()
+        row = _VIEWS_ROW[key] = torch.zeros(3 * P + 4, dtype=torch.float32, device=dev)
+    return row
+
+
 def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radii, f_dc, f_rest, geomBuffer,
                        binningBuffer, imgBuffer, sinks, acc, world, activation=None, raw_opacity=None, raw=()):
     """Data-parallel backward of the split-SH rasterizer with the SH gradient exchanged per view: this rank's
@@ -238,9 +252,8 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
     import torch.distributed as dist
     P, dev = int(f_dc.size(0)), f_dc.device
     stride = 3 * P + 4
-    row = torch.empty(stride, dtype=torch.float32, device=dev)
+    row = _views_row(P, dev)   # its pad float was zeroed once; the previous step's all-gather is done with it
     row[3 * P:3 * P + 3].copy_(rs.campos.reshape(-1))
-    row[3 * P + 3:].zero_()
     split = _C.ShSplit(f_dc, f_rest, None, None, None, None, accumulate=False, d_rgb=row[:3 * P])
     g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
