@@ -55,6 +55,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a, float* __restrict__ pa
     const long long stride = (long long)gridDim.x * 256;
     const bool aligned = ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+    // the addend's quads line up with the slab's when its first element sits on a quad boundary of both
+    const bool add_aligned = a.addend && (a.addend_lo & 3) == 0 && (reinterpret_cast<uintptr_t>(a.addend) & 15) == 0;
+    const float4* A4 = reinterpret_cast<const float4*>(a.addend);
     float4* P4 = reinterpret_cast<float4*>(param);
     float4* G4 = reinterpret_cast<float4*>(grad);
     float4* M4 = reinterpret_cast<float4*>(m);
@@ -69,13 +72,20 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a, float* __restrict__ pa
             qs[u] = q0 + u * stride;
             const long long i0 = qs[u] * 4;
             gs[u] = group_of(a, i0);
+            // a quad with addend elements takes the vector path only when all four have one (quad-aligned)
+            const bool add_none = !a.addend || i0 + 4 <= a.addend_lo || i0 >= a.addend_hi;
+            const bool add_all = add_aligned && i0 >= a.addend_lo && i0 + 4 <= a.addend_hi;
             whole[u] = aligned && qs[u] < nq && i0 + 4 <= a.n &&
-                       (gs[u] + 1 >= a.n_groups || i0 + 4 <= a.begin[gs[u] + 1]);
+                       (gs[u] + 1 >= a.n_groups || i0 + 4 <= a.begin[gs[u] + 1]) && (add_none || add_all);
             if (whole[u]) {
                 p4[u] = ld(P4 + qs[u]);
                 g4[u] = ld(G4 + qs[u]);
                 m4[u] = ld(M4 + qs[u]);
                 v4[u] = ld(V4 + qs[u]);
+                if (add_all) {
+                    const float4 e = ld(A4 + (i0 - a.addend_lo) / 4);
+                    g4[u] = make_float4(g4[u].x + e.x, g4[u].y + e.y, g4[u].z + e.z, g4[u].w + e.w);
+                }
             }
         }
 #pragma unroll
@@ -91,7 +101,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a, float* __restrict__ pa
                 for (long long i = i0; i < i0 + 4 && i < a.n; ++i) {
                     const int g = group_of(a, i);
                     float pp = param[i], mm = m[i], vv = v[i];
-                    adam_elem(pp, grad[i], mm, vv, a.w1, a.beta2, a.omb2, a.step_size[g], a.bc2_sqrt[g], a.eps);
+                    const float gi = a.addend && i >= a.addend_lo && i < a.addend_hi
+                                         ? grad[i] + a.addend[i - a.addend_lo] : grad[i];
+                    adam_elem(pp, gi, mm, vv, a.w1, a.beta2, a.omb2, a.step_size[g], a.bc2_sqrt[g], a.eps);
                     param[i] = pp;
                     m[i] = mm;
                     v[i] = vv;

@@ -566,6 +566,7 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
         p.dL_dsh = nullptr; p.dsh_dc = sp->d_dc; p.dsh_rest = sp->d_rest; p.dsh_off = sp->d_offset;
         p.sh_accumulate = sp->accumulate;
         p.d_rgb = sp->d_rgb;
+        p.defer_view_dir = sp->d_rgb && sp->defer_view_dir;
     }
     set_sh_strides(p, a->sh_split, a->M);
     if (act) {
@@ -585,6 +586,14 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
 int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
                       int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
                       const gsd_sh_split* layout, const gsd_adam_epilogue* adam, void* stream) {
+    return gsd_sh_grad_views_ex(P, D, M, n_views, means3D, views, view_stride, nullptr, nullptr, d_dc, d_rest,
+                                d_offset, nullptr, accumulate, layout, adam, stream);
+}
+
+int gsd_sh_grad_views_ex(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
+                         int64_t view_stride, const float* sh_dc, const float* sh_rest, float* d_dc, float* d_rest,
+                         float* d_offset, float* d_means, int32_t accumulate, const gsd_sh_split* layout,
+                         const gsd_adam_epilogue* adam, void* stream) {
     if (P < 0 || n_views < 0 || M < 1 || M < (D + 1) * (D + 1))
         return fail(GSD_ERR_ARG, "sh_grad_views: need P >= 0, n_views >= 0, M >= (D+1)^2");
     if (view_stride < 3 * (int64_t)P + 3) return fail(GSD_ERR_ARG, "sh_grad_views: view_stride < 3 P + 3");
@@ -595,6 +604,13 @@ int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const fl
     p.means3D = means3D; p.views = views; p.d_dc = d_dc; p.d_rest = d_rest; p.d_off = d_offset;
     p.accumulate = accumulate;
     set_sh_strides(p, layout, M);
+    if (d_means) {
+        const bool contiguous = p.dc_sg == 3 && p.dc_se == 1 && p.rest_sg == 3LL * (M - 1) && p.rest_se == 1;
+        if (!sh_dc || !sh_rest || M != 16 || accumulate || !contiguous || d_offset)
+            return fail(GSD_ERR_ARG, "sh_grad_views d_means: needs sh_dc and sh_rest, M = 16, accumulate 0, "
+                                     "contiguous pieces and no offset sink");
+        p.sh_dc = sh_dc; p.sh_rest = sh_rest; p.d_means = d_means;
+    }
     if (adam && (adam->dc.param || adam->rest.param)) {
         const bool contiguous = p.dc_sg == 3 && p.dc_se == 1 && p.rest_sg == 3LL * (M - 1) && p.rest_se == 1;
         if (accumulate || M != 16 || !contiguous)
@@ -770,8 +786,18 @@ int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, cons
 int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
                   const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
                   double beta2, double eps, int32_t zero_grad, void* stream) {
+    return gsd_adam_step_ex(n, param, grad, exp_avg, exp_avg_sq, n_groups, group_begin, group_lr, group_step, beta1,
+                            beta2, eps, zero_grad, nullptr, 0, 0, stream);
+}
+
+int gsd_adam_step_ex(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
+                     const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
+                     double beta2, double eps, int32_t zero_grad, const float* addend, int64_t addend_begin,
+                     int64_t addend_end, void* stream) {
     if (n < 0 || n_groups < 1 || n_groups > gsd::kAdamMaxGroups)
         return fail(GSD_ERR_ARG, "adam: need n >= 0 and 1 <= n_groups <= 16");
+    if (addend && (addend_begin < 0 || addend_end < addend_begin || addend_end > n))
+        return fail(GSD_ERR_ARG, "adam: need 0 <= addend_begin <= addend_end <= n");
     if (n == 0) return GSD_OK;
     if (!param || !grad || !exp_avg || !exp_avg_sq || !group_begin || !group_lr || !group_step)
         return fail(GSD_ERR_ARG, "null pointer argument");
@@ -795,6 +821,11 @@ int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* e
     a.beta2 = (float)beta2;          // _foreach_mul_(exp_avg_sqs, beta2)
     a.omb2 = (float)(1.0 - beta2);   // _foreach_addcmul_(exp_avg_sqs, grads, grads, 1 - beta2)
     a.eps = (float)eps;
+    if (addend && addend_end > addend_begin) {
+        a.addend = addend;
+        a.addend_lo = addend_begin;
+        a.addend_hi = addend_end;
+    }
     hipStream_t s = as_stream(stream);
     timed(kAdam, s, [&] { gsd::launch_adam(a, param, grad, exp_avg, exp_avg_sq, s); });
     GSD_CHECK(false, s);

@@ -112,6 +112,7 @@ struct PreprocessBwdParams {
     float* dsh_off;
     int sh_accumulate;
     float* d_rgb;          // (P,3) masked dL/dRGB instead of the SH sinks (gsd_sh_split.d_rgb), or NULL
+    int defer_view_dir;    // with d_rgb: no SH half; the geometry half writes d_rgb, without the view-dir term
     int raw_act;           // raw parameters: gradients go to the sinks below (gsd_activation)
     const float* raw_opacity;
     float *a_xyz, *a_scaling, *a_rotation, *a_opacity;
@@ -230,6 +231,9 @@ struct ShViewsParams {
     long long dc_sg, dc_se, rest_sg, rest_se;
     int accumulate;
     AdamEpiDev adam;  // fused Adam epilogue for dc / rest (rows kernel, store mode), p == nullptr: off
+    const float* sh_dc;    // the SH coefficients (contiguous, M = 16) for d_means, else unused
+    const float* sh_rest;
+    float* d_means;        // (P,3): the views' summed view-direction term (gsd_sh_grad_views_ex), or nullptr
 };
 void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t s);
@@ -264,6 +268,8 @@ struct AdamArgs {
     float step_size[kAdamMaxGroups];    // -lr / (1 - beta1^t)
     float bc2_sqrt[kAdamMaxGroups];     // sqrt(1 - beta2^t)
     float w1, beta2, omb2, eps;         // 1 - beta1, beta2, 1 - beta2, eps
+    const float* addend;                // nullptr, or elements [addend_lo, addend_hi) step on grad + addend
+    long long addend_lo, addend_hi;
 };
 void launch_adam(const AdamArgs& a, float* param, float* grad, float* m, float* v, hipStream_t s);
 

@@ -916,6 +916,12 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams& p,
         p.dL_dcolor[3 * idx + 1] = z(r1.w);
         p.dL_dcolor[3 * idx + 2] = z(r2.x);
     }
+    if (p.defer_view_dir) {  // no SH half ran: this view's row of the exchanged SH factor, masked as it masks it
+        const uint8_t cl = p.clamped[idx];
+        p.d_rgb[3 * idx] = (cl & 1) ? 0.f : z(r1.z);
+        p.d_rgb[3 * idx + 1] = (cl & 2) ? 0.f : z(r1.w);
+        p.d_rgb[3 * idx + 2] = (cl & 4) ? 0.f : z(r2.x);
+    }
     float3 dmean;
     Cov6 dcov;
     cov2d_bwd(m, c3, p.focal_x, p.focal_y, p.tan_fovx, p.tan_fovy, Vm, make_float3(r0.z, r0.w, r1.x), dmean, dcov);
@@ -1078,6 +1084,112 @@ __global__ __launch_bounds__(256) void k_sh_grad_views(ShViewsParams p) {
     }
 }
 
+// With d_means (gsd_sh_grad_views_ex; store mode, contiguous pieces, M = 16): the views' summed view-direction
+// term of the SH colour, which the backwards of a defer_view_dir exchange left out of dL/dmeans3D -- per view v,
+// dnormvdv(m - campos_v, sum_k w_k grad B_k(dir_v)) with w_k = sh_k . d_rgb_v (k_preprocess_bwd_sh_rows's
+// expressions).  The coefficients are staged once into the LDS rows; before the rows take the assembled
+// gradient, every lane copies the coefficients of the region elements it will step into registers, so the Adam
+// pass reads no parameter from HBM and one 12.5-KB LDS buffer serves both (a second buffer for the gradient
+// halved the workgroups per CU: 0.242 ms against 0.197 for k_sh_grad_views_rows at one view).
+template <int R, int C0>
+__device__ __forceinline__ void region_params_to_regs(const float* __restrict__ prm, float (&pre)[R]) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int el = i * kShWave + (int)threadIdx.x;
+        const int gi = el / R, j = el - gi * R;
+        pre[i] = prm[gi * kShRowStride + C0 + j];
+    }
+}
+template <int R>
+__device__ __forceinline__ void sh_region_adam_regs(const AdamSinkDev& sk, const AdamEpiDev& e, long long base,
+                                                    int rows, const float (&pre)[R], const float* __restrict__ grd,
+                                                    int c0) {
+    constexpr int kCh = R < 15 ? R : 15;
+    static_assert(R % kCh == 0, "whole chunks");
+    const int lane = threadIdx.x, n = rows * R;
+    float* __restrict__ P = sk.p + base;
+    float* __restrict__ Mo = sk.m + base;
+    float* __restrict__ V = sk.v + base;
+#pragma unroll
+    for (int c = 0; c < R; c += kCh) {
+        float g[kCh], pp[kCh], mm[kCh], vv[kCh];
+        bool in[kCh];
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+            const int el = (c + i) * kShWave + lane;
+            const int gi = el / R, j = el - gi * R;
+            in[i] = rows == kShWave || el < n;
+            g[i] = grd[gi * kShRowStride + c0 + j];
+            pp[i] = pre[c + i];
+            mm[i] = in[i] ? __builtin_nontemporal_load(Mo + el) : 0.f;
+            vv[i] = in[i] ? __builtin_nontemporal_load(V + el) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+            adam_elem(pp[i], g[i], mm[i], vv[i], e.w1, e.beta2, e.omb2, sk.step_size, sk.bc2_sqrt, e.eps);
+            const int el = (c + i) * kShWave + lane;
+            if (in[i]) {
+                P[el] = pp[i];
+                __builtin_nontemporal_store(mm[i], Mo + el);
+                __builtin_nontemporal_store(vv[i], V + el);
+            }
+        }
+    }
+}
+template <int DEG>
+__global__ __launch_bounds__(kShWave) void k_sh_grad_views_dir(ShViewsParams p) {
+    __shared__ float rows_lds[kShWave * kShRowStride];  // the SH coefficients (dc | rest), then the gradient
+    constexpr int M = 16, nc = (DEG + 1) * (DEG + 1);
+    const int g0 = blockIdx.x * kShWave, lane = threadIdx.x, idx = g0 + lane;
+    const int rows = min(kShWave, p.P - g0);
+    sh_region_load<3, 0>(p.sh_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    sh_region_load<3 * (M - 1), 0>(p.sh_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+    __syncthreads();
+    float* row = rows_lds + lane * kShRowStride;
+    float acc[48];
+#pragma unroll
+    for (int k = 0; k < 48; ++k) acc[k] = 0.f;
+    if (idx < p.P) {
+        sh_views_sum<DEG>(p, idx, acc);
+        const float* s = row;  // the coefficients straight from the LDS row (48 registers fewer: occupancy)
+        const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
+        float3 dm = make_float3(0.f, 0.f, 0.f);
+        for (int v = 0; v < p.n_views; ++v) {
+            const float* vrow = p.views + (size_t)v * (size_t)p.view_stride;
+            const float* cam = vrow + (size_t)p.P * 3;
+            const float3 g = make_float3(vrow[3 * idx], vrow[3 * idx + 1], vrow[3 * idx + 2]);
+            const float3 d0 = make_float3(m.x - cam[0], m.y - cam[1], m.z - cam[2]);
+            const float len = sqrtf(dot3(d0, d0));
+            // a view that culled this Gaussian (zero row) adds nothing (and a mean at its centre no NaN)
+            if ((g.x == 0.f && g.y == 0.f && g.z == 0.f) || !(len > 0.f)) continue;
+            const float3 dir = make_float3(d0.x / len, d0.y / len, d0.z / len);
+            float w[48], unused[48];
+#pragma unroll
+            for (int k = 0; k < nc; ++k) w[3 * k] = s[3 * k] * g.x + s[3 * k + 1] * g.y + s[3 * k + 2] * g.z;
+            const float3 ddir = sh_channel_bwd(DEG, w, 1.f, dir.x, dir.y, dir.z, unused);
+            const float3 dmn = dnormvdv(d0, ddir);
+            dm = make_float3(dm.x + dmn.x, dm.y + dmn.y, dm.z + dmn.z);
+        }
+        p.d_means[3 * idx] = dm.x;
+        p.d_means[3 * idx + 1] = dm.y;
+        p.d_means[3 * idx + 2] = dm.z;
+    }
+    const bool adam_dc = p.adam.dc.p != nullptr, adam_rest = p.adam.rest.p != nullptr;
+    float pre_dc[3], pre_rest[3 * (M - 1)];
+    if (adam_dc) region_params_to_regs<3, 0>(rows_lds, pre_dc);
+    if (adam_rest) region_params_to_regs<3 * (M - 1), 3>(rows_lds, pre_rest);
+    __syncthreads();  // every coefficient read: the rows take the gradient
+#pragma unroll
+    for (int k = 0; k < 3 * M; ++k) row[k] = k < 3 * nc ? acc[k] : 0.f;  // zero above the active degree
+    __syncthreads();
+    if (adam_dc) sh_region_adam_regs<3>(p.adam.dc, p.adam, (long long)g0 * 3, rows, pre_dc, rows_lds, 0);
+    else if (p.d_dc) sh_region_store<3, false>(p.d_dc + (size_t)g0 * 3, rows, rows_lds, 0);
+    if (adam_rest)
+        sh_region_adam_regs<3 * (M - 1)>(p.adam.rest, p.adam, (long long)g0 * 3 * (M - 1), rows, pre_rest, rows_lds, 3);
+    else if (p.d_rest)
+        sh_region_store<3 * (M - 1), false>(p.d_rest + (size_t)g0 * 3 * (M - 1), rows, rows_lds, 3);
+}
+
 // The same with coalesced sinks (contiguous rows, M = 16): one wave per 64 Gaussians, the sums through LDS rows
 // and out as lane-consecutive region stores (the SH half of the backward's scheme).
 template <int DEG, bool kAcc>
@@ -1115,6 +1227,16 @@ static void launch_sh_views_rows(const ShViewsParams& p, hipStream_t s) {
 }
 void launch_sh_grad_views(const ShViewsParams& p, hipStream_t s) {
     if (p.P <= 0) return;
+    if (p.d_means) {  // gsd_sh_grad_views_ex checked the layout (contiguous, M = 16, store mode)
+        const dim3 g((p.P + kShWave - 1) / kShWave), b(kShWave);
+        switch (p.D <= 0 ? 0 : (p.D >= 3 ? 3 : p.D)) {
+            case 0: hipLaunchKernelGGL(k_sh_grad_views_dir<0>, g, b, 0, s, p); break;
+            case 1: hipLaunchKernelGGL(k_sh_grad_views_dir<1>, g, b, 0, s, p); break;
+            case 2: hipLaunchKernelGGL(k_sh_grad_views_dir<2>, g, b, 0, s, p); break;
+            default: hipLaunchKernelGGL(k_sh_grad_views_dir<3>, g, b, 0, s, p); break;
+        }
+        return;
+    }
 #ifndef GSD_SH_VIEWS_LANE
     const bool rows = p.M == 16 && (!p.d_dc || (p.dc_sg == 3 && p.dc_se == 1)) &&
                       (!p.d_rest || (p.rest_sg == 3LL * (p.M - 1) && p.rest_se == 1));
@@ -1199,7 +1321,7 @@ static void launch_bwd_sh(const PreprocessBwdParams& p, dim3 g, dim3 b, hipStrea
 template <bool kStr>
 static void launch_bwd(const PreprocessBwdParams& p, hipStream_t s) {
     const dim3 g((p.P + 255) / 256), b(256);
-    if (p.shs || p.sh_dc) {
+    if ((p.shs || p.sh_dc) && !p.defer_view_dir) {
         const int src = p.shs ? 0 : (p.sh_off ? 2 : 1);
         const bool acc = p.sh_accumulate != 0 && !p.shs;
         if (src == 0) launch_bwd_sh<kStr, 0, false>(p, g, b, s);

@@ -66,7 +66,8 @@ class ShSplit:
     additive offset (P,1+R,3) read in place instead of shs = cat(dc, rest) + offset; for the backward,
     the gradient sinks (any may be None) and whether they are added into (accumulate) or stored."""
 
-    def __init__(self, dc, rest, offset=None, d_dc=None, d_rest=None, d_offset=None, accumulate=False, d_rgb=None):
+    def __init__(self, dc, rest, offset=None, d_dc=None, d_rest=None, d_offset=None, accumulate=False, d_rgb=None,
+                 defer_view_dir=False):
         dev = dc.device
         # dc / rest may be strided (P,K,3) views -- e.g. FusedAdam's coefficient-major slabs -- as long as the
         # element e = 3 k + c sits at g * stride(0) + e * stride(2); anything else is copied contiguous
@@ -90,7 +91,7 @@ class ShSplit:
                                  d_offset=_ptr(self.sinks[2]).value, accumulate=int(bool(accumulate)),
                                  d_rgb=_ptr(d_rgb).value, dc_stride_g=(dcs or (0, 0))[0],
                                  dc_stride_e=(dcs or (0, 0))[1], rest_stride_g=(rs or (0, 0))[0],
-                                 rest_stride_e=(rs or (0, 0))[1])
+                                 rest_stride_e=(rs or (0, 0))[1], defer_view_dir=int(bool(defer_view_dir)))
 
 
 def _sh_strides(t):
@@ -249,21 +250,31 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 
 
 def sh_grad_views(D, means3D, views, P, M, d_dc=None, d_rest=None, d_offset=None, accumulate=False, layout=None,
-                  adam=None):
-    """gsd_sh_grad_views: the SH gradient summed over the views whose rows views (n_views, view_stride) hold
+                  adam=None, sh=None, d_means=None):
+    """gsd_sh_grad_views(_ex): the SH gradient summed over the views whose rows views (n_views, view_stride) hold
     [masked dL/dRGB (P*3) | campos (3) | pad] -> written into / added to the given sinks (or, for the pieces
-    ``adam`` (a _native.AdamEpilogue) names, their Adam step applied in place)."""
+    ``adam`` (a _native.AdamEpilogue) names, their Adam step applied in place).  ``d_means`` (P,3): also the
+    views' summed view-direction term that a defer_view_dir backward left out of dL/dmeans3D, from the SH
+    coefficients ``sh`` = (features_dc, features_rest) the views rendered."""
     lib = _native.load()
     dev = means3D.device
     if views.dim() != 2 or not views.is_contiguous() or views.dtype != torch.float32 or views.device != dev:
         raise RuntimeError("sh_grad_views: views must be a contiguous (n_views, stride) float32 device tensor")
     m = _dev_f32(means3D, "means3D", dev)
+    lay = None if layout is None else ctypes.byref(layout.c)
+    ad = None if adam is None else ctypes.byref(adam)
     with torch.cuda.device(dev):
-        _native.check(lib.gsd_sh_grad_views(int(P), int(D), int(M), int(views.size(0)), _ptr(m), _ptr(views),
-                                            int(views.size(1)), _ptr(d_dc), _ptr(d_rest), _ptr(d_offset),
-                                            int(bool(accumulate)),
-                                            None if layout is None else ctypes.byref(layout.c),
-                                            None if adam is None else ctypes.byref(adam), _stream(dev)))
+        if d_means is None:
+            _native.check(lib.gsd_sh_grad_views(int(P), int(D), int(M), int(views.size(0)), _ptr(m), _ptr(views),
+                                                int(views.size(1)), _ptr(d_dc), _ptr(d_rest), _ptr(d_offset),
+                                                int(bool(accumulate)), lay, ad, _stream(dev)))
+            return
+        if sh is None or not all(t.is_contiguous() for t in sh) or not d_means.is_contiguous():
+            raise RuntimeError("sh_grad_views: d_means needs the contiguous SH pieces sh=(dc, rest)")
+        _native.check(lib.gsd_sh_grad_views_ex(int(P), int(D), int(M), int(views.size(0)), _ptr(m), _ptr(views),
+                                               int(views.size(1)), _ptr(sh[0]), _ptr(sh[1]), _ptr(d_dc),
+                                               _ptr(d_rest), _ptr(d_offset), _ptr(d_means), int(bool(accumulate)),
+                                               lay, ad, _stream(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -25,7 +25,7 @@ class ShSplit(ctypes.Structure):
 
     _fields_ = [("dc", _vp), ("rest", _vp), ("offset", _vp), ("d_dc", _vp), ("d_rest", _vp), ("d_offset", _vp),
                 ("accumulate", _i32), ("d_rgb", _vp), ("dc_stride_g", _i64), ("dc_stride_e", _i64),
-                ("rest_stride_g", _i64), ("rest_stride_e", _i64)]
+                ("rest_stride_g", _i64), ("rest_stride_e", _i64), ("defer_view_dir", _i32)]
 
 
 class Activation(ctypes.Structure):
@@ -75,6 +75,8 @@ SIGNATURES = {
     "gsd_rasterize_forward_render": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gsd_rasterize_forward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _sz, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "gsd_sh_grad_views": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "gsd_sh_grad_views_ex": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                                    _vp, _vp]),
     "gsd_rasterize_backward": (_i32, [ctypes.POINTER(RasterArgs), _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_mark_visible": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp]),
@@ -87,6 +89,9 @@ SIGNATURES = {
     "gsd_l1_ssim_backward": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _f32, _vp, _vp, _vp]),
     "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32),
                              ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32, _vp]),
+    "gsd_adam_step_ex": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32),
+                                ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32, _vp,
+                                _i64, _i64, _vp]),
     "gsd_densify_stats": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_knn_workspace_bytes": (_sz, [_i32]),
     "gsd_knn_mean_dist2": (_i32, [_i32, _vp, _vp, _vp, _vp]),

@@ -92,10 +92,11 @@ class FusedAdam(torch.optim.Optimizer):
             self.steps[i] += 1
         return set(active)
 
-    def _adam(self, a: int, b: int, active):
+    def _adam(self, a: int, b: int, active, addends=()):
         """gsd_adam_step over slab elements [a, b) of the parameters in ``active``: one launch per contiguous
         run of them (parameters without a gradient are left out, untouched), each run cut into segments of equal
-        (learning rate, step count), at most 16 per launch."""
+        (learning rate, step count), at most 16 per launch.  ``addends``: [(lo, hi, tensor)] slab ranges whose
+        gradient steps with the tensor added (FlatGrads.addend_ranges; gsd_adam_step_ex)."""
         segs = []   # [begin, end, lr, step]
         for i, (pb, pe) in enumerate(self._span):
             lo, hi = max(pb, a), min(pe, b)
@@ -121,14 +122,30 @@ class FusedAdam(torch.optim.Optimizer):
             for run in runs:
                 r0, r1 = run[0][0], run[-1][1]
                 k = len(run)
-                _native.check(lib.gsd_adam_step(
-                    r1 - r0, ctypes.c_void_p(self.param_slab.data_ptr() + f4 * r0),
-                    ctypes.c_void_p(self.flat.slab.data_ptr() + f4 * r0),
-                    ctypes.c_void_p(self.exp_avg.data_ptr() + f4 * r0),
-                    ctypes.c_void_p(self.exp_avg_sq.data_ptr() + f4 * r0), k,
-                    (ctypes.c_int64 * k)(*[sg[0] - r0 for sg in run]), (ctypes.c_float * k)(*[sg[2] for sg in run]),
-                    (ctypes.c_int64 * k)(*[sg[3] for sg in run]), float(beta1), float(beta2), float(g0["eps"]), 0,
-                    _stream(dev)))
+                # at most one addend per launch: a run holding more is cut at the second one's start
+                pieces, cuts = [], sorted(lo for lo, hi, _ in addends if r0 < hi and lo < r1)
+                bounds = [r0] + [c for c in cuts[1:] if r0 < c < r1] + [r1]
+                for q0, q1 in zip(bounds[:-1], bounds[1:]):
+                    pieces.append((q0, q1))
+                for q0, q1 in pieces:
+                    segs_q = [[max(sg[0], q0), min(sg[1], q1), sg[2], sg[3]] for sg in run if sg[0] < q1 and q0 < sg[1]]
+                    kq = len(segs_q)
+                    add = next(((lo, hi, t) for lo, hi, t in addends if q0 < hi and lo < q1), None)
+                    a_ptr, a_lo, a_hi = None, 0, 0
+                    if add is not None:
+                        lo, hi, t = add
+                        s0 = max(lo, q0)
+                        a_ptr = ctypes.c_void_p(t.data_ptr() + f4 * (s0 - lo))
+                        a_lo, a_hi = s0 - q0, min(hi, q1) - q0
+                    _native.check(lib.gsd_adam_step_ex(
+                        q1 - q0, ctypes.c_void_p(self.param_slab.data_ptr() + f4 * q0),
+                        ctypes.c_void_p(self.flat.slab.data_ptr() + f4 * q0),
+                        ctypes.c_void_p(self.exp_avg.data_ptr() + f4 * q0),
+                        ctypes.c_void_p(self.exp_avg_sq.data_ptr() + f4 * q0), kq,
+                        (ctypes.c_int64 * kq)(*[sg[0] - q0 for sg in segs_q]),
+                        (ctypes.c_float * kq)(*[sg[2] for sg in segs_q]),
+                        (ctypes.c_int64 * kq)(*[sg[3] for sg in segs_q]), float(beta1), float(beta2),
+                        float(g0["eps"]), 0, a_ptr, a_lo, a_hi, _stream(dev)))
 
     @torch.no_grad()
     def step(self, closure=None, zero_grad: bool = False):
@@ -138,7 +155,7 @@ class FusedAdam(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         self.flat.collect()
         active = self._advance(self.flat.settle())
-        self._adam(0, self.param_slab.numel(), active)
+        self._adam(0, self.param_slab.numel(), active, self.flat.addend_ranges())
         if zero_grad:
             self.flat.invalidate()
         return loss
@@ -154,14 +171,15 @@ class FusedAdam(torch.optim.Optimizer):
         parameters (as DistributedDataParallel requires), or their step counts diverge."""
         from .parallel import BUCKET_FLOATS
         ranges = self.flat.allreduce_buckets(bucket_floats or BUCKET_FLOATS)
+        addends = self.flat.addend_ranges()   # rank-summed terms (the exchanged views' mean term): added in the pass
         active = self._advance(self.flat.missing, self.flat.fused)
         for a, b, w in ranges:        # ranges with nothing to wait for first
             if w is None:
-                self._adam(a, b, active)
+                self._adam(a, b, active, addends)
         for a, b, w in ranges:
             if w is not None:
                 w.wait()
-                self._adam(a, b, active)
+                self._adam(a, b, active, addends)
         if zero_grad:
             self.flat.invalidate()
 

@@ -126,6 +126,7 @@ class FlatGrads:
         self.reduced = set()   # views already summed over the ranks this step (mark_reduced)
         self.early = []        # [(a, b, work)]: all-reduces issued inside the backward (early_allreduce)
         self.early_ids = set()
+        self.addends = {}      # id(p) -> tensor: a gradient term already summed over the ranks (add_after_reduce)
         self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
         self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
         self.attach()
@@ -162,6 +163,7 @@ class FlatGrads:
         self.slab.zero_()
         self.stale.clear()
         self.reduced = set()
+        self.addends = {}
         self.attach()
 
     def invalidate(self):
@@ -169,7 +171,34 @@ class FlatGrads:
         self.drain_early()
         self.stale = {id(p) for p in self.params}
         self.reduced = set()
+        self.addends = {}
         self._version = self.slab._version
+
+    def add_after_reduce(self, p, t):
+        """A term of ``p``'s gradient that is already the sum over every rank (gsd_sh_grad_views_ex's view-direction
+        term of the means, from the exchanged SH views): it joins the gradient after the all-reduce of the ranks'
+        own parts -- added by ``allreduce``, or handed to the consumer of ``allreduce_buckets`` (FusedAdam adds it
+        inside its Adam pass: addend_ranges)."""
+        if id(p) not in self._view_of or id(p) in self.addends:
+            raise RuntimeError("add_after_reduce: parameter not in this slab, or already given an addend this step")
+        if t.numel() != p.numel() or not t.is_contiguous() or t.dtype != torch.float32:
+            raise RuntimeError("add_after_reduce: the addend must be a contiguous float32 tensor of p's size")
+        self.addends[id(p)] = t
+
+    def addend_ranges(self):
+        """[(a, b, tensor)]: the slab ranges of the pending addends (consumed: the caller adds them)."""
+        out, off = [], 0
+        for p, v in zip(self.params, self.views):
+            n = v.numel()
+            if id(p) in self.addends:
+                out.append((off, off + n, self.addends[id(p)].reshape(-1)))
+            off += n
+        self.addends = {}
+        return out
+
+    def _apply_addends(self):
+        for a, b, t in self.addend_ranges():
+            self.slab[a:b].add_(t)
 
     def claim(self, params) -> bool:
         """A fused backward is about to produce the gradients of ``params`` in place: True = add into the
@@ -262,7 +291,10 @@ class FlatGrads:
         early = [w for _, _, w in self.early if w is not None]
         self.early, self.early_ids = [], set()
         if not dp_active():
+            self._apply_addends()
             return None
+        if async_op and self.addends:
+            raise RuntimeError("FlatGrads.allreduce(async_op=True): pending addends need the reduced sums first")
         if not async_op:
             for w in early:
                 w.wait()
@@ -272,9 +304,13 @@ class FlatGrads:
                 h = self.slab[a:b].cpu()
                 dist.all_reduce(h, op=op or dist.ReduceOp.SUM)
                 self.slab[a:b].copy_(h)
+            self._apply_addends()
             return None
         works = [dist.all_reduce(self.slab[a:b], op=op or dist.ReduceOp.SUM, async_op=async_op) for a, b in runs]
-        return early + works if async_op else None
+        if async_op:
+            return early + works
+        self._apply_addends()
+        return None
 
     def allreduce_buckets(self, bucket_floats: int = BUCKET_FLOATS):
         """The all-reduce of ``allreduce`` issued asynchronously in buckets of at most ``bucket_floats``, for
@@ -282,7 +318,8 @@ class FlatGrads:
         (FusedAdam.allreduce_step).  Returns [(a, b, work)] covering the whole slab in order: work is None for
         a range that needs no reduction (world size 1, or views already summed) or was reduced synchronously
         (gloo); otherwise the caller waits on it (``work.wait()`` only orders the current stream behind the
-        collective, the host does not block)."""
+        collective, the host does not block).  Pending addends (add_after_reduce) stay for the caller:
+        ``addend_ranges``."""
         self.collect()
         self.settle()
         reduced, self.reduced = self.reduced | self.early_ids, set()

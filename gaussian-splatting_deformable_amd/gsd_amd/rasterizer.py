@@ -241,6 +241,20 @@ def _views_row(P, dev):
     return row
 
 
+_VIEWS_MEANS = {}
+
+
+def _views_means(P, dev):
+    """The views' summed view-direction term of the means (gsd_sh_grad_views_ex d_means), kept per (P, device):
+    the step's Adam pass (or FlatGrads.allreduce) consumes it before the next backward writes it."""
+    key = (P, str(dev))
+    t = _VIEWS_MEANS.get(key)
+    if t is None:
+        _VIEWS_MEANS.clear()
+        t = _VIEWS_MEANS[key] = torch.empty(P, 3, dtype=torch.float32, device=dev)
+    return t
+
+
 def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radii, f_dc, f_rest, geomBuffer,
                        binningBuffer, imgBuffer, sinks, acc, world, activation=None, raw_opacity=None, raw=()):
     """Data-parallel backward of the split-SH rasterizer with the SH gradient exchanged per view: this rank's
@@ -254,7 +268,17 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
     stride = 3 * P + 4
     row = _views_row(P, dev)   # its pad float was zeroed once; the previous step's all-gather is done with it
     row[3 * P:3 * P + 3].copy_(rs.campos.reshape(-1))
-    split = _C.ShSplit(f_dc, f_rest, None, None, None, None, accumulate=False, d_rgb=row[:3 * P])
+    # defer_view_dir: the raw path, whose xyz gradient is a FlatGrads view -- the backward then reads no SH
+    # coefficient (no SH half at all) and gsd_sh_grad_views_ex adds every view's view-direction term of the means
+    # after the all-reduce (FlatGrads.add_after_reduce); elsewhere (an autograd consumer of dL/dmeans3D) this
+    # rank's own term stays in its backward
+    xyz = raw[0] if raw else None
+    flat = getattr(xyz, "_gsd_flat", None)
+    defer = (activation is not None and flat is not None and not acc and xyz.grad is not None
+             and activation.d_xyz == xyz.grad.data_ptr() and f_dc.is_contiguous() and f_rest.is_contiguous()
+             and int(f_rest.size(1)) == 15)
+    split = _C.ShSplit(f_dc, f_rest, None, None, None, None, accumulate=False, d_rgb=row[:3 * P],
+                       defer_view_dir=defer)
     g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
@@ -277,8 +301,11 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
     owner = FusedAdam.fused_owner(ctx.params) if not acc else None
     if owner is not None and f_dc.is_contiguous() and f_rest.is_contiguous():
         epi = owner.fuse({"dc": f_dc, "rest": f_rest}, summed=True)   # every view's sum: final on every rank
+    d_means = _views_means(P, dev) if defer else None
     _C.sh_grad_views(rs.sh_degree, means3D, views, P, 1 + int(f_rest.size(1)), d_dc=sinks[0], d_rest=sinks[1],
-                     accumulate=acc, layout=split, adam=epi)
+                     accumulate=acc, layout=split, adam=epi, sh=(f_dc, f_rest), d_means=d_means)
+    if defer:
+        flat.add_after_reduce(xyz, d_means)
     if epi is not None:
         for p in (f_dc, f_rest):
             torch.autograd.graph.increment_version(p)

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 8
+#define GSD_ABI_VERSION 9
 
 enum {
     GSD_OK = 0,
@@ -81,6 +81,10 @@ typedef struct gsd_sh_split {
                                              Coefficient-major storage (stride_g 1, stride_e P: what
                                              gsd_amd.optim.FusedAdam lays out) makes every SH access of a
                                              wave one contiguous 256-B run instead of 64 rows */
+    int32_t defer_view_dir;  /* ABI 9, with d_rgb: 1 = the backward reads no SH coefficient at all -- it writes
+                                the d_rgb row and leaves the view-direction term of the SH colour
+                                (backward.cu:385-392) out of dL/dmeans3D; gsd_sh_grad_views_ex supplies that
+                                term summed over the exchanged views (d_means).  0 = the term is included. */
 } gsd_sh_split;
 
 /* Optional activation of the per-Gaussian inputs inside the rasterizer (the render() preamble without
@@ -219,6 +223,16 @@ int gsd_rasterize_backward(const gsd_raster_args* args, const int32_t* radii, co
 int gsd_sh_grad_views(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
                       int64_t view_stride, float* d_dc, float* d_rest, float* d_offset, int32_t accumulate,
                       const gsd_sh_split* layout, const gsd_adam_epilogue* adam, void* stream);
+/* gsd_sh_grad_views plus, when d_means != NULL, the view-direction term of the SH colour that a backward with
+ * gsd_sh_split.defer_view_dir left out of dL/dmeans3D, summed over the views (ABI 9):
+ *   d_means[g] = sum_v dnormvdv(means3D[g] - campos_v, sum_c d_rgb_v[g][c] dRGB_c/ddir_v)   (backward.cu:385-392)
+ * stored (P,3).  It needs the SH coefficients every view rendered: sh_dc (P,1,3) and sh_rest (P,M-1,3),
+ * contiguous, M = 16, accumulate 0 (the layout of the training path); with the fused Adam step the coefficients
+ * are read once for both uses. */
+int gsd_sh_grad_views_ex(int32_t P, int32_t D, int32_t M, int32_t n_views, const float* means3D, const float* views,
+                         int64_t view_stride, const float* sh_dc, const float* sh_rest, float* d_dc, float* d_rest,
+                         float* d_offset, float* d_means, int32_t accumulate, const gsd_sh_split* layout,
+                         const gsd_adam_epilogue* adam, void* stream);
 
 /* Near-plane visibility test (auxiliary.h:139-164): present[i] = 1/0. */
 int gsd_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
@@ -288,6 +302,14 @@ int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, cons
 int gsd_adam_step(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
                   const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
                   double beta2, double eps, int32_t zero_grad, void* stream);
+/* gsd_adam_step with an addend (ABI 9): elements i in [addend_begin, addend_end) of this call step on
+ * grad[i] + addend[i - addend_begin] -- a gradient term that arrives already summed over the data-parallel
+ * ranks (gsd_sh_grad_views_ex's d_means) and so must not go through their all-reduce.  addend NULL: as
+ * gsd_adam_step. */
+int gsd_adam_step_ex(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq, int32_t n_groups,
+                     const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
+                     double beta2, double eps, int32_t zero_grad, const float* addend, int64_t addend_begin,
+                     int64_t addend_end, void* stream);
 
 /* Per-view densification statistics (train.py:613-616, scene/gaussian_model.py:1252-1257): for every
  * Gaussian with radii > 0, max_radii2D = max(max_radii2D, radii); grad_accum_3vec += viewspace_grad;

@@ -500,3 +500,32 @@ def test_step_in_backward_rejects_second_producer():
         (out["render"].sum() + 1e-3 * pc._scaling.square().sum()).backward()
         opt.allreduce_step(zero_grad=True)
         assert all(bool(torch.isfinite(p).all()) for p in pc.parameters())
+
+
+def test_fused_adam_addend_matches_torch_adam():
+    """FlatGrads.add_after_reduce (a gradient term already summed over the ranks: the exchanged views' mean term,
+    gsd_sh_grad_views_ex d_means): FusedAdam steps on grad + addend inside its pass (gsd_adam_step_ex), for
+    parameters whose slab range starts on and off a quad boundary, against torch.optim.Adam on the sum."""
+    from gsd_amd.optim import FusedAdam
+    gen = torch.Generator().manual_seed(9)
+    shapes = [(333, 3), (250, 1), (101, 4)]   # the second and third start off a quad boundary of the slab
+    init = [torch.randn(*s, generator=gen) for s in shapes]
+    a = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    b = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    opt_a = FusedAdam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(a)], lr=0.0, eps=1e-15)
+    opt_b = torch.optim.Adam([{"params": [p], "lr": 1e-3 * (i + 1)} for i, p in enumerate(b)], lr=0.0, eps=1e-15,
+                             foreach=True)
+    for k in range(2):
+        gs = [torch.randn(*s, generator=gen) for s in shapes]
+        adds = [torch.randn(*s, generator=gen) * 0.5 for s in shapes]
+        for p, g in zip(a, gs):
+            p.grad.copy_(g.to(DEV))
+        for i in (0, 2):                       # two of the three take an addend
+            opt_a.flat.add_after_reduce(a[i], adds[i].to(DEV).contiguous())
+        for i, (p, g) in enumerate(zip(b, gs)):
+            p.grad = (g + adds[i]).to(DEV) if i in (0, 2) else g.to(DEV)
+        opt_a.step(zero_grad=True)
+        opt_b.step()
+    for pa, pb in zip(a, b):
+        assert float((pa - pb).abs().max()) <= 1e-6
+    assert opt_a.flat.addends == {}

@@ -252,3 +252,56 @@ def test_two_rank_densify_keeps_replicas_identical(tmp_path):
         a0, a1 = got[0][f"arr_{i}"], got[1][f"arr_{i}"]
         assert np.array_equal(a0, a1), i
         np.testing.assert_allclose(a0, p.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+def _worker_addend(rank, world, port, out_dir):
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd.parallel import FlatGrads, init_from_env
+    r, _, w = init_from_env(backend="gloo")
+    grads = view_grads(yaw=2.0 * r)
+    params = [torch.nn.Parameter(torch.zeros(g.shape)) for g in grads]
+    fg = FlatGrads(params, device="cpu")
+    addend = torch.from_numpy(np.random.default_rng(3).standard_normal(grads[0].shape).astype(np.float32))
+    for sync in (True, False):
+        for p, g in zip(params, grads):
+            p.grad.copy_(torch.from_numpy(g))
+        fg.add_after_reduce(params[0], addend.clone())   # the same all-rank total on every rank
+        try:
+            fg.add_after_reduce(params[0], addend.clone())
+            raise AssertionError("a second addend for one parameter did not raise")
+        except RuntimeError:
+            pass
+        if sync:   # allreduce adds it once, after the sum
+            fg.allreduce()
+            np.save(os.path.join(out_dir, f"arank{r}.npy"), fg.slab.numpy())
+        else:      # allreduce_buckets leaves it to the consumer (FusedAdam passes it to its Adam pass)
+            for _, _, wk in fg.allreduce_buckets(bucket_floats=500):
+                if wk is not None:
+                    wk.wait()
+            (a, b, t), = fg.addend_ranges()
+            assert (a, b) == (0, params[0].numel()) and fg.addends == {}
+            np.save(os.path.join(out_dir, f"brank{r}.npy"), fg.slab.numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_addend_joins_after_the_sum(tmp_path):
+    """FlatGrads.add_after_reduce (the exchanged views' summed mean term, already an all-rank total): the
+    synchronous allreduce adds it once after summing the ranks' own gradients; allreduce_buckets sums the
+    ranks' parts only and hands the addend's slab range to its consumer."""
+    world = 2
+    mp.spawn(_worker_addend, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    views = [np.concatenate([g.reshape(-1) for g in view_grads(2.0 * r)]) for r in range(world)]
+    plain = sum(views)
+    addend = np.random.default_rng(3).standard_normal(view_grads(0.0)[0].shape).astype(np.float32).reshape(-1)
+    with_add = plain.copy()
+    with_add[:addend.size] += addend
+    for r in range(world):
+        np.testing.assert_allclose(np.load(os.path.join(str(tmp_path), f"arank{r}.npy")), with_add, rtol=1e-5,
+                                   atol=1e-6)
+        np.testing.assert_allclose(np.load(os.path.join(str(tmp_path), f"brank{r}.npy")), plain, rtol=1e-5,
+                                   atol=1e-6)
