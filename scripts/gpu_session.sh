@@ -1,5 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_multiview.py tests/test_gpu_parity.py -k "views or rank or ranks" -p no:cacheprovider > gpurun_out/t9.log 2>&1; rc=$?; tail -3 gpurun_out/t9.log; [ $rc -ne 0 ] && exit $rc
-export GSD_DP_ONE_RANK=1
-timeout -k 10 300 python bench.py --steps 50 --warmup 5 --cpu-baseline off > gpurun_out/dp9.log 2>&1; rc=$?; grep metric gpurun_out/dp9.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernels_ms'])"; exit $rc
+timeout -k 10 600 python bench.py > gpurun_out/bench_v29.log 2>&1; rc=$?; tail -1 gpurun_out/bench_v29.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof29" -o bench -- python bench.py --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/prof29.log 2>&1; rc=$?; [ $rc -ne 0 ] && exit $rc
+f=$(find gpurun_out/prof29 -name "*kernel_trace.csv" | head -1); python scripts/trace_gaps.py "$f" > gpurun_out/step_trace_v29.txt; tail -3 gpurun_out/step_trace_v29.txt

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Idle gaps between consecutive kernels of a rocprofv3 kernel trace (one bench step, the last complete one
 between two launches of the step's last kernel: the SH backward with the fused Adam epilogue, or the
-separate Adam kernel of the unfused step): prints each kernel's start offset, duration and the gap before it.
+separate Adam kernel of the unfused and the data-parallel steps): prints each kernel's start offset, duration and the gap before it.
     python scripts/trace_gaps.py gpurun_out/prof/bench_kernel_trace.csv"""
 import csv
 import sys
@@ -9,7 +9,8 @@ import sys
 
 def main(path):
     r = sorted(csv.DictReader(open(path)), key=lambda x: int(x["Start_Timestamp"]))
-    last = lambda n: "k_adam" in n or ("k_preprocess_bwd_sh_rows" in n and "true>" in n)  # noqa: E731
+    last = lambda n: ("k_adam" in n or "k_preprocess_bwd_sh_adam" in n  # noqa: E731
+                      or ("k_preprocess_bwd_sh_rows" in n and "true>" in n))
     idx = [i for i, x in enumerate(r) if last(x["Kernel_Name"])]
     a, b = idx[-2], idx[-1]
     t_prev = int(r[a]["End_Timestamp"])
