@@ -49,8 +49,7 @@ char* align_ptr(void* p) { return reinterpret_cast<char*>(up(reinterpret_cast<ui
 
 struct Geom {
     float2* means2D;
-    float4* conic_opacity;
-    float4* rgb;
+    gsd::RenderRec* rec;
     float* depths;
     int* radii;
     uint8_t* clamped;
@@ -67,8 +66,9 @@ void hist_shape(size_t P, int* chunk, int* nblocks) {
     *nblocks = (int)((P + *chunk - 1) / *chunk);
 }
 // GeometryState (rasterizer_impl.h:29-41), re-laid out: what render gathers per
-// instance (xy, conic/opacity, rgb) is 16-B aligned; cov3D is recomputed in
-// the backward instead of stored; no P-wide scan space is needed.
+// instance (xy, conic/opacity, rgb, and the alpha box) is one 64-B record per
+// Gaussian; means2D stays a separate array for the binning; cov3D is recomputed
+// in the backward instead of stored; no P-wide scan space is needed.
 size_t carve_geom(void* base, size_t P, size_t T, Geom* g) {
     char* p = base ? align_ptr(base) : nullptr;
     size_t off = 0;
@@ -79,8 +79,7 @@ size_t carve_geom(void* base, size_t P, size_t T, Geom* g) {
     };
     Geom v;
     v.means2D = reinterpret_cast<float2*>(take(P * sizeof(float2)));
-    v.conic_opacity = reinterpret_cast<float4*>(take(P * sizeof(float4)));
-    v.rgb = reinterpret_cast<float4*>(take(P * sizeof(float4)));
+    v.rec = reinterpret_cast<gsd::RenderRec*>(take(P * sizeof(gsd::RenderRec)));
     v.depths = reinterpret_cast<float*>(take(P * sizeof(float)));
     v.radii = reinterpret_cast<int*>(take(P * sizeof(int)));
     v.clamped = reinterpret_cast<uint8_t*>(take(P));
@@ -334,7 +333,8 @@ void gsd_state_layout(int32_t P, int32_t width, int32_t height, int64_t K, size_
     carve_img(base, (size_t)width * (size_t)height, gx * gy, &im);
     carve_bin(base, (size_t)(K < 0 ? 0 : K), &b);
     if (go) {
-        go[0] = off(g.means2D); go[1] = off(g.conic_opacity); go[2] = off(g.rgb);
+        // conic + opacity and rgb live in the 64-B render records: offsets of the first record's fields
+        go[0] = off(g.means2D); go[1] = off(g.rec) + 8; go[2] = off(g.rec) + 24;
         go[3] = off(g.depths); go[4] = off(g.radii); go[5] = off(g.clamped);
     }
     if (io) {
@@ -376,7 +376,7 @@ static int enqueue_bin(const gsd_raster_args* a, void* geom_buffer, void* image_
     p.view = a->viewmatrix; p.proj = a->projmatrix; p.campos = a->campos;
     p.raw_act = a->activation != nullptr;
     p.radii = radii ? radii : g.radii;
-    p.means2D = g.means2D; p.depths = g.depths; p.conic_opacity = g.conic_opacity; p.rgb = g.rgb;
+    p.means2D = g.means2D; p.depths = g.depths; p.rec = g.rec;
     p.clamped = g.clamped; p.tile_count = use_hist ? nullptr : im.tile_count; p.err_flags = im.counters + 1;
     timed(kPreFwd, s, [&] { gsd::launch_preprocess_fwd(p, s); });
     GSD_CHECK(a->debug, s);
@@ -457,8 +457,8 @@ static int enqueue_render(const gsd_raster_args* a, void* geom_buffer, void* ima
     }
     gsd::RenderParams rp{};
     rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
-    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
-    rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
+    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.rec = g.rec;
+    rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
     rp.out_color = out_color;
     rp.k_guard = k_guard; rp.k_cap = cap;
     timed(kRenderFwd, s, [&] { gsd::launch_render_fwd(rp, s); });
@@ -539,8 +539,8 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
 
     gsd::RenderBwdParams rp{};
     rp.W = a->width; rp.H = a->height; rp.grid_x = gx; rp.num_tiles = T;
-    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.means2D = g.means2D; rp.conic_opacity = g.conic_opacity;
-    rp.rgb = g.rgb; rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
+    rp.ranges = im.ranges; rp.point_list = b.point_list; rp.rec = g.rec;
+    rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
     rp.dL_dpix = dL_dout_color;
     // the per-Gaussian gradient records (scratch) start at zero; render_bwd adds into them
     float* rec = reinterpret_cast<float*>(align_ptr(scratch));

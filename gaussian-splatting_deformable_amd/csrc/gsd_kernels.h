@@ -16,6 +16,35 @@ namespace gsd {
 
 enum : uint32_t { kErrPrefiltered = 1u };
 
+// What the render kernels stage per gathered instance, one 64-B record per Gaussian (k_preprocess_fwd writes it
+// for the visible ones; point_list references no other): one 64-B fetch per instance instead of three from the
+// separate xy, conic + opacity and rgb arrays (the render kernels' FETCH_SIZE was 3.4x their algorithmic bytes),
+// and the alpha box computed once per Gaussian instead of per instance in both passes.
+// Bounding box (x0, x1, y0, y1) of {d : alpha(d) >= 1/255} for a record, inflated for safety.
+// Q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o); half-widths sqrt(t c/det), sqrt(t a/det).
+__device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    const float det = a * c - b * b;
+    const float lo = 255.0f * o;
+    if (!(lo >= 0.999f)) return make_float4(1e30f, -1e30f, 1e30f, -1e30f);  // alpha < 1/255 everywhere (or NaN)
+    if (!(det > 0.0f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f); // degenerate: never cull
+    const float t = 2.0f * 0.69314718f * __builtin_amdgcn_logf(lo);     // 2 ln(255 o), v_log_f32 = log2
+    // hardware sqrt / reciprocal (1 ulp): far inside the 0.1 % inflation
+    const float rdet = __builtin_amdgcn_rcpf(det);
+    const float ex = __builtin_amdgcn_sqrtf(fmaxf(t, 0.f) * c * rdet) * 1.001f + 0.02f;
+    const float ey = __builtin_amdgcn_sqrtf(fmaxf(t, 0.f) * a * rdet) * 1.001f + 0.02f;
+    if (!(ex < 1e30f) || !(ey < 1e30f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
+    return make_float4(xy.x - ex, xy.x + ex, xy.y - ey, xy.y + ey);
+}
+
+struct RenderRec {
+    float4 q0;   // mean2D x, y, conic a, b
+    float4 q1;   // conic c, opacity, r, g
+    float4 q2;   // b, 0, 0, 0
+    float4 box;  // alpha_box(): x0, x1, y0, y1
+};
+static_assert(sizeof(RenderRec) == 64, "one 64-B segment per record");
+
 struct PreprocessParams {
     int P, D, M, W, H, grid_x, grid_y, prefiltered;
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
@@ -36,8 +65,7 @@ struct PreprocessParams {
     int* radii;
     float2* means2D;
     float* depths;
-    float4* conic_opacity;
-    float4* rgb;
+    RenderRec* rec;        // what the render kernels gather per instance (written for visible Gaussians)
     uint8_t* clamped;
     uint32_t* tile_count;
     uint32_t* err_flags;
@@ -149,9 +177,7 @@ struct RenderParams {
     int W, H, grid_x, num_tiles;
     const uint2* ranges;
     const uint32_t* point_list;
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float4* rgb;
+    const RenderRec* rec;
     const float* bg;
     float* final_T;
     uint32_t* n_contrib;
@@ -164,9 +190,7 @@ struct RenderBwdParams {
     int W, H, grid_x, num_tiles;
     const uint2* ranges;
     const uint32_t* point_list;
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float4* rgb;
+    const RenderRec* rec;
     const float* bg;
     const float* final_T;
     const uint32_t* n_contrib;

@@ -194,12 +194,16 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
         col = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
     }
     p.clamped[idx] = cl;
-    p.rgb[idx] = col;
     p.depths[idx] = pv.z;
     p.radii[idx] = (int)my_radius;
     p.means2D[idx] = pix;
     const float opac = p.raw_act ? act_opac(p.opacities[idx]) : p.opacities[idx];
-    p.conic_opacity[idx] = make_float4(conic.x, conic.y, conic.z, opac);
+    const float4 co = make_float4(conic.x, conic.y, conic.z, opac);
+    RenderRec* rr = p.rec + idx;  // what the render kernels gather per instance (RenderRec)
+    rr->q0 = make_float4(pix.x, pix.y, co.x, co.y);
+    rr->q1 = make_float4(co.z, co.w, col.x, col.y);
+    rr->q2 = make_float4(col.z, 0.f, 0.f, 0.f);
+    rr->box = alpha_box(pix, co);
     // per-tile instance counts by global atomics -- only on the fallback path for very
     // large tile grids; normally k_tile_hist builds them from LDS histograms instead
     if (!p.tile_count) return;

@@ -3,8 +3,8 @@
 //
 // One 256-lane workgroup per 16x16 tile; each wave64 owns one 8x8 quadrant.
 // The tile's depth-sorted record list (point_list) is streamed through LDS
-// 256 records at a time (xy, conic+opacity, rgb, and the record's alpha
-// bounding box: 56 B/record, broadcast reads).
+// 256 records at a time, each staged from its Gaussian's 64-B RenderRec (xy,
+// conic+opacity, rgb and the alpha bounding box the preprocess computed).
 //
 // Wave-level culling: a record can only change a pixel where
 // alpha = o*exp(-Q/2) >= 1/255, i.e. inside the ellipse Q <= 2 ln(255 o)
@@ -41,23 +41,6 @@ constexpr int kBatch = 4;
 // saves -- 0.306 vs 0.289 ms per 8x8 quadrant, 0.366 vs 0.261 per 4x4 lane group)
 constexpr int kBwdBatch = 4;  // backward: records whose alphas are evaluated together
 constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
-
-// Bounding box of {d : alpha(d) >= 1/255} for a record, inflated for safety.
-// Q(d) = a dx^2 + 2 b dx dy + c dy^2 <= t = 2 ln(255 o); half-widths sqrt(t c/det), sqrt(t a/det).
-__device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
-    const float a = co.x, b = co.y, c = co.z, o = co.w;
-    const float det = a * c - b * b;
-    const float lo = 255.0f * o;
-    if (!(lo >= 0.999f)) return make_float4(1e30f, -1e30f, 1e30f, -1e30f);  // alpha < 1/255 everywhere (or NaN)
-    if (!(det > 0.0f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f); // degenerate: never cull
-    const float t = 2.0f * 0.69314718f * __builtin_amdgcn_logf(lo);     // 2 ln(255 o), v_log_f32 = log2
-    // hardware sqrt / reciprocal (1 ulp): far inside the 0.1 % inflation
-    const float rdet = __builtin_amdgcn_rcpf(det);
-    const float ex = __builtin_amdgcn_sqrtf(fmaxf(t, 0.f) * c * rdet) * 1.001f + 0.02f;
-    const float ey = __builtin_amdgcn_sqrtf(fmaxf(t, 0.f) * a * rdet) * 1.001f + 0.02f;
-    if (!(ex < 1e30f) || !(ey < 1e30f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
-    return make_float4(xy.x - ex, xy.x + ex, xy.y - ey, xy.y + ey);
-}
 
 // Does the ellipse {d : Q(d) <= t} around (mx, my) meet the rectangle [x0, x1] x [y0, y1]?
 // Q(d) = a dx^2 + 2 b dx dy + c dy^2 (positive definite: a, c > 0, det > 0).  Q is convex, so its minimum
@@ -280,13 +263,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         if (__syncthreads_count(__builtin_amdgcn_inverse_ballot_w64(done_m)) == kTilePix) break;
         const int k = (int)rg.x + i * kTilePix + tid;
         if (k < (int)rg.y) {
-            const uint32_t g = p.point_list[k];
-            const float2 xy = p.means2D[g];
-            const float4 co = p.conic_opacity[g];
-            s_pc[tid] = stage_pc(xy, co);
-            s_bo[tid] = make_float2(co.y, co.w);
-            s_rgb[tid] = p.rgb[g];
-            s_box[tid] = alpha_box(xy, co);
+            const RenderRec* r = p.rec + p.point_list[k];  // one 64-B record per gathered instance
+            const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
+            s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
+            s_bo[tid] = make_float2(q0.w, q1.y);
+            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, 0.f);
+            s_box[tid] = r->box;
         } else {  // slots past the tile's list: finite zeros (the walk below reads list bytes past a group's end)
             s_pc[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
             s_bo[tid] = make_float2(0.f, 0.f);
@@ -438,13 +420,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         const int progress = i * kTilePix + tid;
         if (progress < total) {  // loaded back to front (backward.cu:466-478)
             const uint32_t g = p.point_list[end - progress - 1];
-            const float2 xy = p.means2D[g];
-            const float4 co = p.conic_opacity[g];
+            const RenderRec* r = p.rec + g;
+            const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
             s_id[tid] = g;
-            s_pc[tid] = stage_pc(xy, co);
-            s_bo[tid] = make_float4(co.y, co.w, 0.f, 0.f);
-            s_rgb[tid] = p.rgb[g];
-            s_box[tid] = alpha_box(xy, co);
+            s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
+            s_bo[tid] = make_float4(q0.w, q1.y, 0.f, 0.f);
+            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, 0.f);
+            s_box[tid] = r->box;
         }
 #pragma unroll
         for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;

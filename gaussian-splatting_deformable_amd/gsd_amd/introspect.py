@@ -34,8 +34,9 @@ def decode(P, W, H, num_rendered, geom, binning, img):
     K = int(num_rendered)
     out = dict(
         means2D=_view(geom, gb + go[0], torch.float32, P, 2),
-        conic_opacity=_view(geom, gb + go[1], torch.float32, P, 4),
-        rgb=_view(geom, gb + go[2], torch.float32, P, 4)[:, :3],
+        # conic + opacity and rgb sit inside the 64-B render records (16 floats per Gaussian)
+        conic_opacity=_view(geom, gb + go[1] - 8, torch.float32, P, 16)[:, 2:6],
+        rgb=_view(geom, gb + go[2] - 24, torch.float32, P, 16)[:, 6:9],
         depths=_view(geom, gb + go[3], torch.float32, P),
         radii_internal=_view(geom, gb + go[4], torch.int32, P),
         clamped=_view(geom, gb + go[5], torch.uint8, P),

@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 600 python bench.py > gpurun_out/bench_v29.log 2>&1; rc=$?; tail -1 gpurun_out/bench_v29.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc
-export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof29" -o bench -- python bench.py --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/prof29.log 2>&1; rc=$?; [ $rc -ne 0 ] && exit $rc
-f=$(find gpurun_out/prof29 -name "*kernel_trace.csv" | head -1); python scripts/trace_gaps.py "$f" > gpurun_out/step_trace_v29.txt; tail -3 gpurun_out/step_trace_v29.txt
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ -p no:cacheprovider > gpurun_out/t16.log 2>&1; rc=$?; tail -3 gpurun_out/t16.log; [ $rc -ne 0 ] && exit $rc
+RENDER=1 ITERS=30 bash scripts/ab_bench.sh > gpurun_out/ab16r.log 2>&1 || exit 1
+grep -E "==|render_|preprocess_fwd" gpurun_out/ab16r.log
+BENCH_ARGS="--steps 100 --warmup 10" bash scripts/ab_bench.sh > gpurun_out/ab16.log 2>&1; rc=$?; grep -E "==|views" gpurun_out/ab16.log; exit $rc

@@ -48,8 +48,12 @@ def test_state_layout_is_aligned_and_disjoint():
     lib.gsd_state_layout(1001, 333, 217, 12345, go, io, bo)
     # binning: point_list first (the backward's part, at a K-independent offset), then keys, scratch
     for arr in (list(go), list(io), [bo[2], bo[0], bo[1]]):
-        assert all(o % 256 == 0 for o in arr)
         assert arr == sorted(arr) and len(set(arr)) == len(arr)
+    # conic + opacity and rgb are fields of the 64-B render records (one 256-aligned array)
+    assert go[1] - 8 == go[2] - 24 and (go[1] - 8) % 256 == 0
+    assert go[3] - (go[1] - 8) >= 64 * 1001
+    for arr in ([go[0], go[3], go[4], go[5]], list(io), list(bo)):
+        assert all(o % 256 == 0 for o in arr)
     assert bo[2] == 0
     assert go[5] + 1001 <= lib.gsd_geom_buffer_bytes(1001, 333, 217) - 256
 
