@@ -40,7 +40,7 @@ __device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
 struct RenderRec {
     float4 q0;   // mean2D x, y, conic a, b
     float4 q1;   // conic c, opacity, r, g
-    float4 q2;   // b, 0, 0, 0
+    float4 q2;   // b, the backward culling's ellipse threshold (slack included), 1 / a, 1 / c
     float4 box;  // alpha_box(): x0, x1, y0, y1
 };
 static_assert(sizeof(RenderRec) == 64, "one 64-B segment per record");

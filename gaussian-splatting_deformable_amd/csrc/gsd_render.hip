@@ -52,12 +52,12 @@ __device__ __forceinline__ float edge_min_x(float a, float b, float c, float rc,
     const float dy = fminf(fmaxf(-b * dx * rc, dy0), dy1);
     return a * dx * dx + 2.f * b * dx * dy + c * dy * dy;
 }
-__device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t, float x0, float x1, float y0,
-                                                   float y1) {
+// ra, rc: the hardware reciprocals of a and c (RenderRec.q2, computed once per Gaussian by the preprocess).
+__device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t, float ra, float rc, float x0,
+                                                   float x1, float y0, float y1) {
     const float dx0 = x0 - xy.x, dx1 = x1 - xy.x, dy0 = y0 - xy.y, dy1 = y1 - xy.y;
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // centre inside
     const float a = co.x, b = co.y, c = co.z;
-    const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
     float q = fminf(edge_min_x(a, b, c, rc, dx0, dy0, dy1), edge_min_x(a, b, c, rc, dx1, dy0, dy1));
     q = fminf(q, fminf(edge_min_x(c, b, a, ra, dy0, dx0, dx1), edge_min_x(c, b, a, ra, dy1, dx0, dx1)));
     return !(q > t);  // NaN-safe: keeps the record
@@ -71,8 +71,9 @@ __device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t
 // Slots below t_min are skipped too (the backward's last-contributor bound).
 template <bool kExact, int RW = 8, int RH = 8>
 __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
-                                            const float4* __restrict__ s_bo, uint8_t* __restrict__ s_list, int n,
-                                            float qx0, float qy0, int lane, int t_min = 0) {
+                                            const float4* __restrict__ s_bo, const float4* __restrict__ s_rgb,
+                                            uint8_t* __restrict__ s_list, int n, float qx0, float qy0, int lane,
+                                            int t_min = 0) {
     int m = 0;
 #pragma unroll
     for (int k = 0; k < kTilePix / 64; ++k) {
@@ -83,14 +84,14 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
             hit = bx.y >= qx0 && bx.x <= qx0 + (float)(RW - 1) && bx.w >= qy0 && bx.z <= qy0 + (float)(RH - 1);
             if (kExact && hit) {
                 const float4 pc = s_pc[t];
-                const float2 bo = *reinterpret_cast<const float2*>(&s_bo[t]);
+                const float4 bo = s_bo[t];  // (b, o, alpha threshold with slack, 1 / a)
                 const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
                 const float det = co.x * co.z - co.y * co.y;
-                // alpha >= 1/255  <=>  Q <= 2 ln(255 o); slack: 0.1 % + 0.05 (v_exp / v_log rounding)
-                const float tq = 2.0f * 0.69314718f * __builtin_amdgcn_logf(255.0f * co.w) * 1.001f + 0.05f;
+                // alpha >= 1/255  <=>  Q <= 2 ln(255 o); the threshold carries 0.1 % + 0.05 of slack (v_exp /
+                // v_log rounding) and comes precomputed with the reciprocals (RenderRec.q2)
                 if (co.x > 0.f && co.z > 0.f && det > 0.f)
-                    hit = ellipse_meets_rect(make_float2(pc.x, pc.y), co, tq, qx0, qx0 + (float)(RW - 1), qy0,
-                                             qy0 + (float)(RH - 1));
+                    hit = ellipse_meets_rect(make_float2(pc.x, pc.y), co, bo.z, bo.w, s_rgb[t].w, qx0,
+                                             qx0 + (float)(RW - 1), qy0, qy0 + (float)(RH - 1));
             }
         }
         const unsigned long long mask = wave_ballot(hit);
@@ -424,8 +425,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
             s_id[tid] = g;
             s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
-            s_bo[tid] = make_float4(q0.w, q1.y, 0.f, 0.f);
-            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, 0.f);
+            s_bo[tid] = make_float4(q0.w, q1.y, q2.y, q2.z);   // b, o, ellipse threshold, 1 / a
+            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q2.w);  // r, g, b, 1 / c
             s_box[tid] = r->box;
         }
 #pragma unroll
@@ -434,7 +435,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         const int n = min(kTilePix, toDo);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
-        const int m = wave_compact<true>(s_box, s_pc, s_bo, list, n, tg.qx0, tg.qy0, lane, front_base - wave_lc + 1);
+        const int m = wave_compact<true>(s_box, s_pc, s_bo, s_rgb, list, n, tg.qx0, tg.qy0, lane,
+                                         front_base - wave_lc + 1);
         lds_barrier();  // every wave is done with s_box before s_u.qa is written
         // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor
         const int slot_min = front_base - last_contributor;  // slot t counts for this pixel iff t > slot_min

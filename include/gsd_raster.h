@@ -161,7 +161,8 @@ size_t gsd_binning_buffer_bytes(int64_t num_rendered);
 /* Introspection (tests / debugging; the reference exposes none): byte offsets,
  * from the state buffer's first 256-B aligned address, of
  *   geom[6]  = means2D float2; conic_opacity (4 floats) and rgb (3 floats) of Gaussian 0 -- both inside the
- *              64-B render records (x, y, a, b | c, opacity, r, g | b, 0, 0, 0 | alpha box), so Gaussian i's
+ *              64-B render records (x, y, a, b | c, opacity, r, g | b, culling threshold, 1/a, 1/c |
+ *              alpha box), so Gaussian i's
  *              are 64 i bytes further; depths f32, radii i32, clamped u8
  *   image[6] = final_T f32, n_contrib u32, ranges uint2, tile_count u32, tile_cursor u32, counters u32
  *   bin[3]   = bucket keys u64, merge scratch u64, point_list u32 (point_list first in memory) */
