@@ -49,7 +49,7 @@ def algorithmic_bytes(P, V, K, W, H, C):
     T = ((W + 15) // 16) * ((H + 15) // 16)
     npix = W * H
     return {
-        "preprocess_fwd": 44 * P + 12 * C * V + 4 * P + 45 * V,
+        "preprocess_fwd": 44 * P + 12 * C * V + 4 * P + 81 * V,   # 64-B render record per visible Gaussian
         "tile_hist": 4 * P + 8 * V,
         "tile_scan": 16 * T,
         "scatter_keys": 4 * P + 12 * V + 8 * K,
