@@ -446,7 +446,8 @@ def test_sh_grad_views_sums_per_view_sh_gradients():
     assert rel_l2(out_rest.cpu(), 2 * sums[1].cpu()) <= 1e-5
 
 
-def test_sh_grad_views_deferred_view_direction_term():
+@pytest.mark.parametrize("P,deg", [(20_000, 3), (20_003, 1)])
+def test_sh_grad_views_deferred_view_direction_term(P, deg):
     """gsd_sh_split.defer_view_dir: the backward reads no SH coefficient -- it writes the view's d_rgb row and
     leaves the view-direction term of the SH colour out of dL/dmeans3D -- and gsd_sh_grad_views_ex supplies that
     term summed over the views (d_means).  Summed over two views: deferred dL/dmeans3D + d_means == the ordinary
@@ -454,7 +455,7 @@ def test_sh_grad_views_deferred_view_direction_term():
     from gsd_amd import _C
     from gsd_amd.camera import synthetic_camera
     from gsd_amd.scene import make_gaussians
-    P, W, H = 20_000, 320, 240
+    W, H = 320, 240
     g = make_gaussians(P, W, H, seed=13, device=DEV)
     means = g.xyz.contiguous()
     scales, rots = torch.exp(g.scaling), torch.nn.functional.normalize(g.rotation, dim=1)
@@ -468,7 +469,7 @@ def test_sh_grad_views_deferred_view_direction_term():
         tx, ty = math.tan(cam.FoVx / 2), math.tan(cam.FoVy / 2)
         K, color, radii, geom, binning, img = _C.rasterize_gaussians(
             bg, means, None, opac, scales, rots, 1.0, None, cam.world_view_transform, cam.full_proj_transform, tx,
-            ty, H, W, None, 3, cam.camera_center, False, False, sh_split=_C.ShSplit(f_dc, f_rest))
+            ty, H, W, None, deg, cam.camera_center, False, False, sh_split=_C.ShSplit(f_dc, f_rest))
         dpix = torch.randn(3, H, W, generator=torch.Generator().manual_seed(20 + k)).mul_(1e-3).to(DEV)
         for defer, acc, out in ((False, m3d_full, rows_ref), (True, m3d_defer, rows)):
             row = torch.full((3 * P + 4,), float("nan"), device=DEV)
@@ -477,7 +478,7 @@ def test_sh_grad_views_deferred_view_direction_term():
             sp = _C.ShSplit(f_dc, f_rest, None, None, None, None, d_rgb=row[:3 * P], defer_view_dir=defer)
             grads = _C.rasterize_gaussians_backward(bg, means, radii, None, scales, rots, 1.0, None,
                                                     cam.world_view_transform, cam.full_proj_transform, tx, ty, dpix,
-                                                    None, 3, cam.camera_center, geom, K, binning, img, False,
+                                                    None, deg, cam.camera_center, geom, K, binning, img, False,
                                                     sh_split=sp)
             acc += grads[3]
             out.append(row)
@@ -487,8 +488,8 @@ def test_sh_grad_views_deferred_view_direction_term():
     d_means = torch.full((P, 3), float("nan"), device=DEV)
     out_dc, out_rest = torch.empty_like(f_dc), torch.empty_like(f_rest)
     ref_dc, ref_rest = torch.empty_like(f_dc), torch.empty_like(f_rest)
-    _C.sh_grad_views(3, means, views, P, 16, d_dc=out_dc, d_rest=out_rest, sh=(f_dc, f_rest), d_means=d_means)
-    _C.sh_grad_views(3, means, views, P, 16, d_dc=ref_dc, d_rest=ref_rest)
+    _C.sh_grad_views(deg, means, views, P, 16, d_dc=out_dc, d_rest=out_rest, sh=(f_dc, f_rest), d_means=d_means)
+    _C.sh_grad_views(deg, means, views, P, 16, d_dc=ref_dc, d_rest=ref_rest)
     assert torch.equal(out_dc, ref_dc) and torch.equal(out_rest, ref_rest)
     assert torch.isfinite(d_means).all()
     assert float(d_means.abs().max()) > 0.0
