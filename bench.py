@@ -84,7 +84,9 @@ FUSED_STEP = os.environ.get("GSD_FUSED_STEP", "1") != "0"
 
 def make_optimizer(pc):
     """training_setup (scene/gaussian_model.py:834-864) param groups, spatial_lr_scale = 1, eps 1e-15, as one
-    fused HIP Adam over flat slabs (gsd_amd.optim.FusedAdam; torch.optim.Adam semantics)."""
+    fused HIP Adam over flat slabs (gsd_amd.optim.FusedAdam; torch.optim.Adam semantics).  In the SE(3) mode the
+    per-Gaussian twist (the deformation network's output in the dormant reference path,
+    scene/gaussian_model.py:99-173) is a trained parameter of its own group, so d_se3 reaches the optimizer."""
     from gsd_amd.optim import FusedAdam
     groups = [
         {"params": [pc._xyz], "lr": 0.00016, "name": "xyz"},
@@ -94,6 +96,8 @@ def make_optimizer(pc):
         {"params": [pc._scaling], "lr": 0.005, "name": "scaling"},
         {"params": [pc._rotation], "lr": 0.001, "name": "rotation"},
     ]
+    if getattr(pc, "deform", "additive") == "se3" and pc._twist is not None:
+        groups.append({"params": [pc._twist], "lr": 0.0008, "name": "twist"})
     return FusedAdam(groups, lr=0.0, eps=1e-15)
 
 
@@ -149,8 +153,9 @@ def main():
     cfg = CONFIGS[args.config]
     P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
 
-    params = make_gaussians(P, W, H, seed=args.config).to(dev)   # replicated on every rank
-    pc = DeformableGaussians(params, sh_degree=D)
+    se3 = cfg.get("se3") is not None   # configurations 1 and 3: the per-Gaussian SE(3) deform and its gradient
+    params = make_gaussians(P, W, H, seed=args.config, se3=cfg.get("se3")).to(dev)   # replicated on every rank
+    pc = DeformableGaussians(params, sh_degree=D, deform="se3" if se3 else "additive")
     cam = synthetic_camera(W, H, yaw_deg=2.0 * rank).to(dev)     # one view per GPU, yaw offsets k*2 deg
     bg = torch.zeros(3, device=dev)
     pipe = default_pipe()
@@ -285,8 +290,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"cfg{args.config}: {P} Gaussians, SH deg {D}, {W}x{H}, 1 view/GPU; render fwd + "
-                                   "0.8 L1 + 0.2 (1 - SSIM) + bwd + RCCL all-reduce of per-Gaussian grads + Adam",
+            "config": {"workload": f"cfg{args.config}: {P} Gaussians, SH deg {D}, {W}x{H}, 1 view/GPU; "
+                                   + ("per-Gaussian SE(3) deform (fused exp-map) + " if se3 else "")
+                                   + "render fwd + 0.8 L1 + 0.2 (1 - SSIM) + bwd"
+                                   + (" + d_se3" if se3 else "")
+                                   + " + RCCL all-reduce of per-Gaussian grads + Adam",
                        "P": P, "width": W, "height": H, "sh_degree": D, "views_per_step": world,
                        "parallelism": f"dp{world}", "visible": V, "num_rendered": K,
                        "num_rendered_timed_first": K_start, "num_rendered_timed_last": K_end},

@@ -1,5 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 700 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ -p no:cacheprovider > gpurun_out/t20.log 2>&1; rc=$?; tail -2 gpurun_out/t20.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python bench.py > gpurun_out/bench_v30.log 2>&1; rc=$?; tail -1 gpurun_out/bench_v30.log | cut -c1-200; exit $rc
+for c in 3 1 2 5; do
+  timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 --cpu-baseline off > gpurun_out/bench_cfg$c.log 2>&1; rc=$?
+  echo "cfg $c rc=$rc"; grep metric gpurun_out/bench_cfg$c.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['fwd_bwd_ms_per_view'], d['config']['workload'][:90], d['config']['num_rendered'])"
+  [ $rc -ne 0 ] && { tail -5 gpurun_out/bench_cfg$c.log; exit $rc; }
+done
+exit 0
