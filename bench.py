@@ -136,6 +136,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--densify-interval", type=int, default=None,
+                    help="densify_and_prune every N steps (train.py:610-648); default 100 for config 5, else off")
     args = ap.parse_args()
 
     from gsd_amd import DeformableGaussians, default_pipe, l1_ssim_loss, render
@@ -154,6 +156,8 @@ def main():
     P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
 
     se3 = cfg.get("se3") is not None   # configurations 1 and 3: the per-Gaussian SE(3) deform and its gradient
+    # configuration 5: "densification/prune step active" -- densify_and_prune every 100 views, so P changes
+    densify_every = args.densify_interval if args.densify_interval is not None else (100 if args.config == 5 else 0)
     params = make_gaussians(P, W, H, seed=args.config, se3=cfg.get("se3")).to(dev)   # replicated on every rank
     pc = DeformableGaussians(params, sh_degree=D, deform="se3" if se3 else "additive")
     cam = synthetic_camera(W, H, yaw_deg=2.0 * rank).to(dev)     # one view per GPU, yaw offsets k*2 deg
@@ -167,7 +171,12 @@ def main():
         noise = torch.randn(3, H, W, generator=torch.Generator().manual_seed(100 + rank)).to(dev)
         target = (target + 0.02 * noise).clamp_(0.0, 1.0)
     opt = make_optimizer(pc)
-    flat = opt.flat        # every .grad is a view of this slab: the one buffer the all-reduce sums
+    # every .grad is a view of one slab (opt.flat): the one buffer the all-reduce sums
+    dens = None
+    if densify_every:
+        from gsd_amd.densify import GaussianDensifier
+        dens = GaussianDensifier(pc, opt)
+    nstep = [0]
 
     def step():
         out = render(cam, pc, pipe, bg)
@@ -184,22 +193,39 @@ def main():
             # over each bucket as its sum arrives; a no-op collective at N = 1.  The gradient slab is marked
             # stale for the next step instead of cleared.
             opt.allreduce_step(zero_grad=True)
+        if dens is not None:
+            # train.py:610-648 with the reference's thresholds (densify_grad_threshold 0.0002, min opacity 0.005);
+            # the synthetic scene's extent is its depth range (z in [2, 10])
+            dens.add_densification_stats(out["viewspace_points"], out["radii"])
+            nstep[0] += 1
+            if nstep[0] % densify_every == 0:
+                dens.densify_and_prune(0.0002, 0.005, 10.0, None)   # new slabs (FusedAdam.rebuild): opt.flat
         return out
 
     # Adam moves every parameter by ~lr per step whatever the gradient, so the scene drifts from the configured
     # workload as steps accumulate; each measurement below starts from the initial parameters and optimizer
-    # state (restored outside the timed regions)
+    # state (restored outside the timed regions; with densification the initial scene is rebuilt, P included)
     snapshot = [p.detach().clone() for p in pc.parameters()]
 
     def restore():
         with torch.no_grad():
+            if dens is not None and pc._xyz.shape[0] != snapshot[0].shape[0]:   # densified: the initial P back
+                init = dict(zip(("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"), snapshot[:6]))
+                dens._apply(lambda n, d, m, v: (init[n].clone(), torch.zeros_like(init[n]), torch.zeros_like(init[n])))
             for p, s0 in zip(pc.parameters(), snapshot):
                 p.copy_(s0)
             opt.reset_state()
-        flat.invalidate()   # as a fresh optimizer: no gradients yet
+            if dens is not None:
+                dens._reset_stats()
+        nstep[0] = 0
+        opt.flat.invalidate()   # as a fresh optimizer: no gradients yet
 
     for _ in range(args.warmup):
         step()
+    if dens is not None:
+        # one densification in the warmup as well: PyTorch loads each elementwise kernel's code object on its
+        # first launch (~0.6 s over densify_and_prune's ops on a fresh process), a one-time cost, not a step's
+        dens.densify_and_prune(0.0002, 0.005, 10.0, None)
     restore()
     torch.cuda.synchronize()
     if world > 1:
@@ -219,6 +245,7 @@ def main():
         elapsed = float(t.item())
 
     K_end = int(gsdC.last_forward.get("num_rendered", 0))
+    P_end = int(pc._xyz.shape[0])   # densified count at the end of the timed steps
     restore()
     # fwd+bwd ms/view: render + loss + backward of one view (no optimizer / collective),
     # hipEvents on the current stream, median over >= 100 views, two ways:
@@ -228,7 +255,7 @@ def main():
     #   synced  -- the host starts enqueueing after the first event: its Python prologue is on the clock too.
     def fwd_bwd(queued):
         ts = []
-        flat.invalidate()
+        opt.flat.invalidate()
         for _ in range(max(100, args.steps)):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if queued:
@@ -239,7 +266,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
-            flat.invalidate()   # as after the optimizer step: the next backward stores into the slab
+            opt.flat.invalidate()   # as after the optimizer step: the next backward stores into the slab
         ts.sort()
         return ts[len(ts) // 2]
 
@@ -275,7 +302,7 @@ def main():
                     if tr.get("valu"):   # the bound that applies to the render kernels: VALU issue
                         roof["valu"] = tr["valu"]
         cpu = None
-        if args.cpu_baseline == "auto" and world == 1:
+        if args.cpu_baseline == "auto" and world == 1 and args.config <= 4:   # a bounded CPU sample
             cpu = cpu_baseline(cfg, args.config)
         res = {
             "metric": METRIC,
@@ -297,7 +324,9 @@ def main():
                                    + " + RCCL all-reduce of per-Gaussian grads + Adam",
                        "P": P, "width": W, "height": H, "sh_degree": D, "views_per_step": world,
                        "parallelism": f"dp{world}", "visible": V, "num_rendered": K,
-                       "num_rendered_timed_first": K_start, "num_rendered_timed_last": K_end},
+                       "num_rendered_timed_first": K_start, "num_rendered_timed_last": K_end,
+                       "densify_interval": densify_every or None,
+                       "P_timed_last": P_end},
             "fwd_bwd_ms_per_view": round(fwd_bwd_ms, 4),
             "fwd_bwd_ms_per_view_host_synced": round(fwd_bwd_synced_ms, 4),
             "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},

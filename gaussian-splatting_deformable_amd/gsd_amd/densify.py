@@ -132,21 +132,56 @@ class GaussianDensifier:
         prune = torch.cat((sel, torch.zeros(N * int(sel.sum()), device=sel.device, dtype=torch.bool)))
         self.prune_points(prune)
 
-    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size):
-        """:1219-1233 (after combining the ranks' statistics)."""
+    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, N=2):
+        """:1219-1233 (after combining the ranks' statistics) as ONE optimizer-state surgery: the reference runs
+        clone (append), split (append, then drop the split originals) and the prune as four tensor rebuilds; the
+        result is assembled here directly -- [surviving originals | clones | split children], pruned -- with the
+        same selections, the same torch.normal draw and the same order, so the points, parameters and moments
+        are the reference's (tests/test_gpu_train.py::test_densify_and_prune_matches_reference).  Clone and split
+        select from the original points only (the split's padded gradients are zero for the clones), and the
+        statistics are reset by the reference's densification_postfix before its final prune, so the screen-size
+        test (max_radii2D) never fires there; it is kept as the reference writes it.
+        2M Gaussians: one rebuild instead of four."""
         self.sync_stats()
         grads = self.xyz_gradient_accum / self.denom
         grads[grads.isnan()] = 0.0
-        self.densify_and_clone(grads, max_grad, extent)
-        self.densify_and_split(grads, max_grad, extent)
         pc = self.pc
         with torch.no_grad():
-            prune = (pc.get_opacity < min_opacity).squeeze()
+            scal = pc.get_scaling
+            smax = scal.max(dim=1).values
+            clone = torch.logical_and(torch.norm(grads, dim=-1) >= max_grad, smax <= self.percent_dense * extent)
+            split = torch.logical_and(grads.squeeze(-1) >= max_grad, smax > self.percent_dense * extent)
+            # densify_and_split's draw (after the clones, which draw nothing): rank 0's samples on every rank
+            stds = scal[split].repeat(N, 1)
+            samples = broadcast_(torch.normal(mean=torch.zeros((stds.size(0), 3), device=stds.device), std=stds))
+            rots = build_rotation(pc._rotation[split]).repeat(N, 1, 1)
+            src = dict(zip(_NAMES, (p.detach() for p in self._params())))
+            children = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + src["xyz"][split].repeat(N, 1),
+                        "scaling": torch.log(scal[split].repeat(N, 1) / (0.8 * N))}
+            keep = ~split
+
+            def assemble(n, d):
+                kid = children[n] if n in children else d[split].repeat(N, *([1] * (d.dim() - 1)))
+                return torch.cat((d[keep], d[clone], kid), 0)
+
+            opac = assemble("opacity", src["opacity"])
+            prune = (pc.opacity_activation(opac) < min_opacity).squeeze(-1)
             if max_screen_size:
-                big_vs = self.max_radii2D > max_screen_size
-                big_ws = pc.get_scaling.max(dim=1).values > 0.1 * extent
+                P_new = opac.shape[0]   # the statistics were reset before this test: max_radii2D is all zero
+                big_vs = torch.zeros(P_new, dtype=torch.bool, device=opac.device) > max_screen_size
+                big_ws = pc.scaling_activation(assemble("scaling", src["scaling"])).max(dim=1).values > 0.1 * extent
                 prune = torch.logical_or(torch.logical_or(prune, big_vs), big_ws)
-        self.prune_points(prune)
+            live = ~prune
+
+            fresh = int(clone.sum()) + N * int(split.sum())   # clones and children start with zero moments
+
+            def surgery(n, d, m, v):
+                zm = torch.zeros((fresh,) + tuple(d.shape[1:]), dtype=d.dtype, device=d.device)
+                return (assemble(n, d)[live], torch.cat((m[keep], zm), 0)[live],
+                        torch.cat((v[keep], zm), 0)[live])
+
+        self._apply(surgery)
+        self._reset_stats()
 
     def reset_opacity(self):
         """:960-963 -- opacities to min(sigmoid(o), 0.01), with zero moments for that group."""

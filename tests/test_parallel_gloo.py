@@ -305,3 +305,44 @@ def test_two_rank_addend_joins_after_the_sum(tmp_path):
                                    atol=1e-6)
         np.testing.assert_allclose(np.load(os.path.join(str(tmp_path), f"brank{r}.npy")), plain, rtol=1e-5,
                                    atol=1e-6)
+
+
+def test_single_pass_densify_equals_clone_split_prune():
+    """GaussianDensifier.densify_and_prune assembles the reference's result in one optimizer-state surgery; it
+    must equal the reference's own sequence -- densify_and_clone, densify_and_split (same torch.normal draw),
+    then the opacity / world-size prune over the statistics the postfix reset -- point for point, moments
+    included (CPU, the slab stand-in)."""
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    outs = []
+    for single in (True, False):
+        pc, ps, dens = _densify_model()
+        with torch.no_grad():
+            pc._opacity[::7] = -8.0   # some points below the prune threshold
+        dens.denom, dens.xyz_gradient_accum, dens.max_radii2D, dens.xyz_gradient_accum_3vec = _rank_stats(0, 300)
+        for p in ps:   # distinct moments per point, so the row bookkeeping shows
+            m, v = dens.opt.moments(p)
+            m.copy_(torch.arange(p.numel(), dtype=torch.float32).reshape(p.shape))
+            v.copy_(m * 0.5)
+        torch.manual_seed(77)
+        if single:
+            dens.densify_and_prune(2e-4, 0.005, 2.0, 30)
+        else:   # gaussian_model.py:1219-1233 step by step
+            grads = dens.xyz_gradient_accum / dens.denom
+            grads[grads.isnan()] = 0.0
+            dens.densify_and_clone(grads, 2e-4, 2.0)
+            dens.densify_and_split(grads, 2e-4, 2.0)
+            with torch.no_grad():
+                prune = (pc.get_opacity < 0.005).squeeze()
+                big_vs = dens.max_radii2D > 30
+                big_ws = pc.get_scaling.max(dim=1).values > 0.1 * 2.0
+                prune = torch.logical_or(torch.logical_or(prune, big_vs), big_ws)
+            dens.prune_points(prune)
+        outs.append(([p.detach().clone() for p in ps], [torch.cat([t.reshape(-1) for t in dens.opt.moments(p)])
+                                                        for p in ps]))
+    (pa, ma), (pb, mb) = outs
+    assert pa[0].shape[0] not in (300,) and pa[0].shape == pb[0].shape
+    for a, b in zip(pa + ma, pb + mb):
+        assert torch.equal(a, b)
