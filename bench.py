@@ -321,7 +321,8 @@ def main():
                                    + ("per-Gaussian SE(3) deform (fused exp-map) + " if se3 else "")
                                    + "render fwd + 0.8 L1 + 0.2 (1 - SSIM) + bwd"
                                    + (" + d_se3" if se3 else "")
-                                   + " + RCCL all-reduce of per-Gaussian grads + Adam",
+                                   + " + RCCL all-reduce of per-Gaussian grads + Adam"
+                                   + (f"; densify_and_prune every {densify_every} steps" if densify_every else ""),
                        "P": P, "width": W, "height": H, "sh_degree": D, "views_per_step": world,
                        "parallelism": f"dp{world}", "visible": V, "num_rendered": K,
                        "num_rendered_timed_first": K_start, "num_rendered_timed_last": K_end,
