@@ -217,11 +217,22 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
     const int ch = blockIdx.z;
     const int ox = blockIdx.x * kSsimTile, oy = blockIdx.y * kSsimTile;
     const size_t plane = (size_t)p.H * p.W;
+    const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimRows;
+    // the thread's own image and ground-truth pixels, loaded with the staging loads (not after the window
+    // passes, where their latency was exposed)
+    float xs[kSsimRows], ys[kSsimRows];
+#pragma unroll
+    for (int j = 0; j < kSsimRows; ++j) {
+        const int gy = oy + r0 + j, gx = ox + c;
+        const bool ok = gy < p.H && gx < p.W;
+        const size_t o = ch * plane + (ok ? (size_t)gy * p.W + gx : 0);
+        xs[j] = ok ? img[o] : 0.f;
+        ys[j] = ok ? gt[o] : 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < 3; ++q) stage(gmaps + ((size_t)q * p.C + ch) * plane, sg[q], p.H, p.W, ox, oy);
     __syncthreads();
     for (int r = threadIdx.x >> 5; r < kSsimIn; r += kSsimThreads / 32) {
-        const int c = threadIdx.x & 31;
         float a = 0.f, cc = 0.f, e = 0.f;
 #pragma unroll
         for (int k = 0; k < 11; ++k) {
@@ -235,7 +246,6 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
         sh[2][r][c] = e;
     }
     __syncthreads();
-    const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimRows;
     const float g = gscale ? sign * gscale[0] : sign;  // d out / d loss (autograd's incoming gradient)
     float acc[3][kSsimRows];
 #pragma unroll
@@ -257,21 +267,39 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
         const int gy = oy + r0 + j, gx = ox + c;
         if (gy >= p.H || gx >= p.W) continue;
         const size_t o = ch * plane + (size_t)gy * p.W + gx;
-        const float x = img[o], y = gt[o];
+        const float x = xs[j], y = ys[j];
         const float diff = x - y;
         const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);  // torch.abs backward: sign, 0 at 0
         dimg[o] = g * (acc[0][j] + 2.f * x * acc[1][j] + y * acc[2][j] + p.coef_l1 * sgn);
     }
 }
 
-// Fixed-order sum of the per-workgroup partials (one workgroup): out = {loss, L1, SSIM}.
-__global__ __launch_bounds__(256) void k_loss_sum(int nblk, const float* __restrict__ partial, float inv_n,
-                                                  float lambda, float* __restrict__ out) {
-    __shared__ float red[2][4];
+// Fixed-order sum of the per-workgroup partials (one workgroup): out = {loss, L1, SSIM}.  The partials are
+// (f, l1) pairs, read two blocks per 16-B load, four loads in flight per lane per round (a strided scalar loop
+// over the 6120 pairs of a 1080p view was ~24 dependent L2 round trips: 7.0 us).
+constexpr int kSumThreads = 1024;
+__global__ __launch_bounds__(kSumThreads) void k_loss_sum(int nblk, const float* __restrict__ partial, float inv_n,
+                                                          float lambda, float* __restrict__ out) {
+    __shared__ float red[2][kSumThreads / 64];
+    const float4* p4 = reinterpret_cast<const float4*>(partial);
+    const int n4 = nblk >> 1;
     float f = 0.f, l = 0.f;
-    for (int b = threadIdx.x; b < nblk; b += 256) {
-        f += partial[2 * b];
-        l += partial[2 * b + 1];
+    for (int b = threadIdx.x; b < n4; b += 4 * kSumThreads) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = b + u * kSumThreads;
+            v[u] = i < n4 ? p4[i] : float4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f += v[u].x + v[u].z;
+            l += v[u].y + v[u].w;
+        }
+    }
+    if ((nblk & 1) && threadIdx.x == 0) {
+        f += partial[2 * (nblk - 1)];
+        l += partial[2 * (nblk - 1) + 1];
     }
     f = wave_sum(f);
     l = wave_sum(l);
@@ -281,8 +309,14 @@ __global__ __launch_bounds__(256) void k_loss_sum(int nblk, const float* __restr
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float ssim = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) * inv_n;
-        const float l1 = ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * inv_n;
+        float fs = 0.f, ls = 0.f;
+#pragma unroll
+        for (int w = 0; w < kSumThreads / 64; ++w) {
+            fs += red[0][w];
+            ls += red[1][w];
+        }
+        const float ssim = fs * inv_n;
+        const float l1 = ls * inv_n;
         out[0] = (1.f - lambda) * l1 + lambda * (1.f - ssim);
         out[1] = l1;
         out[2] = ssim;
@@ -315,7 +349,7 @@ void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const f
     const double n = (double)C * H * W;
     const dim3 grid(p.tiles_x, p.tiles_y, C);
     hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, partial);
-    hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(256), 0, s, p.tiles_x * p.tiles_y * C, partial, (float)(1.0 / n),
+    hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(kSumThreads), 0, s, p.tiles_x * p.tiles_y * C, partial, (float)(1.0 / n),
                        lambda, out3);
     if (dimg)
         hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, (const float*)nullptr, 1.0f,
