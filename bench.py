@@ -178,6 +178,10 @@ def main():
         dens = GaussianDensifier(pc, opt)
     nstep = [0]
 
+    # autograd's seed gradient d loss / d loss = 1, allocated once (a bare loss.backward() launches a fill each
+    # step; identical semantics)
+    seed = None if os.environ.get("GSD_BENCH_BARE_BACKWARD") else torch.ones((), device=dev)
+
     def step():
         out = render(cam, pc, pipe, bg)
         loss = l1_ssim_loss(out["render"], target, 0.2)   # train.py:529, lambda_dssim = 0.2
@@ -186,9 +190,9 @@ def main():
             # the Adam step there (FusedAdam.step_in_backward, gsd_adam_epilogue); with N > 1 the gradients
             # are summed first, and leaving the block runs allreduce_step as below
             with opt.step_in_backward():
-                loss.backward()
+                loss.backward(seed)
         else:
-            loss.backward()
+            loss.backward(seed)
             # the gradient all-reduce (RCCL, bucketed, asynchronous) overlapped with the Adam pass, which runs
             # over each bucket as its sum arrives; a no-op collective at N = 1.  The gradient slab is marked
             # stale for the next step instead of cleared.
@@ -262,7 +266,7 @@ def main():
                 torch.cuda._sleep(2_000_000)
             e0.record()
             o = render(cam, pc, pipe, bg)
-            l1_ssim_loss(o["render"], target, 0.2).backward()
+            l1_ssim_loss(o["render"], target, 0.2).backward(seed)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))

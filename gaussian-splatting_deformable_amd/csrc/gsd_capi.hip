@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -61,7 +62,12 @@ struct Geom {
 bool hist_binning(size_t T) { return T <= (size_t)gsd::kHistMaxTiles; }
 
 void hist_shape(size_t P, int* chunk, int* nblocks) {
-    const size_t c = (P + gsd::kHistTargetBlocks - 1) / gsd::kHistTargetBlocks;
+    static const size_t target = [] {  // GSD_HIST_BLOCKS: experiment override of kHistTargetBlocks
+        const char* e = getenv("GSD_HIST_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        return (size_t)(v > 0 ? v : gsd::kHistTargetBlocks);
+    }();
+    const size_t c = (P + target - 1) / target;
     *chunk = (int)(c < 256 ? 256 : c);
     *nblocks = (int)((P + *chunk - 1) / *chunk);
 }

@@ -1,5 +1,11 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 300 python scripts/prof_densify.py --steps 3 > gpurun_out/dens.log 2>&1 && \
-timeout -k 10 400 python bench.py --config 5 --steps 300 --warmup 5 > gpurun_out/b5.log 2>&1; rc=$?
-grep -v amdgpu.ids gpurun_out/dens.log | cut -c1-160 | tail -20; tail -c 2500 gpurun_out/b5.log; exit $rc
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+for v in 0 1 0 1; do
+if [ $v = 1 ]; then export GSD_BENCH_BARE_BACKWARD=1; else unset GSD_BENCH_BARE_BACKWARD; fi
+timeout -k 10 200 python bench.py --steps 300 --warmup 20 --cpu-baseline off > gpurun_out/b_$v.log 2>&1 || exit 1
+python - "$v" <<'PY'
+import json,sys
+d=json.loads(open(f"gpurun_out/b_{sys.argv[1]}.log").read().strip().splitlines()[-1])
+print("bare" if sys.argv[1]=="1" else "seed", d["value"], d["ms_per_step"], d["fwd_bwd_ms_per_view"], d["kernels_ms"]["l1_ssim"])
+PY
+done
