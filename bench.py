@@ -234,12 +234,20 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    step_ev = [] if os.environ.get("GSD_BENCH_STEP_TIMES") else None   # diagnostics: per-step device times
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if step_ev is not None:
+            step_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+            step_ev[-1][0].record()
         out = step()
+        if step_ev is not None:
+            step_ev[-1][1].record()
         if i == 0:
             K_start = int(gsdC.last_forward.get("num_rendered", 0))  # host value, already read by the forward
     torch.cuda.synchronize()
+    if step_ev is not None and rank == 0:
+        print("step ms:", " ".join("%.3f" % a.elapsed_time(b) for a, b in step_ev), file=sys.stderr)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
