@@ -18,7 +18,50 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
+
+
+# Weight gradients reduce over all P rows (K = P, a 256 x 256 output): one GEMM of that shape gets ~16 output
+# tiles -- 16 workgroups on 256 CUs (hipBLASLt picked MT64x64x256 / MT32x64x128 without split-K: 1.8-2.3 ms per
+# layer at P = 1M).  Split-K by hand instead: a batched GEMM over row chunks, then a sum over the chunks.
+_SPLITK_ROWS = 8192
+
+
+def _weight_grad(g: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """g^T h summed over the rows, as float32: (N, out), (N, in) -> (out, in)."""
+    N = g.shape[0]
+    S = N // _SPLITK_ROWS
+    if S < 2:
+        return (g.t() @ h).float()
+    main = S * _SPLITK_ROWS
+    dw = torch.bmm(g[:main].view(S, _SPLITK_ROWS, -1).transpose(1, 2), h[:main].view(S, _SPLITK_ROWS, -1))
+    dw = dw.sum(0, dtype=torch.float32)
+    if main < N:
+        dw += (g[main:].t() @ h[main:]).float()
+    return dw
+
+
+class _Linear(torch.autograd.Function):
+    """y = h W^T + b (then ReLU when `relu`), in h's dtype (f32 or bf16; W and b cast to it), with the split-K
+    weight gradient above; dW and db come back in float32 (the parameters' dtype)."""
+
+    @staticmethod
+    def forward(ctx, h, W, b, relu):
+        Wc, bc = W.to(h.dtype), b.to(h.dtype)
+        # bias and ReLU in the GEMM's epilogue (hipBLASLt) where torch offers it
+        y = torch._addmm_activation(bc, h, Wc.t()) if relu else torch.addmm(bc, h, Wc.t())
+        ctx.relu = relu
+        ctx.save_for_backward(h, Wc, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        h, Wc, y = ctx.saved_tensors
+        gy = gy.to(h.dtype)
+        g = torch.ops.aten.threshold_backward(gy, y, 0) if ctx.relu else gy.contiguous()  # one pass
+        dh = g @ Wc if ctx.needs_input_grad[0] else None
+        dW = _weight_grad(g, h) if ctx.needs_input_grad[1] else None
+        db = g.sum(0, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        return dh, dW, db, None
 
 
 def positional_encoding(x: torch.Tensor, n_freqs: int = 10) -> torch.Tensor:
@@ -55,12 +98,17 @@ class DirectTemporalNeRF(nn.Module):
             return z(P, 3), z(P, 3), z(P, 4), z(P, 48)
         ex = positional_encoding(x, self.n_freqs)
         et = positional_encoding(ts, self.n_freqs)
-        dt = self.compute_dtype
-        with torch.autocast(device_type=x.device.type, dtype=dt, enabled=dt != torch.float32):
-            h = torch.cat((ex, et), dim=-1)
-            for i, layer in enumerate(self._time):
-                h = F.relu(layer(h))
-                if i in self.skips:
-                    h = torch.cat((ex, h), dim=-1)
-            outs = (self._time_out(h), self._time_out_scale(h), self._time_out_rot(h), self._time_out_shs(h))
-        return tuple(o.float() for o in outs)
+        dt = self.compute_dtype if self.compute_dtype != torch.float32 else ex.dtype  # f32: the input's own
+        # the hidden layers and the heads in `dt` (as autocast would cast them), bias + ReLU fused after each GEMM;
+        # the four heads as one 58-wide GEMM over the concatenated weights
+        exd = ex.to(dt)
+        h = torch.cat((exd, et.to(dt)), dim=-1)
+        for i, layer in enumerate(self._time):
+            h = _Linear.apply(h, layer.weight, layer.bias, True)
+            if i in self.skips:
+                h = torch.cat((exd, h), dim=-1)
+        heads = (self._time_out, self._time_out_scale, self._time_out_rot, self._time_out_shs)
+        W = torch.cat([m.weight for m in heads], dim=0)
+        b = torch.cat([m.bias for m in heads], dim=0)
+        o = _Linear.apply(h, W, b, False).float()
+        return tuple(t.contiguous() for t in o.split([m.out_features for m in heads], dim=-1))

@@ -39,3 +39,39 @@ def test_forward_matches_restatement_and_zero_phase():
     ref = deform_mlp_ref.forward(net.state_dict(), x, t, 5000)
     for g, r in zip(got, ref):
         assert float((g.double() - r).abs().max()) <= 1e-5 * max(1.0, float(r.abs().max()))
+
+
+def test_split_k_gradients_match_plain_linear_layers():
+    """The module's backward (gsd_amd.deform_mlp._Linear: bias + ReLU fused, split-K weight gradient over
+    8192-row chunks plus a remainder, the four heads as one GEMM) against the same network written with
+    torch.nn.functional.linear and autograd, on more rows than two chunks."""
+    import torch.nn.functional as F
+
+    from gsd_amd.deform_mlp import DirectTemporalNeRF, positional_encoding
+    torch.manual_seed(1)
+    net = DirectTemporalNeRF().double()
+    P = 2 * 8192 + 37
+    x = torch.randn(P, 3, dtype=torch.float64)
+    t = torch.full((P, 1), 0.21, dtype=torch.float64)
+    w = [torch.randn(P, n, dtype=torch.float64) for n in (3, 3, 4, 48)]
+
+    def plain(xx):
+        ex, et = positional_encoding(xx), positional_encoding(t)
+        h = torch.cat((ex, et), -1)
+        for i, layer in enumerate(net._time):
+            h = F.relu(F.linear(h, layer.weight, layer.bias))
+            if i in net.skips:
+                h = torch.cat((ex, h), -1)
+        return [F.linear(h, m.weight, m.bias) for m in (net._time_out, net._time_out_scale, net._time_out_rot,
+                                                        net._time_out_shs)]
+
+    grads = {}
+    for name, fn in (("fused", lambda xx: net(xx, t, 5000)), ("plain", plain)):
+        net.zero_grad()
+        xx = x.clone().requires_grad_(True)
+        outs = fn(xx)
+        sum((o * wi).sum() for o, wi in zip(outs, w)).backward()
+        grads[name] = [xx.grad] + [p.grad.clone() for p in net.parameters()]
+    # the module returns float32 outputs (as the reference's .float()), so its gradients carry float32 rounding
+    for a, b in zip(grads["fused"], grads["plain"]):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
