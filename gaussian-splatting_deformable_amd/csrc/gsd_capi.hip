@@ -254,12 +254,12 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kMlp, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
                                                "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "sh_grad_views", "adam",         "densify_stats",
-                                               "knn"};
+                                               "knn",            "deform_mlp"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -862,6 +862,24 @@ int gsd_knn_mean_dist2(int32_t P, const float* points, float* mean_dist2, void* 
     int e = 0;
     timed(kKnn, s, [&] { e = gsd::launch_knn(P, points, mean_dist2, workspace, s); });
     if (e) return fail(GSD_ERR_HIP, std::string("knn sort: ") + hipGetErrorString((hipError_t)e));
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int32_t gsd_deform_mlp_fragments(void) { return gsd::kMlpFrags; }
+int32_t gsd_deform_mlp_biases(void) { return gsd::kMlpBias; }
+
+int gsd_deform_mlp_forward_bf16(int32_t P, const float* x, const float* t, const void* frags, const float* bias,
+                                float* d_xyz, float* d_scale, float* d_rot, float* d_sh, void* stream) {
+    if (P < 0) return fail(GSD_ERR_ARG, "invalid P");
+    if (P == 0) return GSD_OK;
+    if (!x || !t || !frags || !bias || !d_xyz || !d_scale || !d_rot || !d_sh)
+        return fail(GSD_ERR_ARG, "null pointer argument");
+    if ((reinterpret_cast<uintptr_t>(frags) | reinterpret_cast<uintptr_t>(bias)) & 15)
+        return fail(GSD_ERR_ARG, "deform_mlp: frags and bias must be 16-B aligned");
+    gsd::MlpParams p{P, x, t, frags, bias, d_xyz, d_scale, d_rot, d_sh};
+    hipStream_t s = as_stream(stream);
+    timed(kMlp, s, [&] { gsd::launch_mlp_fwd(p, s); });
     GSD_CHECK(false, s);
     return GSD_OK;
 }

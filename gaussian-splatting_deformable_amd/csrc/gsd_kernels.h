@@ -283,6 +283,23 @@ void launch_densify_stats(int P, const float* vgrad, const int* radii, float* ac
 size_t knn_workspace(int P, size_t* sort_bytes);
 int launch_knn(int P, const float* pts, float* out, void* ws, hipStream_t s);
 
+// deformation network forward on the bf16 matrix cores (gsd_mlp.hip)
+constexpr int kMlpLayers = 9;      // 8 hidden + the four heads as one
+constexpr int kMlpFrags = 64512;   // 16-B A fragments of all layers (1008 KB)
+constexpr int kMlpBias = 2112;     // packed biases (32 per row block)
+struct MlpParams {
+    int P;
+    const float* x;      // (P,3) canonical means
+    const float* t;      // (P) time
+    const void* frags;   // kMlpFrags x 16 B, fragment-major (gsd_amd.deform_mlp.pack_fused_mlp)
+    const float* bias;   // kMlpBias floats, [layer][row block][lane half][register]
+    float* d_xyz;        // (P,3)
+    float* d_scale;      // (P,3)
+    float* d_rot;        // (P,4)
+    float* d_sh;         // (P,48)
+};
+void launch_mlp_fwd(const MlpParams& p, hipStream_t s);
+
 constexpr int kAdamMaxGroups = 16;
 struct AdamArgs {
     long long n;                        // elements in the slabs

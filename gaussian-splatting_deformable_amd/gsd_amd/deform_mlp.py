@@ -16,6 +16,8 @@ f32 accumulation).  The encoding is one fused elementwise HIP-friendly torch exp
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -64,6 +66,83 @@ class _Linear(torch.autograd.Function):
         return dh, dW, db, None
 
 
+# ---- the fused bf16 forward (gsd_mlp.hip via gsd_deform_mlp_forward_bf16) ----
+# Inside each 16-wide k-step the kernel's B operand (the previous layer's accumulator registers) holds, at logical
+# position p = 8 h + j, feature 8 (j >> 2) + 4 h + (j & 3): the weights' input columns are permuted to match.
+_PERM16 = (0, 1, 2, 3, 8, 9, 10, 11, 4, 5, 6, 7, 12, 13, 14, 15)
+
+
+def _perm_cols(W: torch.Tensor) -> torch.Tensor:
+    n = W.shape[1]
+    idx = torch.arange(n, device=W.device).view(-1, 16)[:, list(_PERM16)].reshape(-1)
+    return W[:, idx]
+
+
+def _frag_major(W: torch.Tensor) -> torch.Tensor:
+    """(RB*32, KS*16) -> [ks][rb][lane = 32 h + r][j] = W[32 rb + r][16 ks + 8 h + j], bf16."""
+    M, K = W.shape
+    RB, KS = M // 32, K // 16
+    return W.to(torch.bfloat16).view(RB, 32, KS, 2, 8).permute(2, 0, 3, 1, 4).reshape(-1)
+
+
+def _lane_bias(b: torch.Tensor, rows: int) -> torch.Tensor:
+    """b padded to `rows`, rounded to bf16 (autocast's bias), as [rb][h][reg] = b[32 rb + (reg&3) + 8 (reg>>2) + 4 h]."""
+    dev = b.device
+    bp = torch.zeros(rows, dtype=torch.float32, device=dev)
+    bp[: b.numel()] = b.detach().to(torch.bfloat16).float()
+    reg = torch.arange(16, device=dev)
+    row = (32 * torch.arange(rows // 32, device=dev)[:, None, None] + 4 * torch.arange(2, device=dev)[None, :, None]
+           + ((reg & 3) + 8 * (reg >> 2))[None, None, :])
+    return bp[row.reshape(-1)]
+
+
+@torch.no_grad()
+def pack_fused_mlp(net: "DirectTemporalNeRF"):
+    """The network's weights and biases in the layout gsd_deform_mlp_forward_bf16 reads (gsd_mlp.hip): nine
+    layers (8 hidden, the heads as one 58 -> 64-row GEMM), K padded to 16, fragment-major bf16."""
+    hid = list(net._time)
+    Ws, bs = [], []
+    W0 = hid[0].weight
+    Ws.append(torch.cat((W0, W0.new_zeros(W0.shape[0], 96 - W0.shape[1])), 1))
+    bs.append(hid[0].bias)
+    for i in range(1, len(hid)):
+        W = hid[i].weight
+        if i - 1 in net.skips:   # cat(enc(x) 63, h): the encoding in natural order, one zero column, h permuted
+            W = torch.cat((W[:, :63], W.new_zeros(W.shape[0], 1), _perm_cols(W[:, 63:])), 1)
+        else:
+            W = _perm_cols(W)
+        Ws.append(W)
+        bs.append(hid[i].bias)
+    heads = (net._time_out, net._time_out_scale, net._time_out_rot, net._time_out_shs)
+    Wh = _perm_cols(torch.cat([m.weight for m in heads], 0))
+    Ws.append(torch.cat((Wh, Wh.new_zeros(64 - Wh.shape[0], Wh.shape[1])), 0))
+    bs.append(torch.cat([m.bias for m in heads], 0))
+    frags = torch.cat([_frag_major(W) for W in Ws])
+    bias = torch.cat([_lane_bias(b, W.shape[0]) for W, b in zip(Ws, bs)])
+    return frags.contiguous(), bias.contiguous()
+
+
+def _fused_forward(net: "DirectTemporalNeRF", x: torch.Tensor, ts: torch.Tensor):
+    from . import _native
+    from ._C import _ptr, _stream
+    lib = _native.load()
+    P = x.shape[0]
+    key = tuple((p.data_ptr(), p._version) for p in net.parameters())
+    if getattr(net, "_fused_key", None) != key:   # repacked when a parameter changed (optimizer step, load)
+        net._fused_pack = pack_fused_mlp(net)
+        net._fused_key = key
+    frags, bias = net._fused_pack
+    if frags.numel() != 8 * lib.gsd_deform_mlp_fragments() or bias.numel() != lib.gsd_deform_mlp_biases():
+        raise RuntimeError("deform_mlp: packed layout does not match the library")
+    xc = x.detach().to(torch.float32).contiguous()
+    tc = ts.detach().to(torch.float32).reshape(-1).expand(P).contiguous()
+    outs = tuple(torch.empty(P, n, dtype=torch.float32, device=x.device) for n in (3, 3, 4, 48))
+    with torch.cuda.device(x.device):
+        _native.check(lib.gsd_deform_mlp_forward_bf16(P, _ptr(xc), _ptr(tc), _ptr(frags), _ptr(bias),
+                                                      *(_ptr(o) for o in outs), _stream(x.device)))
+    return outs
+
+
 def positional_encoding(x: torch.Tensor, n_freqs: int = 10) -> torch.Tensor:
     """[x, sin(x 2^0), cos(x 2^0), ..., sin(x 2^(n-1)), cos(x 2^(n-1))] (gaussian_model.py:33-82, log sampling)."""
     freqs = 2.0 ** torch.linspace(0.0, n_freqs - 1, steps=n_freqs, device=x.device)
@@ -90,12 +169,23 @@ class DirectTemporalNeRF(nn.Module):
         self._time_out_rot = nn.Linear(W, 4)
         self._time_out_shs = nn.Linear(W, 48)
 
+    def _use_fused(self, x: torch.Tensor) -> bool:
+        """The fused bf16 kernel (gsd_mlp.hip) serves the bf16 evaluation without autograd on a HIP device, for
+        the reference architecture (8 x 256, skip after layer 4, 10 frequencies); GSD_MLP_TORCH=1 keeps torch."""
+        if self.compute_dtype != torch.bfloat16 or x.device.type != "cuda" or os.environ.get("GSD_MLP_TORCH"):
+            return False
+        if (self.D, self.W, self.n_freqs, self.skips) != (8, 256, 10, (4,)):
+            return False
+        return not (torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())))
+
     def forward(self, x: torch.Tensor, ts: torch.Tensor, iteration: int):
         """-> (dx (P,3), d_scale (P,3), d_rot (P,4), d_sh (P,48)) as in gaussian_model.py:290-316."""
         P = x.shape[0]
         if iteration < self.zero_before:
             z = x.new_zeros
             return z(P, 3), z(P, 3), z(P, 4), z(P, 48)
+        if self._use_fused(x):
+            return _fused_forward(self, x, ts)
         ex = positional_encoding(x, self.n_freqs)
         et = positional_encoding(ts, self.n_freqs)
         dt = self.compute_dtype if self.compute_dtype != torch.float32 else ex.dtype  # f32: the input's own

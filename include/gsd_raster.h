@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 9
+#define GSD_ABI_VERSION 10
 
 enum {
     GSD_OK = 0,
@@ -326,6 +326,18 @@ int gsd_densify_stats(int32_t P, const float* viewspace_grad, const int32_t* rad
  * (256-B aligned). */
 size_t gsd_knn_workspace_bytes(int32_t P);
 int gsd_knn_mean_dist2(int32_t P, const float* points, float* mean_dist2, void* workspace, void* stream);
+
+/* Deformation network forward on the bf16 matrix cores (ABI 10; gsd_mlp.hip): DirectTemporalNeRF
+ * (scene/gaussian_model.py:242-316, the positional encoding :33-82) evaluated as the module does under
+ * autocast-bf16, one kernel, every activation in registers.  Replaces the module's forward call
+ * (gaussian_model.py:290-316) when no gradient is needed.  x (P,3), t (P) float32; frags:
+ * gsd_deform_mlp_fragments() 16-byte A-operand fragments (bf16 weights, K-permuted and fragment-major, packed by
+ * gsd_amd.deform_mlp.pack_fused_mlp); bias: gsd_deform_mlp_biases() float32 (bf16-rounded, packed per lane);
+ * both 16-B aligned.  Outputs float32 (P,3) / (P,3) / (P,4) / (P,48): dx, d log-scale, d quaternion, dSH. */
+int32_t gsd_deform_mlp_fragments(void);
+int32_t gsd_deform_mlp_biases(void);
+int gsd_deform_mlp_forward_bf16(int32_t P, const float* x, const float* t, const void* frags, const float* bias,
+                                float* d_xyz, float* d_scale, float* d_rot, float* d_sh, void* stream);
 
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead

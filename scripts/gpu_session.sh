@@ -1,11 +1,5 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
-for v in 0 1 0 1; do
-if [ $v = 1 ]; then export GSD_BENCH_BARE_BACKWARD=1; else unset GSD_BENCH_BARE_BACKWARD; fi
-timeout -k 10 200 python bench.py --steps 300 --warmup 20 --cpu-baseline off > gpurun_out/b_$v.log 2>&1 || exit 1
-python - "$v" <<'PY'
-import json,sys
-d=json.loads(open(f"gpurun_out/b_{sys.argv[1]}.log").read().strip().splitlines()[-1])
-print("bare" if sys.argv[1]=="1" else "seed", d["value"], d["ms_per_step"], d["fwd_bwd_ms_per_view"], d["kernels_ms"]["l1_ssim"])
-PY
-done
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/mlp; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_mlp.py > gpurun_out/mlp/t.log 2>&1; rc=$?; grep -E "PASS|FAIL|Error|assert" gpurun_out/mlp/t.log | head -30; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 scripts/prof_deform_mlp.py > gpurun_out/mlp/mlp.log 2>&1 || { tail -20 gpurun_out/mlp/mlp.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/mlp/mlp.log

@@ -57,6 +57,13 @@ def main():
 
         for _ in range(3):
             fwd_bwd()
+        if dt == torch.bfloat16:   # no-grad forward: the fused HIP kernel (gsd_mlp.hip) vs torch layer by layer
+            os.environ["GSD_MLP_TORCH"] = "1"
+            fwd()
+            t_ms = median_ms(fwd, a.iters)
+            del os.environ["GSD_MLP_TORCH"]
+            fwd()
+            print("bfloat16  P=%d  no-grad fwd torch %.3f ms (%.1f TFLOP/s)" % (a.P, t_ms, fpg * a.P / (t_ms * 1e-3) / 1e12))
         f_ms = median_ms(fwd, a.iters)
         fb_ms = median_ms(fwd_bwd, a.iters)
         f_tf = fpg * a.P / (f_ms * 1e-3) / 1e12

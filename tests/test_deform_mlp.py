@@ -75,3 +75,82 @@ def test_split_k_gradients_match_plain_linear_layers():
     # the module returns float32 outputs (as the reference's .float()), so its gradients carry float32 rounding
     for a, b in zip(grads["fused"], grads["plain"]):
         assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max())
+
+
+def _emulate_fused_mlp(frags, bias, x, t):
+    """The arithmetic of k_mlp_fwd (gsd_mlp.hip) lane by lane on the CPU, from the packed buffers alone:
+    v_mfma_f32_32x32x16_bf16's operand maps (lane l = 32 h + r holds A[r][8 h + j] and B[8 h + j][r]; register
+    `reg` of the accumulator is D[(reg&3) + 8 (reg>>2) + 4 h][r]), the accumulator registers 8 s .. 8 s + 7
+    reused as the next layer's B fragment of k-step 2 rb + s, bf16 rounding where the kernel rounds.  x (32,3),
+    t (32,): one wave."""
+    import numpy as np
+
+    from gsd_amd.deform_mlp import positional_encoding
+    bf = lambda a: torch.as_tensor(a, dtype=torch.float32).to(torch.bfloat16).float().numpy()  # noqa: E731
+    F = frags.float().numpy().reshape(-1, 64, 8)   # [fragment][lane][j]
+    Bz = bias.numpy()
+    ks_of = [6, 16, 16, 16, 16, 20, 16, 16, 16]
+    rb_of = [8] * 8 + [2]
+    enc = torch.cat((positional_encoding(torch.as_tensor(x)), positional_encoding(torch.as_tensor(t)[:, None])), -1)
+    enc = np.concatenate((bf(enc), np.zeros((32, 12), np.float32)), 1)   # (32 Gaussians, 96)
+    lanes = np.arange(64)
+    h, r = lanes >> 5, lanes & 31
+    # B fragments: bfr[ks][lane][j]
+    enc_fr = np.stack([enc[r[:, None], 16 * ks + 8 * h[:, None] + np.arange(8)[None, :]] for ks in range(6)])
+    act = enc_fr
+    fo = bo = 0
+    regs = np.arange(16)
+    for L in range(9):
+        KS, RB = ks_of[L], rb_of[L]
+        B = np.concatenate((enc_fr[:4], act)) if L == 5 else act
+        acc = np.zeros((RB, 64, 16), np.float64)
+        for ks in range(KS):
+            # B matrix (16 x 32) of this k-step from the lanes' fragments
+            Bm = np.zeros((16, 32))
+            Bm[8 * h[:, None] + np.arange(8)[None, :], r[:, None]] = B[ks]
+            for rb in range(RB):
+                A = np.zeros((32, 16))
+                A[r[:, None], 8 * h[:, None] + np.arange(8)[None, :]] = F[fo + ks * RB + rb]
+                D = A @ Bm                                   # (32 rows, 32 Gaussians)
+                acc[rb] += D[(regs[None, :] & 3) + 8 * (regs[None, :] >> 2) + 4 * h[:, None], r[:, None]]
+        fo += KS * RB
+        bl = Bz[bo: bo + RB * 32].reshape(RB, 2, 16)
+        bo += RB * 32
+        v = acc.astype(np.float32) + bl[:, h, :]            # (RB, lane, reg)
+        if L < 8:
+            v = bf(np.maximum(v, 0.0))
+            act = np.stack([v[rb, :, 8 * s: 8 * s + 8] for rb in range(RB) for s in range(2)])   # (16, lane, 8)
+        else:
+            out = np.zeros((32, 64), np.float32)
+            f = 32 * np.arange(RB)[:, None, None] + ((regs & 3) + 8 * (regs >> 2))[None, None, :] + 4 * h[None, :, None]
+            out[np.broadcast_to(r[None, :, None], f.shape), f] = bf(v)
+            return out[:, :58]
+
+
+def test_fused_mlp_packing_emulated():
+    """pack_fused_mlp's layout and k permutation, checked by emulating the kernel's MFMA operand maps on the CPU
+    (no GPU needed): the emulated outputs equal the module's float32 forward within bf16 rounding."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF, pack_fused_mlp
+    torch.manual_seed(3)
+    net = DirectTemporalNeRF()
+    with torch.no_grad():   # larger weights than the default init so every layer's ReLU pattern matters
+        for p in net.parameters():
+            p.mul_(2.0)
+    frags, bias = pack_fused_mlp(net)
+    x = torch.rand(32, 3) * 2 - 1
+    t = torch.full((32,), 0.4)
+    got = torch.as_tensor(_emulate_fused_mlp(frags, bias, x.numpy(), t.numpy()))
+    with torch.no_grad():
+        ref = torch.cat(net(x, t[:, None], 5000), -1)
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 3e-2, err
+    # and a wrong permutation is caught: natural k order in the hidden layers breaks it
+    import gsd_amd.deform_mlp as dm
+    saved = dm._PERM16
+    try:
+        dm._PERM16 = tuple(range(16))
+        f2, b2 = pack_fused_mlp(net)
+    finally:
+        dm._PERM16 = saved
+    bad = torch.as_tensor(_emulate_fused_mlp(f2, b2, x.numpy(), t.numpy()))
+    assert float((bad - ref).abs().max() / ref.abs().max()) > 0.1

@@ -1,0 +1,83 @@
+"""The fused deformation-network forward (gsd_mlp.hip, gsd_deform_mlp_forward_bf16) on the GPU against the
+module's torch bf16 path (the same rounding points, hipBLASLt's accumulation order), its float32 forward, and the
+lane-level CPU emulation of the kernel (tests/test_deform_mlp.py).  P off the 32- and 128-Gaussian grains."""
+from __future__ import annotations
+
+import os
+
+import pytest
+import torch
+
+from conftest import PKG  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(seed, scale=1.0):
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    torch.manual_seed(seed)
+    net = DirectTemporalNeRF(dtype=torch.bfloat16)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(scale)
+    return net.cuda()
+
+
+@pytest.mark.parametrize("P", [1, 77, 5003])
+def test_fused_mlp_matches_torch_bf16_and_f32(P):
+    from gsd_amd import _native
+    net = _net(11, 2.0)
+    g = torch.Generator().manual_seed(P)
+    x = (torch.rand(P, 3, generator=g) * 4 - 2).cuda()
+    t = torch.full((P, 1), 0.35, device="cuda")
+    lib = _native.load()
+    lib.gsd_timing_enable(1)
+    lib.gsd_timing_reset()
+    with torch.no_grad():
+        fused = torch.cat(net(x, t, 5000), -1)
+    names = (torch.zeros(32 * 64, dtype=torch.uint8)).numpy()
+    import ctypes
+    buf = ctypes.create_string_buffer(32 * 64)
+    n = lib.gsd_timing_collect(64, buf, None, None)
+    lib.gsd_timing_enable(0)
+    launched = [buf.raw[32 * i: 32 * i + 32].split(b"\0")[0].decode() for i in range(n)]
+    assert "deform_mlp" in launched   # the HIP kernel ran, not the torch path
+    os.environ["GSD_MLP_TORCH"] = "1"
+    try:
+        with torch.no_grad():
+            ref_bf16 = torch.cat(net(x, t, 5000), -1)
+    finally:
+        del os.environ["GSD_MLP_TORCH"]
+    net32 = _net(11, 2.0)
+    net32.compute_dtype = torch.float32
+    with torch.no_grad():
+        ref32 = torch.cat(net32(x, t, 5000), -1)
+    assert torch.isfinite(fused).all()
+    scale = float(ref32.abs().max())
+    assert float((fused - ref_bf16).abs().max()) <= 2e-2 * scale
+    assert float((fused - ref32).abs().max()) <= 4e-2 * scale
+    # most outputs are bit-identical to torch's bf16 path (same rounding points, different summation order)
+    assert float((fused == ref_bf16).float().mean()) > 0.5
+
+
+def test_fused_mlp_matches_lane_emulation():
+    from test_deform_mlp import _emulate_fused_mlp
+
+    from gsd_amd.deform_mlp import pack_fused_mlp
+    net = _net(12, 2.0)
+    x = (torch.rand(32, 3) * 2 - 1)
+    t = torch.full((32,), 0.4)
+    with torch.no_grad():
+        got = torch.cat(net(x.cuda(), t[:, None].cuda(), 5000), -1).cpu()
+    frags, bias = pack_fused_mlp(net)
+    want = torch.as_tensor(_emulate_fused_mlp(frags.cpu(), bias.cpu(), x.numpy(), t.numpy()))
+    assert float((got - want).abs().max()) <= 1e-2 * float(want.abs().max())
+
+
+def test_fused_mlp_not_used_with_grad():
+    net = _net(13)
+    x = torch.rand(100, 3, device="cuda", requires_grad=True)
+    t = torch.full((100, 1), 0.1, device="cuda")
+    outs = net(x, t, 5000)
+    sum(o.sum() for o in outs).backward()   # the torch path, differentiable
+    assert x.grad is not None and torch.isfinite(x.grad).all()
