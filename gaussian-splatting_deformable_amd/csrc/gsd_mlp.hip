@@ -11,7 +11,8 @@
 // conversion, the B operand of the next layer with no lane movement and no LDS.  The k order inside each
 // 16-wide k-step is then permuted (element j of lane half h is feature 8(j>>2) + 4h + (j&3) of the step); the
 // host packs the weights with the same permutation (gsd_amd.deform_mlp.pack_fused_mlp).  The weights (1008 KB
-// in bf16) are read as A fragments straight from L2: 1 KB per wave per MFMA, coalesced, one k-step ahead.
+// in bf16) are read as A fragments straight from L2: 1 KB per wave per k-step and row block, coalesced, one
+// k-step ahead; each feeds the wave's two column blocks of 32 Gaussians.
 //
 // Layers (k-steps KS of 16 inputs x row blocks RB of 32 outputs):
 //   0      cat(enc(x) 63, enc(t) 21) = 84 -> 96 (natural order)       KS  6, RB 8
@@ -21,12 +22,19 @@
 //   heads  dx 3 | d log-scale 3 | d quaternion 4 | dSH 48 = 58 -> 64  KS 16, RB 2
 // Bias + ReLU in f32 on the accumulators, each activation rounded to bf16 (as autocast's bf16 GEMM outputs);
 // the heads' outputs rounded to bf16 and returned as f32 (the module's .float()).
+#include <cstdlib>
+
 #include "gsd_kernels.h"
 
 namespace gsd {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#ifndef GSD_MLP_PREFETCH1
+#define GSD_MLP_PREFETCH1 2
+#endif
+constexpr int kMlpPrefetch1 = GSD_MLP_PREFETCH1;  // NC = 1: k-steps of weight fragments in flight
 
 __host__ __device__ constexpr int mlp_ks(int l) { return l == 0 ? 6 : (l == 5 ? 20 : 16); }
 __host__ __device__ constexpr int mlp_rb(int l) { return l == kMlpLayers - 1 ? 2 : 8; }
@@ -62,42 +70,51 @@ __device__ __forceinline__ float enc_feature(int k, float x0, float x1, float x2
     return 0.f;
 }
 
-// acc[rb] = sum over the k-steps of W-fragment(ks, rb) x in(ks); the first KS0 steps from in0, the rest from in1.
-// The fragments of a layer are laid out [ks][rb][lane] (one 1-KB wave load each, a k-step's RB of them
-// contiguous); the next k-step's are loaded while this one's MFMAs run, and a scheduling barrier per k-step keeps
-// the compiler from hoisting the whole layer's loads (which took every register and spilled).
-template <int KS0, int KS1, int RB>
-__device__ __forceinline__ void mlp_layer(const bf16x8* __restrict__ w, const bf16x8 (&in0)[KS0 > 0 ? KS0 : 1],
-                                          const bf16x8 (&in1)[KS1 > 0 ? KS1 : 1], f32x16 (&acc)[RB], int lane) {
+// acc[c][rb] = sum over the k-steps of W-fragment(ks, rb) x in_c(ks), for the wave's NC column blocks of 32
+// Gaussians (each A fragment feeds NC MFMAs); the first KS0 steps from in0, the rest from in1.  The fragments of a
+// layer are laid out [ks][rb][lane] (one 1-KB wave load each, a k-step's RB of them contiguous); the next k-step's
+// are loaded while this one's MFMAs run, and a scheduling barrier per k-step keeps the compiler from hoisting the
+// whole layer's loads (which took every register and spilled).  (Sharing each k-step's fragments among the
+// workgroup's four waves through an LDS double buffer, one barrier per step, was slower: 2.32 ms against 1.75 at
+// P = 1M, NC = 1.)
+template <int NC, int KS0, int KS1, int RB>
+__device__ __forceinline__ void mlp_layer(const bf16x8* __restrict__ w, const bf16x8 (&in0)[NC][KS0 > 0 ? KS0 : 1],
+                                          const bf16x8 (&in1)[NC][KS1 > 0 ? KS1 : 1], f32x16 (&acc)[NC][RB],
+                                          int lane) {
     constexpr int KS = KS0 + KS1;
+    constexpr int D = NC == 1 ? kMlpPrefetch1 : 1;  // k-steps of fragments in flight (registers: D x RB x 4)
     const bf16x8* wl = w + lane;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x16{};
-    bf16x8 a[RB];
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) a[rb] = wl[rb * 64];
+        for (int rb = 0; rb < RB; ++rb) acc[c][rb] = f32x16{};
+    bf16x8 a[D + 1][RB];  // ring: step ks reads slot ks % (D + 1)
+#pragma unroll
+    for (int d = 0; d < D && d < KS; ++d)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) a[d][rb] = wl[(d * RB + rb) * 64];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 an[RB];
-        if (ks + 1 < KS) {
+        if (ks + D < KS) {
 #pragma unroll
-            for (int rb = 0; rb < RB; ++rb) an[rb] = wl[((ks + 1) * RB + rb) * 64];
+            for (int rb = 0; rb < RB; ++rb) a[(ks + D) % (D + 1)][rb] = wl[((ks + D) * RB + rb) * 64];
         }
-        const bf16x8 b = ks < KS0 ? in0[ks < KS0 ? ks : 0] : in1[ks >= KS0 ? ks - KS0 : 0];
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rb], b, acc[rb], 0, 0, 0);
+        for (int c = 0; c < NC; ++c) {
+            const bf16x8 b = ks < KS0 ? in0[c][ks < KS0 ? ks : 0] : in1[c][ks >= KS0 ? ks - KS0 : 0];
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+                acc[c][rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks % (D + 1)][rb], b, acc[c][rb], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        if (ks + 1 < KS) {
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) a[rb] = an[rb];
-        }
     }
 }
 
 // bias (packed per lane: [rb][h][reg]), ReLU, bf16: accumulator registers 8 s .. 8 s + 7 of row block rb become
 // k-step 2 rb + s of the next layer's B operand
-__device__ __forceinline__ void mlp_hidden_epilogue(const f32x16 (&acc)[8], const float* __restrict__ bias, int h,
-                                                    bf16x8 (&act)[16]) {
+template <int NC>
+__device__ __forceinline__ void mlp_hidden_epilogue(const f32x16 (&acc)[NC][8], const float* __restrict__ bias, int h,
+                                                    bf16x8 (&act)[NC][16]) {
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) {
         const float4* bq = reinterpret_cast<const float4*>(bias + (rb * 2 + h) * 16);
@@ -111,73 +128,103 @@ __device__ __forceinline__ void mlp_hidden_epilogue(const f32x16 (&acc)[8], cons
             bv[4 * q + 3] = v.w;
         }
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int c = 0; c < NC; ++c)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) act[2 * rb + s][j] = (__bf16)fmaxf(acc[rb][8 * s + j] + bv[8 * s + j], 0.f);
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    act[c][2 * rb + s][j] = (__bf16)fmaxf(acc[c][rb][8 * s + j] + bv[8 * s + j], 0.f);
     }
 }
 
+// NC column blocks of 32 Gaussians per wave (1 or 2): 2 halves the weight traffic from L2 per MFMA at twice the
+// accumulator registers
+template <int NC>
 __global__ __launch_bounds__(256) void k_mlp_fwd(MlpParams p) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
-    const int g = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (lane & 31);
-    const bool live = g < p.P;
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f, t = 0.f;
-    if (live) {
-        x0 = p.x[3 * g];
-        x1 = p.x[3 * g + 1];
-        x2 = p.x[3 * g + 2];
-        t = p.t[g];
-    }
+    const int g0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 * NC + (lane & 31);  // column block c: g0 + 32 c
     // The encoding, 96 bf16 features per Gaussian, through LDS: lane half h computes features [48 h, 48 h + 48)
-    // of its Gaussian in a loop (one inlined copy of sinf / cosf: 96 unrolled copies spilled ~700 SGPRs), then
-    // layer 0's B operand is read back in natural k order -- lane half h holds features 16 ks + 8 h + j.
-    __shared__ __attribute__((aligned(16))) __bf16 s_enc[4][32][96];
+    // of its Gaussians in a loop (one inlined copy of sinf / cosf: 96 unrolled copies spilled ~700 SGPRs), then
+    // the B operand of layer 0 (and the encoding's k-steps of layer 5) is read back in natural k order -- lane
+    // half h holds features 16 ks + 8 h + j.
+    __shared__ __attribute__((aligned(16))) __bf16 s_enc[4][32 * NC][96];
     __bf16(*my)[96] = s_enc[threadIdx.x >> 6];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int g = g0 + 32 * c;
+        float x0 = 0.f, x1 = 0.f, x2 = 0.f, t = 0.f;
+        if (g < p.P) {
+            x0 = p.x[3 * g];
+            x1 = p.x[3 * g + 1];
+            x2 = p.x[3 * g + 2];
+            t = p.t[g];
+        }
 #pragma unroll 1
-    for (int k = 48 * h; k < 48 * h + 48; ++k) my[lane & 31][k] = (__bf16)enc_feature(k, x0, x1, x2, t);
+        for (int k = 48 * h; k < 48 * h + 48; ++k) my[32 * c + (lane & 31)][k] = (__bf16)enc_feature(k, x0, x1, x2, t);
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    bf16x8 enc[6];
-#pragma unroll
-    for (int ks = 0; ks < 6; ++ks) enc[ks] = *reinterpret_cast<const bf16x8*>(&my[lane & 31][16 * ks + 8 * h]);
     const bf16x8* W = reinterpret_cast<const bf16x8*>(p.frags);
-    f32x16 acc[8];
-    bf16x8 act[16];
-    const bf16x8 none[1] = {};
-    mlp_layer<6, 0, 8>(W + mlp_frag_off(0), enc, none, acc, lane);
-    mlp_hidden_epilogue(acc, p.bias + mlp_bias_off(0), h, act);
+    f32x16 acc[NC][8];
+    bf16x8 act[NC][16];
+    const bf16x8 none[NC][1] = {};
+    {
+        bf16x8 enc[NC][6];
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int ks = 0; ks < 6; ++ks)
+                enc[c][ks] = *reinterpret_cast<const bf16x8*>(&my[32 * c + (lane & 31)][16 * ks + 8 * h]);
+        mlp_layer<NC, 6, 0, 8>(W + mlp_frag_off(0), enc, none, acc, lane);
+    }
+    mlp_hidden_epilogue<NC>(acc, p.bias + mlp_bias_off(0), h, act);
 #pragma unroll
     for (int l = 1; l < 8; ++l) {
-        if (l == 5) {  // cat(enc(x), h): enc's first four k-steps (feature 63 = t meets a zero weight column)
-            bf16x8 ex[4] = {enc[0], enc[1], enc[2], enc[3]};
-            mlp_layer<4, 16, 8>(W + mlp_frag_off(5), ex, act, acc, lane);
+        if (l == 5) {  // cat(enc(x), h): the encoding's first four k-steps (feature 63 = t meets a zero weight column)
+            bf16x8 ex[NC][4];
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks)
+                    ex[c][ks] = *reinterpret_cast<const bf16x8*>(&my[32 * c + (lane & 31)][16 * ks + 8 * h]);
+            mlp_layer<NC, 4, 16, 8>(W + mlp_frag_off(5), ex, act, acc, lane);
         } else {
-            mlp_layer<0, 16, 8>(W + mlp_frag_off(l), none, act, acc, lane);
+            mlp_layer<NC, 0, 16, 8>(W + mlp_frag_off(l), none, act, acc, lane);
         }
-        mlp_hidden_epilogue(acc, p.bias + mlp_bias_off(l), h, act);
+        mlp_hidden_epilogue<NC>(acc, p.bias + mlp_bias_off(l), h, act);
     }
-    f32x16 out[2];
-    mlp_layer<0, 16, 2>(W + mlp_frag_off(8), none, act, out, lane);
-    if (!live) return;
+    f32x16 out[NC][2];
+    mlp_layer<NC, 0, 16, 2>(W + mlp_frag_off(8), none, act, out, lane);
     const float* bh = p.bias + mlp_bias_off(8);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int c = 0; c < NC; ++c) {
+        const int g = g0 + 32 * c;
+        if (g >= p.P) continue;
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int f = 32 * rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;  // this register's output feature
-            const float v = (float)(__bf16)(out[rb][reg] + bh[(rb * 2 + h) * 16 + reg]);
-            if (f < 3) p.d_xyz[3 * g + f] = v;
-            else if (f < 6) p.d_scale[3 * g + f - 3] = v;
-            else if (f < 10) p.d_rot[4 * g + f - 6] = v;
-            else if (f < 58) p.d_sh[48 * g + f - 10] = v;
-        }
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int f = 32 * rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;  // this register's output feature
+                const float v = (float)(__bf16)(out[c][rb][reg] + bh[(rb * 2 + h) * 16 + reg]);
+                if (f < 3) p.d_xyz[3 * g + f] = v;
+                else if (f < 6) p.d_scale[3 * g + f - 3] = v;
+                else if (f < 10) p.d_rot[4 * g + f - 6] = v;
+                else if (f < 58) p.d_sh[48 * g + f - 10] = v;
+            }
+    }
 }
 
 void launch_mlp_fwd(const MlpParams& p, hipStream_t s) {
     if (p.P <= 0) return;
-    const int waves = (p.P + 31) / 32;
-    hipLaunchKernelGGL(k_mlp_fwd, dim3((waves + 3) / 4), dim3(256), 0, s, p);
+    static const int nc = [] {  // GSD_MLP_NC: column blocks per wave (experiment)
+        const char* e = getenv("GSD_MLP_NC");
+        return e && atoi(e) == 1 ? 1 : 2;
+    }();
+    const int per_block = 4 * 32 * nc;
+    const dim3 grid((p.P + per_block - 1) / per_block);
+    if (nc == 1) hipLaunchKernelGGL(k_mlp_fwd<1>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_mlp_fwd<2>, grid, dim3(256), 0, s, p);
 }
 
 }  // namespace gsd
