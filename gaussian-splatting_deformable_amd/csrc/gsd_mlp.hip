@@ -12,7 +12,7 @@
 // 16-wide k-step is then permuted (element j of lane half h is feature 8(j>>2) + 4h + (j&3) of the step); the
 // host packs the weights with the same permutation (gsd_amd.deform_mlp.pack_fused_mlp).  The weights (1008 KB
 // in bf16) are read as A fragments straight from L2: 1 KB per wave per k-step and row block, coalesced, one
-// k-step ahead; each feeds the wave's two column blocks of 32 Gaussians.
+// k-step ahead.  Two waves per SIMD (256 registers each).
 //
 // Layers (k-steps KS of 16 inputs x row blocks RB of 32 outputs):
 //   0      cat(enc(x) 63, enc(t) 21) = 84 -> 96 (natural order)       KS  6, RB 8
@@ -32,7 +32,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #ifndef GSD_MLP_PREFETCH1
-#define GSD_MLP_PREFETCH1 2
+#define GSD_MLP_PREFETCH1 1
 #endif
 constexpr int kMlpPrefetch1 = GSD_MLP_PREFETCH1;  // NC = 1: k-steps of weight fragments in flight
 
@@ -137,10 +137,11 @@ __device__ __forceinline__ void mlp_hidden_epilogue(const f32x16 (&acc)[NC][8], 
     }
 }
 
-// NC column blocks of 32 Gaussians per wave (1 or 2): 2 halves the weight traffic from L2 per MFMA at twice the
-// accumulator registers
+// NC column blocks of 32 Gaussians per wave (1 or 2).  NC = 1 fits 256 registers (5 spilled), so two waves per
+// SIMD hide each other's stalls: 1.33 ms at P = 1M.  NC = 2 halves the weight traffic from L2 per MFMA but needs
+// ~500 registers, one wave per SIMD: 1.57 ms.
 template <int NC>
-__global__ __launch_bounds__(256) void k_mlp_fwd(MlpParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NC == 1 ? 2 : 1))) void k_mlp_fwd(MlpParams p) {
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int g0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 * NC + (lane & 31);  // column block c: g0 + 32 c
     // The encoding, 96 bf16 features per Gaussian, through LDS: lane half h computes features [48 h, 48 h + 48)
@@ -219,7 +220,7 @@ void launch_mlp_fwd(const MlpParams& p, hipStream_t s) {
     if (p.P <= 0) return;
     static const int nc = [] {  // GSD_MLP_NC: column blocks per wave (experiment)
         const char* e = getenv("GSD_MLP_NC");
-        return e && atoi(e) == 1 ? 1 : 2;
+        return e && atoi(e) == 2 ? 2 : 1;
     }();
     const int per_block = 4 * 32 * nc;
     const dim3 grid((p.P + per_block - 1) / per_block);
