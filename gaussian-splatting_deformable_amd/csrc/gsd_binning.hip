@@ -141,13 +141,27 @@ __global__ __launch_bounds__(256) void k_colscan_final(HistParams p, uint32_t* _
     if (t >= p.num_tiles) return;
     const int T = p.num_tiles;
     uint32_t base = 0;
+#pragma unroll 8
     for (int s = 0; s < (int)blockIdx.y; ++s) base += p.part[(size_t)s * T + t];
     const int b0 = blockIdx.y * kColSeg, b1 = min(p.num_blocks, b0 + kColSeg);
-    for (int b = b0; b < b1; ++b) {
-        uint32_t* h = p.hist + (size_t)b * T + t;
-        const uint32_t v = *h;
-        *h = base;
-        base += v;
+    // the segment's rows loaded together (independent of the running base), then the exclusive prefix written:
+    // one round of load latency instead of one per row
+    if (b1 - b0 == kColSeg) {
+        uint32_t v[kColSeg];
+#pragma unroll
+        for (int i = 0; i < kColSeg; ++i) v[i] = p.hist[(size_t)(b0 + i) * T + t];
+#pragma unroll
+        for (int i = 0; i < kColSeg; ++i) {
+            p.hist[(size_t)(b0 + i) * T + t] = base;
+            base += v[i];
+        }
+    } else {
+        for (int b = b0; b < b1; ++b) {
+            uint32_t* h = p.hist + (size_t)b * T + t;
+            const uint32_t v = *h;
+            *h = base;
+            base += v;
+        }
     }
     if ((int)blockIdx.y == (int)gridDim.y - 1) tile_count[t] = base;
 }

@@ -1,7 +1,5 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/mlp; export TMPDIR=/tmp
-for nc in 1 2 1 2; do
-GSD_MLP_NC=$nc timeout -k 10 300 python3 scripts/prof_deform_mlp.py --iters 30 > gpurun_out/mlp/m.log 2>&1 || { tail -20 gpurun_out/mlp/m.log; exit 1; }
-echo "NC=$nc"; grep "bfloat16.*fwd+bwd" gpurun_out/mlp/m.log | cut -c1-70
-done
-GSD_MLP_NC=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_mlp.py > gpurun_out/mlp/t.log 2>&1; rc=$?; tail -1 gpurun_out/mlp/t.log; exit $rc
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/cs; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py > gpurun_out/cs/t.log 2>&1; rc=$?; tail -1 gpurun_out/cs/t.log; [ $rc -ne 0 ] && exit $rc
+rm -rf gpurun_out/cs/prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cs/prof -o b -- python3 bench.py --steps 50 --warmup 5 --cpu-baseline off > gpurun_out/cs/b.log 2>&1 || exit 1
