@@ -1,5 +1,5 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/cs; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py > gpurun_out/cs/t.log 2>&1; rc=$?; tail -1 gpurun_out/cs/t.log; [ $rc -ne 0 ] && exit $rc
-rm -rf gpurun_out/cs/prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cs/prof -o b -- python3 bench.py --steps 50 --warmup 5 --cpu-baseline off > gpurun_out/cs/b.log 2>&1 || exit 1
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/mlp1; export TMPDIR=/tmp
+rm -rf gpurun_out/mlp1/prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/mlp1/prof -o m -- python3 scripts/prof_mlp_once.py > gpurun_out/mlp1/prof.log 2>&1 || { tail gpurun_out/mlp1/prof.log; exit 1; }
+grep done gpurun_out/mlp1/prof.log; cut -d, -f1-4 gpurun_out/mlp1/prof/m_kernel_stats.csv | cut -c1-120
