@@ -1,5 +1,6 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/mlp1; export TMPDIR=/tmp
-rm -rf gpurun_out/mlp1/prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/mlp1/prof -o m -- python3 scripts/prof_mlp_once.py > gpurun_out/mlp1/prof.log 2>&1 || { tail gpurun_out/mlp1/prof.log; exit 1; }
-grep done gpurun_out/mlp1/prof.log; cut -d, -f1-4 gpurun_out/mlp1/prof/m_kernel_stats.csv | cut -c1-120
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/mlp; export TMPDIR=/tmp
+for v in build build_sp build build_sp; do
+GSD_HIP_LIB=$GRAFT_REPO_ROOT/gaussian-splatting_deformable_amd/$v/libgsd_hip.so timeout -k 10 300 python3 scripts/prof_deform_mlp.py --iters 30 > gpurun_out/mlp/m.log 2>&1 || { tail -20 gpurun_out/mlp/m.log; exit 1; }
+echo "$v"; grep "bfloat16.*fwd+bwd" gpurun_out/mlp/m.log | cut -c1-70
+done
