@@ -285,6 +285,43 @@ def main():
     fwd_bwd_ms = fwd_bwd(True)
     fwd_bwd_synced_ms = fwd_bwd(False)
 
+    # the data-parallel exchange on its own (SURVEY.md 8(e) "all-reduce ms"), at the sizes of the step's: the
+    # all-gather of the per-view masked dL/dRGB rows (3P + 3 floats per rank) and the all-reduce of the rest of the
+    # gradient slab (every parameter but the SH pieces, which the ranks assemble from the gathered views); medians
+    # of 10 after 2 warm-ups, hipEvents on the current stream around the (synchronous) collective
+    exchange = None
+    if world > 1:
+        n_red = sum(p.numel() for p in pc.parameters()) - pc._features_dc.numel() - pc._features_rest.numel()
+        red = torch.zeros(n_red, device=dev)
+        row = torch.zeros(3 * P + 3, device=dev)
+        rows = torch.empty(world, 3 * P + 3, device=dev)
+        nccl = dist.get_backend() == "nccl"
+
+        def gather():
+            if nccl:
+                dist.all_gather_into_tensor(rows, row)
+            else:
+                dist.all_gather(list(rows.unbind(0)), row)
+
+        def timed_ms(fn):
+            ts = []
+            for it in range(12):
+                dist.barrier()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize()
+                if it >= 2:
+                    ts.append(e0.elapsed_time(e1))
+            ts.sort()
+            return ts[len(ts) // 2]
+
+        exchange = {"backend": dist.get_backend(),
+                    "allreduce_floats": int(n_red), "allreduce_ms": round(timed_ms(lambda: dist.all_reduce(red)), 4),
+                    "allgather_floats_per_rank": 3 * P + 3, "allgather_ms": round(timed_ms(gather), 4)}
+        del red, row, rows
+
     # per-kernel device times: a separate pass of full steps with the C-ABI's hipEvent timing on
     restore()
     kernel_times(enable=True, reset=True)
@@ -346,6 +383,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if exchange is not None:
+            res["exchange"] = exchange
         print(json.dumps(res), flush=True)
     if dist.is_initialized():
         dist.barrier()
