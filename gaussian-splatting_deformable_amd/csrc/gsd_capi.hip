@@ -254,12 +254,13 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
-                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kMlp, kNumKernels };
+                kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kMlp, kMlpBwd,
+                kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
                                                "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "sh_grad_views", "adam",         "densify_stats",
-                                               "knn",            "deform_mlp"};
+                                               "knn",            "deform_mlp",   "deform_mlp_relu_bias"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -880,6 +881,24 @@ int gsd_deform_mlp_forward_bf16(int32_t P, const float* x, const float* t, const
     gsd::MlpParams p{P, x, t, frags, bias, d_xyz, d_scale, d_rot, d_sh};
     hipStream_t s = as_stream(stream);
     timed(kMlp, s, [&] { gsd::launch_mlp_fwd(p, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int32_t gsd_relu_backward_bias_blocks(int64_t P, int32_t rows_per_block) {
+    return (P < 0 || rows_per_block <= 0) ? 0 : gsd::relu_bwd_bias_blocks(P, rows_per_block);
+}
+
+int gsd_relu_backward_bias(int64_t P, int32_t N, int32_t bf16, const void* grad_out, const void* out, void* grad_in,
+                           float* bias_partial, int32_t rows_per_block, void* stream) {
+    if (P < 0 || N <= 0 || (N & 1) || N > 512 || rows_per_block <= 0)
+        return fail(GSD_ERR_ARG, "relu_backward_bias: need P >= 0, even 0 < N <= 512, rows_per_block > 0");
+    if (P == 0) return GSD_OK;
+    if (!grad_out || !grad_in || !bias_partial) return fail(GSD_ERR_ARG, "null pointer argument");
+    hipStream_t s = as_stream(stream);
+    timed(kMlpBwd, s, [&] {
+        gsd::launch_relu_bwd_bias(P, N, bf16, grad_out, out, grad_in, bias_partial, rows_per_block, s);
+    });
     GSD_CHECK(false, s);
     return GSD_OK;
 }

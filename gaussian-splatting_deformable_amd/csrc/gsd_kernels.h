@@ -299,6 +299,9 @@ struct MlpParams {
     float* d_sh;         // (P,48)
 };
 void launch_mlp_fwd(const MlpParams& p, hipStream_t s);
+int relu_bwd_bias_blocks(long long P, int rows);
+void launch_relu_bwd_bias(long long P, int N, int bf16, const void* gy, const void* y, void* g, float* part,
+                          int rows, hipStream_t s);
 
 constexpr int kAdamMaxGroups = 16;
 struct AdamArgs {

@@ -229,3 +229,93 @@ void launch_mlp_fwd(const MlpParams& p, hipStream_t s) {
 }
 
 }  // namespace gsd
+
+namespace gsd {
+
+// ---- the deformation network's backward, between its GEMMs (gsd_amd.deform_mlp._Linear.backward) ----
+// g = gy where y > 0 (ReLU backward; every element when y is null) and the bias gradient's per-block column sums,
+// in one pass: torch ran threshold_backward and then sum(0) over g, reading the (P, N) gradient twice.  A
+// workgroup owns `rows` consecutive rows; a thread owns a column pair of every (256 / (N/2))-th row of them and
+// keeps its two sums in float32; the row lanes are combined through LDS in a fixed order, so part[block][c] is
+// deterministic and the caller's sum over blocks is too.
+template <typename T>
+struct Pair;
+template <>
+struct Pair<float> {
+    typedef float2 V;
+    __device__ static float lo(V v) { return v.x; }
+    __device__ static float hi(V v) { return v.y; }
+    __device__ static V zero() { return make_float2(0.f, 0.f); }
+    __device__ static V select(V v, V y, bool relu) {
+        return relu ? make_float2(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f) : v;
+    }
+};
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+template <>
+struct Pair<__bf16> {
+    typedef bf16x2 V;
+    __device__ static float lo(V v) { return (float)v.x; }
+    __device__ static float hi(V v) { return (float)v.y; }
+    __device__ static V zero() { return V{}; }
+    __device__ static V select(V v, V y, bool relu) {
+        if (!relu) return v;
+        V r = v;
+        if (!((float)y.x > 0.f)) r.x = (__bf16)0.f;
+        if (!((float)y.y > 0.f)) r.y = (__bf16)0.f;
+        return r;
+    }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_relu_bwd_bias(long long P, int N, const T* __restrict__ gy,
+                                                        const T* __restrict__ y, T* __restrict__ g,
+                                                        float* __restrict__ part, int rows) {
+    typedef typename Pair<T>::V V;
+    __shared__ float2 red[256];
+    const int half = N >> 1, lanes = 256 / half;  // threads per row, rows per pass
+    const int tid = threadIdx.x, cp = tid % half, rl = tid / half;
+    const long long r0 = (long long)blockIdx.x * rows, r1 = min(P, r0 + rows);
+    float s0 = 0.f, s1 = 0.f;
+    const bool relu = y != nullptr;
+    if (rl < lanes) {
+        const V* gy2 = reinterpret_cast<const V*>(gy);
+        const V* y2 = reinterpret_cast<const V*>(y);
+        V* g2 = reinterpret_cast<V*>(g);
+#pragma unroll 4
+        for (long long r = r0 + rl; r < r1; r += lanes) {
+            const long long e = r * half + cp;
+            const V v = Pair<T>::select(gy2[e], relu ? y2[e] : Pair<T>::zero(), relu);
+            g2[e] = v;
+            s0 += Pair<T>::lo(v);
+            s1 += Pair<T>::hi(v);
+        }
+    }
+    red[tid] = make_float2(s0, s1);
+    __syncthreads();
+    if (tid < half) {
+        float2 a = red[tid];
+        for (int l = 1; l < lanes; ++l) {
+            const float2 b = red[l * half + tid];
+            a.x += b.x;
+            a.y += b.y;
+        }
+        part[(size_t)blockIdx.x * N + 2 * tid] = a.x;
+        part[(size_t)blockIdx.x * N + 2 * tid + 1] = a.y;
+    }
+}
+
+int relu_bwd_bias_blocks(long long P, int rows) { return (int)((P + rows - 1) / rows); }
+
+void launch_relu_bwd_bias(long long P, int N, int bf16, const void* gy, const void* y, void* g, float* part,
+                          int rows, hipStream_t s) {
+    const int nb = relu_bwd_bias_blocks(P, rows);
+    if (nb <= 0) return;
+    if (bf16)
+        hipLaunchKernelGGL(k_relu_bwd_bias<__bf16>, dim3(nb), dim3(256), 0, s, P, N, (const __bf16*)gy,
+                           (const __bf16*)y, (__bf16*)g, part, rows);
+    else
+        hipLaunchKernelGGL(k_relu_bwd_bias<float>, dim3(nb), dim3(256), 0, s, P, N, (const float*)gy,
+                           (const float*)y, (float*)g, part, rows);
+}
+
+}  // namespace gsd

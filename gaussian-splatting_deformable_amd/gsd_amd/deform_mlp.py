@@ -42,6 +42,26 @@ def _weight_grad(g: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     return dw
 
 
+_RELU_ROWS = 512   # rows per workgroup of gsd_relu_backward_bias
+
+
+def _relu_bias_backward(gy: torch.Tensor, y):
+    """(g, db) on a HIP device in one pass (gsd_relu_backward_bias): g = gy where y > 0 (y None: gy) and the bias
+    gradient db = column sums of g in float32 (per-block partials summed in a fixed order)."""
+    from . import _native
+    from ._C import _ptr, _stream
+    lib = _native.load()
+    P, N = gy.shape
+    gy = gy.contiguous()
+    y = None if y is None else y.contiguous()
+    g = torch.empty_like(gy)
+    part = torch.empty(lib.gsd_relu_backward_bias_blocks(P, _RELU_ROWS), N, dtype=torch.float32, device=gy.device)
+    with torch.cuda.device(gy.device):
+        _native.check(lib.gsd_relu_backward_bias(P, N, int(gy.dtype == torch.bfloat16), _ptr(gy), _ptr(y), _ptr(g),
+                                                 _ptr(part), _RELU_ROWS, _stream(gy.device)))
+    return g, part.sum(0)
+
+
 class _Linear(torch.autograd.Function):
     """y = h W^T + b (then ReLU when `relu`), in h's dtype (f32 or bf16; W and b cast to it), with the split-K
     weight gradient above; dW and db come back in float32 (the parameters' dtype)."""
@@ -59,10 +79,15 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, gy):
         h, Wc, y = ctx.saved_tensors
         gy = gy.to(h.dtype)
-        g = torch.ops.aten.threshold_backward(gy, y, 0) if ctx.relu else gy.contiguous()  # one pass
+        if (gy.is_cuda and gy.dtype in (torch.float32, torch.bfloat16) and gy.dim() == 2 and gy.shape[1] % 2 == 0
+                and gy.shape[1] <= 512):
+            g, db = _relu_bias_backward(gy, y if ctx.relu else None)   # mask + bias gradient, one HIP pass
+        else:
+            g = torch.ops.aten.threshold_backward(gy, y, 0) if ctx.relu else gy.contiguous()
+            db = g.sum(0, dtype=torch.float32)
         dh = g @ Wc if ctx.needs_input_grad[0] else None
         dW = _weight_grad(g, h) if ctx.needs_input_grad[1] else None
-        db = g.sum(0, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        db = db if ctx.needs_input_grad[2] else None
         return dh, dW, db, None
 
 

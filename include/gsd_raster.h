@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 10
+#define GSD_ABI_VERSION 11
 
 enum {
     GSD_OK = 0,
@@ -338,6 +338,15 @@ int32_t gsd_deform_mlp_fragments(void);
 int32_t gsd_deform_mlp_biases(void);
 int gsd_deform_mlp_forward_bf16(int32_t P, const float* x, const float* t, const void* frags, const float* bias,
                                 float* d_xyz, float* d_scale, float* d_rot, float* d_sh, void* stream);
+
+/* The deformation network's backward between its GEMMs (ABI 11): grad_in = grad_out where out > 0 (ReLU
+ * backward, torch.ops.aten.threshold_backward; every element when out is NULL, the heads) and, in the same pass, the
+ * bias gradient's column sums per block of rows_per_block rows: bias_partial[(blocks, N)] float32, blocks =
+ * gsd_relu_backward_bias_blocks(P, rows_per_block); the caller sums them over the blocks (the bias gradient,
+ * gaussian_model.py:242-316 under autograd).  (P, N) row-major, N even and <= 512, float32 (bf16 = 0) or bf16. */
+int32_t gsd_relu_backward_bias_blocks(int64_t P, int32_t rows_per_block);
+int gsd_relu_backward_bias(int64_t P, int32_t N, int32_t bf16, const void* grad_out, const void* out, void* grad_in,
+                           float* bias_partial, int32_t rows_per_block, void* stream);
 
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead

@@ -1,6 +1,5 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/dp; export TMPDIR=/tmp
-GSD_DIST_BACKEND=gloo HSA_ENABLE_IPC_MODE_LEGACY=0 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/dp/b2.log 2>&1 || { tail -20 gpurun_out/dp/b2.log; exit 1; }
-grep '"metric"' gpurun_out/dp/b2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d.get('exchange'))"
-GSD_DP_ONE_RANK=1 HSA_ENABLE_IPC_MODE_LEGACY=0 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/dp/b1.log 2>&1 || { tail -20 gpurun_out/dp/b1.log; exit 1; }
-grep '"metric"' gpurun_out/dp/b1.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d.get('exchange'))"
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/mlp; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_mlp.py tests/test_gpu_train.py -k "mlp or relu or offset" > gpurun_out/mlp/t.log 2>&1; rc=$?; grep -E "passed|failed|Error|assert" gpurun_out/mlp/t.log | tail -5; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 scripts/prof_deform_mlp.py --iters 20 > gpurun_out/mlp/m.log 2>&1 || { tail -20 gpurun_out/mlp/m.log; exit 1; }
+grep "P=" gpurun_out/mlp/m.log

@@ -81,3 +81,52 @@ def test_fused_mlp_not_used_with_grad():
     outs = net(x, t, 5000)
     sum(o.sum() for o in outs).backward()   # the torch path, differentiable
     assert x.grad is not None and torch.isfinite(x.grad).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("P,N,relu", [(1, 256, True), (1000, 256, True), (5003, 58, False), (70_001, 256, True)])
+def test_relu_backward_bias_matches_torch(dtype, P, N, relu):
+    """gsd_relu_backward_bias (the MLP backward's ReLU mask + bias-gradient sums in one pass) against
+    threshold_backward and sum(0); the mask bit for bit, the sums within float32 reordering."""
+    from gsd_amd.deform_mlp import _relu_bias_backward
+    g0 = torch.Generator(device="cuda").manual_seed(P)
+    gy = torch.randn(P, N, device="cuda", generator=g0).to(dtype)
+    y = torch.randn(P, N, device="cuda", generator=g0).relu().to(dtype) if relu else None
+    g, db = _relu_bias_backward(gy, y)
+    want = torch.ops.aten.threshold_backward(gy, y, 0) if relu else gy
+    assert torch.equal(g, want)
+    ref = want.double().sum(0)
+    assert float((db.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(want.double().abs().sum(0).max()))
+
+
+def test_mlp_training_backward_matches_reference_torch_path():
+    """The module's backward on the GPU (split-K weight gradients, fused mask + bias kernel) against plain
+    F.linear autograd, float32."""
+    import torch.nn.functional as F
+
+    from gsd_amd.deform_mlp import positional_encoding
+    net = _net(14)
+    net.compute_dtype = torch.float32
+    P = 20_000
+    x = (torch.rand(P, 3, device="cuda") * 2 - 1)
+    t = torch.full((P, 1), 0.2, device="cuda")
+    w = [torch.randn(P, n, device="cuda") for n in (3, 3, 4, 48)]
+
+    def plain(xx):
+        ex, et = positional_encoding(xx), positional_encoding(t)
+        h = torch.cat((ex, et), -1)
+        for i, layer in enumerate(net._time):
+            h = F.relu(F.linear(h, layer.weight, layer.bias))
+            if i in net.skips:
+                h = torch.cat((ex, h), -1)
+        return [F.linear(h, m.weight, m.bias) for m in (net._time_out, net._time_out_scale, net._time_out_rot,
+                                                        net._time_out_shs)]
+
+    grads = {}
+    for name, fn in (("fused", lambda xx: net(xx, t, 5000)), ("plain", plain)):
+        net.zero_grad()
+        xx = x.clone().requires_grad_(True)
+        sum((o * wi).sum() for o, wi in zip(fn(xx), w)).backward()
+        grads[name] = [xx.grad] + [p.grad.clone() for p in net.parameters()]
+    for a, b in zip(grads["fused"], grads["plain"]):
+        assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-7
