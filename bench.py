@@ -25,6 +25,7 @@ oracle on one full view of the same workload.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -224,6 +225,7 @@ def main():
         nstep[0] = 0
         opt.flat.invalidate()   # as a fresh optimizer: no gradients yet
 
+    gc.collect()   # before the warmup, so the device is busy again when the timed steps start
     for _ in range(args.warmup):
         step()
     if dens is not None:
@@ -235,6 +237,13 @@ def main():
     if world > 1:
         dist.barrier()
     step_ev = [] if os.environ.get("GSD_BENCH_STEP_TIMES") else None   # diagnostics: per-step device times
+    # Python's cyclic garbage collector off inside the timed steps (as timeit does): a collection pass stalls the
+    # host, which paces the device through the per-step num_rendered read-back (+0.15 ms on one step of every
+    # ~10 at 1M Gaussians).  The collection is done before the warmup: a pause of the host here, with the device
+    # idle, let its clocks drop for the first timed steps.
+    no_gc = os.environ.get("GSD_BENCH_GC", "off") == "off"
+    if no_gc:
+        gc.disable()
     t0 = time.perf_counter()
     for i in range(args.steps):
         if step_ev is not None:
@@ -246,6 +255,8 @@ def main():
         if i == 0:
             K_start = int(gsdC.last_forward.get("num_rendered", 0))  # host value, already read by the forward
     torch.cuda.synchronize()
+    if no_gc:
+        gc.enable()
     if step_ev is not None and rank == 0:
         print("step ms:", " ".join("%.3f" % a.elapsed_time(b) for a, b in step_ev), file=sys.stderr)
     if world > 1:
