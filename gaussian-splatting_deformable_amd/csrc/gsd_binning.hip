@@ -28,13 +28,54 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     }
     return v;
 }
+// kLds (T <= kScanLdsTiles): the counts are loaded tile-interleaved (coalesced) into LDS, each thread scans its
+// run of `per` consecutive tiles there and leaves each tile's exclusive base in place, and the ranges / cursors go
+// out in a second tile-interleaved pass (end = the next tile's base).  Loaded and written straight from each
+// thread's run, every memory instruction touched 64 separate segments: 11.0 us at 1080p, 8.5 with the LDS passes
+// (the rest is the one workgroup's launch and barrier latency).
+constexpr int kScanLdsTiles = 32767;
+template <bool kLds>
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(int T, const uint32_t* __restrict__ tile_count,
                                                             uint2* __restrict__ ranges, uint32_t* __restrict__ cursor,
                                                             uint32_t* __restrict__ counters) {
+    extern __shared__ uint32_t s_base[];  // kLds: [T + 1], the counts (coalesced loads), then each tile's base
     __shared__ uint32_t s_wave[kScanThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int per = (T + kScanThreads - 1) / kScanThreads;
     const int b0 = min(T, tid * per), b1 = min(T, b0 + per);
+    if constexpr (kLds) {
+        for (int t = tid; t < T; t += kScanThreads) s_base[t] = tile_count[t];
+        __syncthreads();
+        uint32_t local = 0;
+        for (int i = b0; i < b1; ++i) local += s_base[i];
+        const uint32_t incl = wave_incl_scan(local, lane);
+        if (lane == 63) s_wave[wid] = incl;
+        __syncthreads();
+        if (wid == 0) {
+            uint32_t v = lane < kScanThreads / 64 ? s_wave[lane] : 0u;
+            v = wave_incl_scan(v, lane);
+            if (lane < kScanThreads / 64) s_wave[lane] = v;
+        }
+        __syncthreads();
+        uint32_t run = incl - local + (wid ? s_wave[wid - 1] : 0u);
+        for (int i = b0; i < b1; ++i) {  // the thread's own tiles only: count read, base written in place
+            const uint32_t c = s_base[i];
+            s_base[i] = run;
+            run += c;
+        }
+        if (tid == kScanThreads - 1) {
+            s_base[T] = s_wave[kScanThreads / 64 - 1];
+            counters[0] = s_wave[kScanThreads / 64 - 1];
+        }
+        __syncthreads();
+        // empty tiles keep (0,0) as after the reference's memset (rasterizer_impl.cu:310)
+        for (int t = tid; t < T; t += kScanThreads) {
+            const uint32_t b = s_base[t], e = s_base[t + 1];
+            ranges[t] = e > b ? make_uint2(b, e) : make_uint2(0u, 0u);
+            cursor[t] = b;
+        }
+        return;
+    }
     uint32_t keep[kScanKeep];
     uint32_t local = 0;
     if (per <= kScanKeep) {
@@ -401,7 +442,17 @@ __global__ __launch_bounds__(256) void k_tile_sort(int T, const uint2* __restric
 
 void launch_tile_scan(int T, const uint32_t* tile_count, uint2* ranges, uint32_t* cursor, uint32_t* counters,
                       hipStream_t s) {
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, s, T, tile_count, ranges, cursor, counters);
+    if (T <= kScanLdsTiles) {
+        const size_t lds = sizeof(uint32_t) * ((size_t)T + 1);
+        if (lds > 65536)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tile_scan<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_tile_scan<true>, dim3(1), dim3(kScanThreads), lds, s, T, tile_count, ranges, cursor,
+                           counters);
+    } else {
+        hipLaunchKernelGGL(k_tile_scan<false>, dim3(1), dim3(kScanThreads), 0, s, T, tile_count, ranges, cursor,
+                           counters);
+    }
 }
 void launch_scatter_keys(const BinParams& p, hipStream_t s) {
     if (p.P > 0) hipLaunchKernelGGL(k_scatter_keys, dim3((p.P + 255) / 256), dim3(256), 0, s, p);

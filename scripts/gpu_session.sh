@@ -1,7 +1,6 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/w2; export TMPDIR=/tmp
-for g in 0 1 0 1 0 1; do
-GSD_BENCH_PRIME=$g GSD_BENCH_STEP_TIMES=1 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/w2/b.log 2> gpurun_out/w2/s.log || exit 1
-python3 -c "import json; d=json.loads(open('gpurun_out/w2/b.log').read().strip().splitlines()[-1]); print('prime $g', d['value'], d['ms_per_step'])"
-grep "step ms" gpurun_out/w2/s.log | cut -c1-60
-done
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/cs; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py > gpurun_out/cs/t.log 2>&1; rc=$?; tail -1 gpurun_out/cs/t.log; [ $rc -ne 0 ] && exit $rc
+rm -rf gpurun_out/cs/prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cs/prof -o b -- python3 bench.py --steps 30 --warmup 5 --cpu-baseline off > gpurun_out/cs/b.log 2>&1 || exit 1
+grep -o '"gsd::k_tile_scan[^,]*,[0-9]*,[0-9]*,[0-9.]*' gpurun_out/cs/prof/b_kernel_stats.csv
