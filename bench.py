@@ -181,7 +181,7 @@ def main():
 
     # autograd's seed gradient d loss / d loss = 1, allocated once (a bare loss.backward() launches a fill each
     # step; identical semantics)
-    seed = None if os.environ.get("GSD_BENCH_BARE_BACKWARD") else torch.ones((), device=dev)
+    seed = torch.ones((), device=dev)
 
     def step():
         out = render(cam, pc, pipe, bg)
