@@ -1,8 +1,5 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/final4; export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/final4/gpu_tests.log 2>&1; rc=$?
-tail -2 gpurun_out/final4/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/final4/smoke.log 2>&1 || exit 1
-tail -1 gpurun_out/final4/smoke.log
-timeout -k 10 300 python3 bench.py --config 5 --steps 100 --warmup 5 --cpu-baseline off > gpurun_out/final4/b5.log 2>&1 || exit 1
-tail -1 gpurun_out/final4/b5.log | cut -c1-200
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/final6; export TMPDIR=/tmp
+rm -rf gpurun_out/final6/prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final6/prof -o b -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/final6/b.log 2>&1 || exit 1
+tail -1 gpurun_out/final6/b.log | cut -c1-120
