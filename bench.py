@@ -230,7 +230,7 @@ def main():
         step()
     if dens is not None:
         # one densification in the warmup as well: PyTorch loads each elementwise kernel's code object on its
-        # first launch (~0.6 s over densify_and_prune's ops on a fresh process), a one-time cost, not a step's
+        # first launch (~0.1 s over densify_and_prune's ops on a fresh process), a one-time cost, not a step's
         dens.densify_and_prune(0.0002, 0.005, 10.0, None)
     restore()
     torch.cuda.synchronize()

@@ -61,7 +61,13 @@ def main():
     for i in range(a.steps):
         timed(f"step after {i}", step)
     # the first call above includes PyTorch's one-time code-object loads for its elementwise kernels
-    timed("densify_and_prune (2nd)", lambda: dens.densify_and_prune(0.0002, 0.005, 10.0, None))
+    if os.environ.get("PROF_OPS2"):   # torch.profiler over the warm call
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            timed("densify_and_prune (2nd)", lambda: dens.densify_and_prune(0.0002, 0.005, 10.0, None))
+        print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=30))
+    else:
+        timed("densify_and_prune (2nd)", lambda: dens.densify_and_prune(0.0002, 0.005, 10.0, None))
     for i in range(a.steps):
         timed(f"step after 2nd {i}", step)
     print("P", pc._xyz.shape[0])
