@@ -74,8 +74,18 @@ def lib():
         L.orc_cov3d.argtypes = [ctypes.c_int, _f32p, ctypes.c_float, _f32p, _f32p]
         L.orc_mark_visible.restype = None
         L.orc_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
+        L.orc_set_threads.restype = None
+        L.orc_set_threads.argtypes = [ctypes.c_int]
+        L.orc_get_threads.restype = ctypes.c_int
+        L.orc_get_threads.argtypes = []
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """Threads of the oracle's parallel loops (0: OpenMP's default); returns the count in effect."""
+    lib().orc_set_threads(int(n))
+    return int(lib().orc_get_threads())
 
 
 def _f32(a):

@@ -1,7 +1,7 @@
 /*
  * raster_oracle.c -- TEST INFRASTRUCTURE ONLY.
  *
- * A single-threaded, float32 CPU restatement of the reference rasterizer
+ * A float32 CPU restatement of the reference rasterizer
  * (Heng14/gaussian-splatting_deformable, submodules/diff-gaussian-rasterization).
  * It is the checker the parity tests, __graft_entry__.smoke() and bench.py's
  * cpu_baseline leg compare the HIP path against.  Nothing in the product path
@@ -18,14 +18,36 @@
  *
  * Atomic-accumulated gradients (backward render) are summed here in double
  * and rounded once, i.e. the order-free value the float atomics approximate.
+ *
+ * Threads (OpenMP, orc_set_threads): the per-Gaussian loops split over
+ * Gaussians, the render loops over tiles, the instance emission over Gaussians
+ * at their scanned offsets; each result element has one writer, so the
+ * outputs do not depend on the thread count, except the backward render's
+ * double sums, which each thread keeps in its own buffer and which are added
+ * in thread order (differences at the 1e-16 level before the float rounding).
  */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define TILE_X 16 /* config.h:16 BLOCK_X */
 #define TILE_Y 16 /* config.h:17 BLOCK_Y */
+
+/* thread count of every parallel loop below; 0 = OpenMP's default (OMP_NUM_THREADS or all cores) */
+static int g_threads = 0;
+void orc_set_threads(int n) { g_threads = n > 0 ? n : 0; }
+int orc_get_threads(void) {
+#ifdef _OPENMP
+    return g_threads > 0 ? g_threads : omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+#define NT orc_get_threads()
 
 /* auxiliary.h:22-39 */
 static const float C0 = 0.28209479177387814f;
@@ -201,6 +223,7 @@ void orc_preprocess(int P, int D, int M, const float* means3D, const float* scal
     const float fx = (float)W / (2.0f * tanx);
     const int gx = (W + TILE_X - 1) / TILE_X, gy = (H + TILE_Y - 1) / TILE_Y;
     (void)M;
+#pragma omp parallel for schedule(static) num_threads(NT)
     for (int i = 0; i < P; ++i) {
         radii[i] = 0; tiles_touched[i] = 0;
         depths[i] = 0; means2D[2 * i] = means2D[2 * i + 1] = 0;
@@ -274,9 +297,14 @@ int64_t orc_binning(int P, int W, int H, const float* means2D, const float* dept
     if (!keys_out) return K;
     uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (K ? K : 1));
     uint32_t* vals = (uint32_t*)malloc(sizeof(uint32_t) * (K ? K : 1));
-    uint64_t off = 0;
+    /* duplicateWithKeys: Gaussian i writes from offsets[i-1] (rasterizer_impl.cu:84) */
+    uint32_t* starts = (uint32_t*)malloc(sizeof(uint32_t) * (P ? P : 1));
+    acc = 0;
+    for (int i = 0; i < P; ++i) { starts[i] = acc; acc += tiles_touched[i]; }
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(NT)
     for (int i = 0; i < P; ++i) {
         if (!(radii[i] > 0)) continue;
+        uint64_t off = starts[i];
         int rmin[2], rmax[2];
         get_rect(means2D[2 * i], means2D[2 * i + 1], radii[i], gx, gy, rmin, rmax);
         uint32_t dbits;
@@ -289,6 +317,7 @@ int64_t orc_binning(int P, int W, int H, const float* means2D, const float* dept
                 keys[off] = key; vals[off] = (uint32_t)i; ++off;
             }
     }
+    free(starts);
     int end_bit = 32 + (int)orc_higher_msb((uint32_t)(gx * gy));
     uint64_t* k2 = (uint64_t*)malloc(sizeof(uint64_t) * (K ? K : 1));
     uint32_t* v2 = (uint32_t*)malloc(sizeof(uint32_t) * (K ? K : 1));
@@ -327,6 +356,7 @@ void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_
                     const float* features, const float* conic_opacity, const float* bg,
                     float* out_color, float* final_T, uint32_t* n_contrib) {
     const int gx = (W + TILE_X - 1) / TILE_X, gy = (H + TILE_Y - 1) / TILE_Y;
+#pragma omp parallel for collapse(2) schedule(dynamic, 1) num_threads(NT)
     for (int ty = 0; ty < gy; ++ty)
         for (int tx = 0; tx < gx; ++tx) {
             const uint32_t r0 = ranges[2 * (ty * gx + tx)], r1 = ranges[2 * (ty * gx + tx) + 1];
@@ -368,8 +398,18 @@ void orc_render_bwd(int P, int W, int H, const uint32_t* ranges, const uint32_t*
                     const uint32_t* n_contrib, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
                     float* dL_dopacity, float* dL_dcolors) {
     const int gx = (W + TILE_X - 1) / TILE_X, gy = (H + TILE_Y - 1) / TILE_Y;
-    double* acc = (double*)calloc((size_t)P * 9 + 1, sizeof(double)); /* m2x m2y cx cy cw op r g b */
+    const int nt = NT;
+    /* one double accumulator set per thread: m2x m2y cx cy cw op r g b */
+    double* accs = (double*)calloc(((size_t)P * 9 + 1) * nt, sizeof(double));
     const float ddelx_dx = (float)(0.5 * W), ddely_dy = (float)(0.5 * H);
+#pragma omp parallel num_threads(nt)
+    {
+#ifdef _OPENMP
+    double* acc = accs + ((size_t)P * 9 + 1) * omp_get_thread_num();
+#else
+    double* acc = accs;
+#endif
+#pragma omp for collapse(2) schedule(dynamic, 1)
     for (int ty = 0; ty < gy; ++ty)
         for (int tx = 0; tx < gx; ++tx) {
             const uint32_t r0 = ranges[2 * (ty * gx + tx)], r1 = ranges[2 * (ty * gx + tx) + 1];
@@ -423,6 +463,14 @@ void orc_render_bwd(int P, int W, int H, const uint32_t* ranges, const uint32_t*
                     }
                 }
         }
+    }
+    for (int t = 1; t < nt; ++t) {
+        const double* a = accs + ((size_t)P * 9 + 1) * t;
+#pragma omp parallel for schedule(static) num_threads(nt)
+        for (size_t j = 0; j < (size_t)P * 9; ++j) accs[j] += a[j];
+    }
+    const double* acc = accs;
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int g = 0; g < P; ++g) {
         const double* a = acc + 9 * (size_t)g;
         dL_dmean2D[3 * g + 0] = (float)a[0]; dL_dmean2D[3 * g + 1] = (float)a[1]; dL_dmean2D[3 * g + 2] = 0.0f;
@@ -431,7 +479,7 @@ void orc_render_bwd(int P, int W, int H, const uint32_t* ranges, const uint32_t*
         dL_dopacity[g] = (float)a[5];
         for (int ch = 0; ch < 3; ++ch) dL_dcolors[3 * g + ch] = (float)a[6 + ch];
     }
-    free(acc);
+    free(accs);
 }
 
 /* backward.cu:144-274 computeCov2DCUDA -- dL_dmeans is ASSIGNED (backward.cu:273) */
@@ -612,6 +660,7 @@ void orc_preprocess_bwd(int P, int D, int M, const float* means3D, const int* ra
                         const float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh,
                         float* dL_dscale, float* dL_drot) {
     const float fy = (float)H / (2.0f * tany), fx = (float)W / (2.0f * tanx);
+#pragma omp parallel for schedule(static) num_threads(NT)
     for (int i = 0; i < P; ++i) {
         if (!(radii[i] > 0)) continue;
         const float* m = means3D + 3 * i;

@@ -1,13 +1,19 @@
-"""BASELINE.json configurations 2, 3 and 5 at their full sizes.
+"""BASELINE.json configurations 1-5 at their full sizes.
 
+- cfg 1 (10k Gaussians, SH0, 400x400, identity SE(3)): the zero twist through the fused SE(3) kernel (exactly
+  the identity on the means) into the rasterizer, against the C oracle, and d_twist through the whole chain
+  against the oracle chain (C rasterizer backward -> float64 autograd of se3_ref).
+- cfg 4 (1M, SH3, 1920x1080: the bench workload) and cfg 5 (2M, SH3, 3840x2160): the whole view against the
+  OpenMP C oracle -- num_rendered, radii, ranges, point_list and the per-Gaussian state bit-exact, image and
+  final_T within 1e-5, n_contrib within 0.1 %, all eight gradients within rel L2 1e-4.
 - cfg 2 (100k Gaussians, SH2, 800x800, static): the whole view against the C oracle -- binning and
   per-Gaussian state bit-exact, image / gradients within the bars of test_gpu_parity.py.
 - cfg 3 (500k, SH3, 1920x1080, per-Gaussian SE(3) + d_se3): the fused SE(3) kernel against the float64
   restatement of rigid_body.exp_se3 (oracle/se3_ref.py); the rasterizer on the moved Gaussians against the C
   oracle (bit-exact binning); d_twist through the whole chain (HIP rasterizer backward -> HIP SE(3) backward)
   against the oracle chain (C rasterizer backward -> float64 autograd of se3_ref).
-- cfg 5 (2M, SH3, 3840x2160, densification active): too large for the single-threaded oracle in a test, so
-  size-independent properties of the forward (ranges partition [0, K), (tile, depth, id) order, every visible
+- cfg 5 (2M, SH3, 3840x2160, densification active): besides the oracle check above, size-independent
+  properties of the forward (ranges partition [0, K), (tile, depth, id) order, every visible
   Gaussian binned, n_contrib <= range length, final_T in [1e-4, 1]), then a full training view through render()
   + loss + backward + the fused densification statistics + densify_and_prune on the FusedAdam slabs, whose
   point count must be exactly P + clones + 2 splits - split parents, followed by another view.
@@ -21,7 +27,7 @@ import pytest
 import torch
 
 from conftest import scene_inputs
-from test_gpu_parity import check_forward, gpu_backward, gpu_forward, oracle_fwd_bwd, rel_l2
+from test_gpu_parity import check_forward, check_forward_against, gpu_backward, gpu_forward, oracle_fwd_bwd, rel_l2
 
 pytestmark = pytest.mark.gpu
 
@@ -70,6 +76,74 @@ def test_config2_full_view_matches_oracle(oracle_mod):
         got = gt.cpu().numpy().reshape(ob[name].shape)
         assert np.isfinite(got).all(), name
         assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+
+
+def full_view_matches_oracle(oracle_mod, P, W, H, deg, seed):
+    """One whole view at a BASELINE configuration's size: forward (check_forward: bit-exact binning and
+    per-Gaussian state, image / final_T / n_contrib bars) and all eight gradients against the C oracle."""
+    d = scene_inputs(P, W, H, deg, seed=seed, device=DEV)
+    dpix = torch.randn(3, H, W, generator=torch.Generator().manual_seed(seed)).mul_(1e-3).to(DEV)
+    o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    fwd = gpu_forward(d)
+    K = check_forward_against(o, d, fwd)
+    assert K == o["num_rendered"] > P
+    grads = gpu_backward(d, fwd, dpix)
+    for name, gt in zip(GRAD_NAMES, grads):
+        got = gt.cpu().numpy().reshape(ob[name].shape)
+        assert np.isfinite(got).all(), name
+        assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+    return d, fwd
+
+
+def test_config4_full_view_matches_oracle(oracle_mod):
+    """BASELINE configuration 4, the bench workload: 1M Gaussians, SH3, 1920x1080, seed 4."""
+    d, fwd = full_view_matches_oracle(oracle_mod, 1_000_000, 1920, 1080, 3, seed=4)
+    check_invariants(1_000_000, 1920, 1080, fwd)
+
+
+def test_config5_full_view_matches_oracle(oracle_mod):
+    """BASELINE configuration 5's view: 2M Gaussians, SH3, 3840x2160 (K ~ 6.5M instances, 32400 tiles)."""
+    d, fwd = full_view_matches_oracle(oracle_mod, 2_000_000, 3840, 2160, 3, seed=5)
+    del d, fwd
+    torch.cuda.empty_cache()
+
+
+def test_config1_identity_se3_chain_matches_oracle(oracle_mod):
+    """BASELINE configuration 1: 10k Gaussians, SH0, 400x400, identity SE(3).  The zero twist through the fused
+    SE(3) kernel leaves the means bit-identical (the guarded series, not the reference's NaN at theta = 0,
+    SURVEY.md 0.5); the rasterizer on its output matches the oracle; d_twist / d_means / d_rot through the HIP
+    chain match float64 autograd of se3_ref fed with the oracle's rasterizer gradients."""
+    from gsd_amd import _C
+    from gsd_amd.scene import make_gaussians
+    from oracle import se3_ref
+    P, W, H, deg = 10_000, 400, 400, 0
+    g = make_gaussians(P, W, H, seed=1, se3="identity")
+    assert float(g.twist.abs().max()) == 0.0
+    d = scene_inputs(P, W, H, deg, seed=1, device=DEV)
+    twist = g.twist.to(DEV)
+    means0, rots0 = d["means3D"], d["rotations"]
+    m, q = _C.se3_deform_forward(twist, means0, rots0)
+    assert torch.equal(m, means0)
+    tw64, x64, q64 = (t.detach().cpu().double().requires_grad_(True) for t in (twist, means0, rots0))
+    m_ref, q_ref = se3_ref.deform(tw64, x64, q64)
+    assert torch.isfinite(m_ref).all() and torch.isfinite(q_ref).all()
+    assert rel_l2(q.cpu(), q_ref.detach()) <= 1e-6
+    d["means3D"], d["rotations"] = m.contiguous(), q.contiguous()
+    o, fwd = check_forward(oracle_mod, d)
+    dpix = torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)).mul_(1e-3).to(DEV)
+    _, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    grads = dict(zip(GRAD_NAMES, gpu_backward(d, fwd, dpix)))
+    for name in GRAD_NAMES:
+        got = grads[name].cpu().numpy().reshape(ob[name].shape)
+        assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+    d_tw, d_m, d_q = _C.se3_deform_backward(twist, means0, rots0, grads["dL_dmeans3D"].reshape(P, 3).contiguous(),
+                                            grads["dL_drotations"].reshape(P, 4).contiguous())
+    up_m = torch.from_numpy(ob["dL_dmeans3D"].reshape(P, 3)).double()
+    up_q = torch.from_numpy(ob["dL_drotations"].reshape(P, 4)).double()
+    ((m_ref * up_m).sum() + (q_ref * up_q).sum()).backward()
+    for got, want, name in ((d_tw, tw64.grad, "d_twist"), (d_m, x64.grad, "d_means"), (d_q, q64.grad, "d_rot")):
+        assert torch.isfinite(got).all(), name
+        assert rel_l2(got.cpu(), want) <= 1e-4, (name, rel_l2(got.cpu(), want))
 
 
 def test_config3_se3_full_view_matches_oracle_chain(oracle_mod):

@@ -77,9 +77,15 @@ def oracle_fwd_bwd(oracle_mod, d, dpix=None, *, colors=None, cov3D=None, scale_m
 
 
 def check_forward(oracle_mod, d, **mode):
-    from gsd_amd.introspect import decode
     o, _ = oracle_fwd_bwd(oracle_mod, d, **mode)
     fwd = gpu_forward(d, **mode)
+    check_forward_against(o, d, fwd, colors=mode.get("colors"))
+    return o, fwd
+
+
+def check_forward_against(o, d, fwd, colors=None):
+    """The forward's bars against an oracle forward `o` of the same inputs; returns num_rendered."""
+    from gsd_amd.introspect import decode
     K, color, radii, geom, binning, img = fwd
     torch.cuda.synchronize()
     st = {k: v.cpu().numpy() for k, v in decode(d["means3D"].shape[0], d["W"], d["H"], K, geom, binning, img).items()}
@@ -90,7 +96,7 @@ def check_forward(oracle_mod, d, **mode):
     np.testing.assert_array_equal(st["depths"][vis].view(np.uint32), o["depths"][vis].view(np.uint32))
     np.testing.assert_array_equal(st["means2D"][vis].view(np.uint32), o["means2D"][vis].view(np.uint32))
     np.testing.assert_array_equal(st["conic_opacity"][vis].view(np.uint32), o["conic_opacity"][vis].view(np.uint32))
-    if mode.get("colors") is None:
+    if colors is None:
         np.testing.assert_array_equal(st["rgb"][vis].view(np.uint32), o["rgb"][vis].view(np.uint32))
         cl = np.stack([(st["clamped"] >> c) & 1 for c in range(3)], 1).astype(bool)
         np.testing.assert_array_equal(cl[vis], o["clamped"][vis].astype(bool))
@@ -102,7 +108,7 @@ def check_forward(oracle_mod, d, **mode):
     nc_mismatch = np.mean(st["n_contrib"].astype(np.uint32) != o["n_contrib"])
     assert nc_mismatch <= 1e-3, nc_mismatch
     assert np.abs(st["final_T"] - o["final_T"]).max() <= 1e-5
-    return o, fwd
+    return K
 
 
 CASES = [  # (P, W, H, deg, seed): config-1 shape, odd sizes, every SH degree
@@ -133,6 +139,37 @@ def test_backward_matches_oracle(oracle_mod, P, W, H, deg, seed):
         got = gt.cpu().numpy().reshape(ob[name].shape)
         assert np.isfinite(got).all(), name
         assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+
+
+def test_backward_low_opacity(oracle_mod):
+    """Opacity logits down to -9 (o ~ 1.2e-4, far below the 1/255 alpha floor) and up to +4: every gradient,
+    dL/dopacity included, within rel L2 1e-4 of the oracle's sum of G * dL/dalpha (backward.cu:552), and
+    per Gaussian within 1e-3 relative (+ 1e-3 of the largest) where the oracle's dL/dopacity is non-zero --
+    the kernel recovers dL/dopacity from its sum of o * G * dL/dalpha, which must not lose the small
+    opacities.  Gaussians that never reach alpha >= 1/255 get exactly zero."""
+    P, W, H, deg = 8_000, 320, 240, 3
+    d = scene_inputs(P, W, H, deg, seed=21, device=DEV)
+    logit = torch.empty(P).uniform_(-9.0, 4.0, generator=torch.Generator().manual_seed(21))
+    d["opacities"] = torch.sigmoid(logit)[:, None].contiguous().to(DEV)
+    d["scales"] = d["scales"] * 2.0     # larger footprints: more low-opacity Gaussians cross the alpha floor
+    dpix = torch.randn(3, H, W, generator=torch.Generator().manual_seed(22)).mul_(1e-3).to(DEV)
+    o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    fwd = gpu_forward(d)
+    check_forward_against(o, d, fwd)
+    grads = gpu_backward(d, fwd, dpix)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for name, gt in zip(names, grads):
+        got = gt.cpu().numpy().reshape(ob[name].shape)
+        assert np.isfinite(got).all(), name
+        assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+    got = grads[2].cpu().numpy().reshape(-1).astype(np.float64)
+    want = ob["dL_dopacity"].reshape(-1).astype(np.float64)
+    op = d["opacities"].cpu().numpy().reshape(-1)
+    low = (op < 0.02) & (want != 0)
+    assert low.sum() > 20, low.sum()          # the case is exercised
+    assert np.all(np.abs(got - want) <= 1e-3 * np.abs(want) + 1e-3 * np.abs(want).max())
+    assert np.all(got[op < 1.0 / 255.0] == 0.0)
 
 
 def test_backward_run_to_run_noise():
