@@ -16,11 +16,18 @@ processed by all ranks / max-over-ranks wall time of the K timed steps.
 Also reported (rank 0): fwd+bwd ms/view (hipEvents, median over >= 100 views,
 SURVEY.md 8(d)); per-kernel device times (hipEvents around each launch inside
 the C-ABI, from a separate pass so they do not perturb the timed steps); the
-roofline of the dominant kernel; and the CPU baseline -- the single-threaded C
-oracle on one full view of the same workload.
+roofline of the dominant kernel -- its binding roof from the committed PMC pass
+of the same workload (VALU issue for the render kernels, HBM otherwise; traffic
+null when no PMC pass of that workload exists); and the CPU baseline -- the
+OpenMP C oracle on the host's cores, full views of the same workload for ~10 s.
 
   python bench.py [--gpus N --steps K --warmup W --config 4 --cpu-baseline auto|off]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+``--gpus N`` means N ranks: without a launcher (no WORLD_SIZE in the environment) and N > 1, this process
+starts ``torch.distributed.run`` with N ranks on this node and exits with its status, before anything touches
+the GPU.  Under a launcher, WORLD_SIZE must equal N; fewer visible devices than ranks is refused unless
+GSD_DIST_BACKEND=gloo (the one-GPU rehearsal).
 """
 from __future__ import annotations
 
@@ -29,6 +36,8 @@ import gc
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,6 +51,9 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "training views/sec + fwd+bwd ms/view, 1M Gaussians @1080p SH3, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU issue roof: 256 CUs x 4 SIMDs, a wave64 v_fma_f32 every 2 cycles per SIMD with more than one wave resident
+# (MI355X_MICROARCH.md), at the 2.4 GHz peak engine clock -> 1228.8 G wave-instructions/s
+VALU_PEAK_GINST = 1024 * 0.5 * 2.4
 
 
 def algorithmic_bytes(P, V, K, W, H, C):
@@ -64,20 +76,53 @@ def algorithmic_bytes(P, V, K, W, H, C):
     }
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*/pmc_traffic.json,
-    written by scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes), or None."""
+def pmc_traffic(kernel, workload):
+    """HBM bytes (and the VALU issue figures) per launch of ``kernel`` from the newest committed PMC summary of
+    the same workload (profiles/**/pmc_traffic.json whose "_workload" is ``workload``, e.g. "cfg4"; written by
+    scripts/pmc_traffic.py from rocprofv3 FETCH_SIZE / WRITE_SIZE / SQ_* passes over that configuration), or None
+    -- a summary of another workload or without a workload tag is never used."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True))
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if kernel in d:
-            return {"hbm_bytes": d[kernel]["hbm_bytes"], "valu": d[kernel].get("valu"),
+        if d.get("_workload") == workload and kernel in d:
+            return {"hbm_bytes": d[kernel].get("hbm_bytes"), "valu": d[kernel].get("valu"),
                     "source": os.path.relpath(f, ROOT)}
     return None
+
+
+def roofline(kernel, ms, nbytes, workload):
+    """The dominant kernel against its binding roof.  HBM: algorithmic bytes / the live average launch time vs
+    8 TB/s.  VALU issue (when a PMC pass of this workload counted the kernel's instructions): the counted wave64
+    VALU instructions per launch / the live launch time vs VALU_PEAK_GINST.  ``bound`` is whichever of the two
+    the kernel is closer to; the other stays in the block as a secondary figure."""
+    ach = nbytes / (ms * 1e-3) / 1e9
+    hbm = {"achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4)}
+    roof = {"kernel": kernel, "bound": "hbm", **hbm, "traffic": None, "algorithmic_bytes": int(nbytes),
+            "avg_launch_ms": round(ms, 4), "workload": workload}
+    tr = pmc_traffic(kernel, workload)
+    if tr is None:
+        return roof
+    roof["traffic"] = tr["hbm_bytes"]
+    roof["traffic_source"] = tr["source"]
+    v = tr.get("valu")
+    if v and v.get("instructions"):
+        rate = v["instructions"] / (ms * 1e-3) / 1e9
+        valu = {"achieved": round(rate, 2), "peak": VALU_PEAK_GINST, "unit": "G wave64-VALU-instr/s",
+                "frac": round(rate / VALU_PEAK_GINST, 4), "instructions_per_launch": int(v["instructions"]),
+                "pmc_issue_per_simd_cycle": v.get("issue_per_simd_cycle"),
+                "pmc_lds_issue_wait_frac": v.get("lds_issue_wait_frac")}
+        if valu["frac"] > hbm["frac"]:
+            roof.update(bound="valu", achieved=valu["achieved"], peak=valu["peak"], unit=valu["unit"],
+                        frac=valu["frac"])
+            roof["valu"] = valu
+            roof["hbm"] = hbm
+        else:
+            roof["valu"] = valu
+    return roof
 
 
 FUSED_STEP = os.environ.get("GSD_FUSED_STEP", "1") != "0"
@@ -102,8 +147,28 @@ def make_optimizer(pc):
     return FusedAdam(groups, lr=0.0, eps=1e-15)
 
 
-def cpu_baseline(cfg, seed):
-    """Single-threaded C oracle (oracle/raster_oracle.c), one full view fwd+bwd of the same workload."""
+def host_cpu():
+    """CPU model name and the CPUs this process may run on (lscpu's "Model name" and the affinity mask)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, avail
+
+
+def cpu_baseline(cfg, seed, min_seconds=10.0, max_views=64):
+    """The C oracle (oracle/raster_oracle.c) on the host cores: OpenMP over Gaussians and tiles with OpenMP's
+    default thread count (OMP_NUM_THREADS: 16 on the GPU box, this process's CPU share there), full views
+    forward + backward of the same workload repeated until ~``min_seconds`` have passed."""
     import numpy as np
 
     from gsd_amd.camera import synthetic_camera
@@ -121,13 +186,51 @@ def cpu_baseline(cfg, seed):
     opac = torch.sigmoid(g.opacity).numpy()
     dpix = np.random.default_rng(0).standard_normal((3, H, W)).astype(np.float32) * 1e-3
     oracle.build()
+    threads = oracle.set_threads(0)
+    model, avail = host_cpu()
+    xyz = g.xyz.numpy()
+    n = 0
     t0 = time.perf_counter()
-    fwd = oracle.forward(g.xyz.numpy(), opac, **kw)
-    oracle.backward(fwd, dpix, g.xyz.numpy(), **kw)
-    dt = time.perf_counter() - t0
-    return {"value": 1.0 / dt, "unit": "views/s", "cores": 1, "kind": "port",
-            "sample": f"1 full view of the bench workload (P={P}, {W}x{H}, SH{D}) forward+backward with the "
-                      f"single-threaded C oracle: {dt:.1f} s"}
+    while True:
+        fwd = oracle.forward(xyz, opac, **kw)
+        oracle.backward(fwd, dpix, xyz, **kw)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds or n >= max_views:
+            break
+    return {"value": n / dt, "unit": "views/s", "cores": threads, "kind": "port",
+            "host": {"model": model, "cpus_available": avail, "omp_threads": threads},
+            "sample": f"{n} full views of the bench workload (P={P}, {W}x{H}, SH{D}) forward+backward with the "
+                      f"OpenMP C oracle on {threads} threads ({model}): {dt:.1f} s"}
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launcher_argv(n, argv, port):
+    """The torch.distributed.run command that runs this script as ``n`` ranks on this node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def check_ranks(gpus, env=None):
+    """Refusals of --gpus N (before anything touches the GPU): returns an error message or None.
+    Under a launcher WORLD_SIZE must be N; N ranks need N visible devices unless GSD_DIST_BACKEND=gloo (several
+    ranks on one GPU, the rehearsal of the data-parallel path)."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        return f"--gpus must be >= 1, got {gpus}"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and int(ws) != gpus:
+        return f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks"
+    if gpus > 1 and env.get("GSD_DIST_BACKEND") != "gloo":
+        ndev = torch.cuda.device_count()   # counts devices without initialising HIP in this process
+        if ndev < gpus:
+            return f"--gpus {gpus} needs {gpus} visible GPUs, found {ndev} (GSD_DIST_BACKEND=gloo rehearses on fewer)"
+    return None
 
 
 def main():
@@ -140,8 +243,15 @@ def main():
     ap.add_argument("--densify-interval", type=int, default=None,
                     help="densify_and_prune every N steps (train.py:610-648); default 100 for config 5, else off")
     args = ap.parse_args()
+    err = check_ranks(args.gpus)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # N ranks on this node: a child launcher, started before this process initialises the GPU
+        sys.exit(subprocess.call(launcher_argv(args.gpus, sys.argv[1:], free_port())))
 
-    from gsd_amd import DeformableGaussians, default_pipe, l1_ssim_loss, render
+    from gsd_amd import DeformableGaussians, default_pipe, render, training_loss
     from gsd_amd import _C as gsdC
     from gsd_amd._native import kernel_times
     from gsd_amd.camera import synthetic_camera
@@ -185,7 +295,9 @@ def main():
 
     def step():
         out = render(cam, pc, pipe, bg)
-        loss = l1_ssim_loss(out["render"], target, 0.2)   # train.py:529, lambda_dssim = 0.2
+        # train.py:323-332 + :529, lambda_dssim = 0.2: the offset-norm term is 0 (and skipped) when nothing moves
+        # the means (configurations 2, 4, 5); in the SE(3) mode (1, 3) it is the moved distance's mean norm
+        loss = training_loss(out["render"], target, out["means3D_offset"], 0.2)
         if FUSED_STEP:
             # backward + Adam: at N = 1 every gradient is final inside the preprocess backward, which applies
             # the Adam step there (FusedAdam.step_in_backward, gsd_adam_epilogue); with N > 1 the gradients
@@ -215,7 +327,7 @@ def main():
     def restore():
         with torch.no_grad():
             if dens is not None and pc._xyz.shape[0] != snapshot[0].shape[0]:   # densified: the initial P back
-                init = dict(zip(("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"), snapshot[:6]))
+                init = dict(zip(dens._names(), snapshot))
                 dens._apply(lambda n, d, m, v: (init[n].clone(), torch.zeros_like(init[n]), torch.zeros_like(init[n])))
             for p, s0 in zip(pc.parameters(), snapshot):
                 p.copy_(s0)
@@ -285,7 +397,7 @@ def main():
                 torch.cuda._sleep(2_000_000)
             e0.record()
             o = render(cam, pc, pipe, bg)
-            l1_ssim_loss(o["render"], target, 0.2).backward(seed)
+            training_loss(o["render"], target, o["means3D_offset"], 0.2).backward(seed)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
@@ -349,20 +461,12 @@ def main():
         dom = max(kt, key=lambda k: kt[k][0]) if kt else None
         roof = None
         if dom:
-            nbytes = algorithmic_bytes(P, V, K, W, H, (min(D, 3) + 1) ** 2).get(dom)
+            # the kernel-timing pass's scene: V and K of its last view, P of that view (no densification in it)
+            nbytes = algorithmic_bytes(int(pc._xyz.shape[0]), V, K, W, H, (min(D, 3) + 1) ** 2).get(dom)
             if nbytes:
-                ach = nbytes / (per_kernel[dom] * 1e-3) / 1e9
-                roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                        "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(per_kernel[dom], 4)}
-                tr = pmc_traffic(dom)
-                if tr is not None:
-                    roof["traffic"] = tr["hbm_bytes"]
-                    roof["traffic_source"] = tr["source"]
-                    if tr.get("valu"):   # the bound that applies to the render kernels: VALU issue
-                        roof["valu"] = tr["valu"]
+                roof = roofline(dom, per_kernel[dom], nbytes, f"cfg{args.config}")
         cpu = None
-        if args.cpu_baseline == "auto" and world == 1 and args.config <= 4:   # a bounded CPU sample
+        if args.cpu_baseline == "auto" and world == 1:   # rank 0 at N = 1 only; a bounded CPU sample
             cpu = cpu_baseline(cfg, args.config)
         res = {
             "metric": METRIC,

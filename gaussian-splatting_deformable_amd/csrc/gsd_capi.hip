@@ -255,12 +255,13 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
                 kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kMlp, kMlpBwd,
-                kNumKernels };
+                kOffNorm, kOffNormBwd, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
                                                "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "sh_grad_views", "adam",         "densify_stats",
-                                               "knn",            "deform_mlp",   "deform_mlp_relu_bias"};
+                                               "knn",            "deform_mlp",   "deform_mlp_relu_bias",
+                                               "offset_norm",    "offset_norm_bwd"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -786,6 +787,32 @@ int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, cons
     timed(kLossBwd, s, [&] {
         gsd::launch_l1_ssim_bwd(C, H, W, w, lambda_dssim, img, gt, ws.gmaps, grad_out, sign, dL_dimg, s);
     });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+size_t gsd_offset_norm_workspace_bytes(int64_t P) {
+    return P > 0 ? (size_t)gsd::offnorm_blocks(P) * sizeof(float) : sizeof(float);
+}
+
+int gsd_offset_norm(int64_t P, const float* offset, float scale, float* out, void* workspace, void* stream) {
+    if (P <= 0) return fail(GSD_ERR_ARG, "offset_norm: need P > 0 (the mean of no rows is undefined)");
+    if (P >= (1ll << 40)) return fail(GSD_ERR_ARG, "P too large");
+    if (!offset || !out || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
+    hipStream_t s = as_stream(stream);
+    timed(kOffNorm, s, [&] { gsd::launch_offset_norm(P, offset, scale, static_cast<float*>(workspace), out, s); });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int gsd_offset_norm_backward(int64_t P, const float* offset, const float* grad_out, float scale, float* d_offset,
+                             void* stream) {
+    if (P < 0) return fail(GSD_ERR_ARG, "invalid P");
+    if (P == 0) return GSD_OK;
+    if (P >= (1ll << 40)) return fail(GSD_ERR_ARG, "P too large");
+    if (!offset || !d_offset) return fail(GSD_ERR_ARG, "null pointer argument");
+    hipStream_t s = as_stream(stream);
+    timed(kOffNormBwd, s, [&] { gsd::launch_offset_norm_bwd(P, offset, grad_out, scale, d_offset, s); });
     GSD_CHECK(false, s);
     return GSD_OK;
 }

@@ -322,6 +322,10 @@ void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const f
                     float* gmaps, float* partial, float* out3, float* dimg, hipStream_t s);
 void launch_l1_ssim_bwd(int C, int H, int W, const float* w11, float lambda, const float* img, const float* gt,
                         const float* gmaps, const float* gscale, float sign, float* dimg, hipStream_t s);
+int offnorm_blocks(long long P);
+void launch_offset_norm(long long P, const float* off, float scale, float* partial, float* out, hipStream_t s);
+void launch_offset_norm_bwd(long long P, const float* off, const float* gscale, float scale, float* d_off,
+                            hipStream_t s);
 
 constexpr int kHistThreads = 512;       // LDS-histogram binning workgroup
 constexpr int kHistMaxTiles = 40960;    // 160 KiB of u32 bins; larger grids use global-atomic binning

@@ -363,4 +363,74 @@ void launch_l1_ssim_bwd(int C, int H, int W, const float* w11, float lambda, con
     hipLaunchKernelGGL(k_ssim_bwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, gscale, sign, dimg);
 }
 
+// ---- offset-norm regulariser (train.py:329-332): R = mean_g ||off_g||, the per-Gaussian 3-D offsets of the
+// deformation.  Forward: per-workgroup partial sums of the row norms, then one workgroup sums them in a fixed order
+// (deterministic, no float atomics).  Backward: dR/doff_g = g * scale * off_g / ||off_g||, zero where the norm is
+// zero (torch's norm backward masks the division there).  HBM: 12 B per row read, 12 B written backward.
+constexpr int kOffThreads = 256;
+constexpr int kOffMaxBlocks = 1024;
+
+int offnorm_blocks(long long P) {
+    const long long b = (P + kOffThreads * 4 - 1) / (kOffThreads * 4);
+    return (int)(b < 1 ? 1 : (b > kOffMaxBlocks ? kOffMaxBlocks : b));
+}
+
+__device__ __forceinline__ float row_norm(const float* __restrict__ off, long long g) {
+    const float x = off[3 * g], y = off[3 * g + 1], z = off[3 * g + 2];
+    return sqrtf(x * x + y * y + z * z);
+}
+
+__global__ __launch_bounds__(kOffThreads) void k_offnorm_partial(long long P, const float* __restrict__ off,
+                                                                 float* __restrict__ partial) {
+    __shared__ float red[kOffThreads / 64];
+    float acc = 0.f;
+    for (long long g = (long long)blockIdx.x * kOffThreads + threadIdx.x; g < P; g += (long long)gridDim.x * kOffThreads)
+        acc += row_norm(off, g);
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(kOffMaxBlocks) void k_offnorm_final(int nblk, const float* __restrict__ partial,
+                                                                 float scale, float* __restrict__ out) {
+    __shared__ float red[kOffMaxBlocks / 64];
+    float v = threadIdx.x < (unsigned)nblk ? partial[threadIdx.x] : 0.f;
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kOffMaxBlocks / 64; ++w) t += red[w];
+        out[0] = t * scale;
+    }
+}
+
+__global__ __launch_bounds__(kOffThreads) void k_offnorm_bwd(long long P, const float* __restrict__ off,
+                                                             const float* __restrict__ gscale, float scale,
+                                                             float* __restrict__ d_off) {
+    const long long g = (long long)blockIdx.x * kOffThreads + threadIdx.x;
+    if (g >= P) return;
+    const float c = (gscale ? gscale[0] : 1.f) * scale;
+    const float x = off[3 * g], y = off[3 * g + 1], z = off[3 * g + 2];
+    const float n = sqrtf(x * x + y * y + z * z);
+    const float k = n > 0.f ? c / n : 0.f;
+    d_off[3 * g] = x * k;
+    d_off[3 * g + 1] = y * k;
+    d_off[3 * g + 2] = z * k;
+}
+
+void launch_offset_norm(long long P, const float* off, float scale, float* partial, float* out, hipStream_t s) {
+    const int nb = offnorm_blocks(P);
+    hipLaunchKernelGGL(k_offnorm_partial, dim3(nb), dim3(kOffThreads), 0, s, P, off, partial);
+    hipLaunchKernelGGL(k_offnorm_final, dim3(1), dim3(kOffMaxBlocks), 0, s, nb, (const float*)partial, scale, out);
+}
+
+void launch_offset_norm_bwd(long long P, const float* off, const float* gscale, float scale, float* d_off,
+                            hipStream_t s) {
+    const long long nb = (P + kOffThreads - 1) / kOffThreads;
+    hipLaunchKernelGGL(k_offnorm_bwd, dim3((unsigned)nb), dim3(kOffThreads), 0, s, P, off, gscale, scale, d_off);
+}
+
 }  // namespace gsd

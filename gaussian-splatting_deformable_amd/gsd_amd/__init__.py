@@ -10,8 +10,9 @@ reference: ``GaussianRasterizationSettings``, ``GaussianRasterizer``,
 from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer, rasterize_gaussians  # noqa: F401
 from .deform import se3_deform  # noqa: F401
 from .renderer import render, DeformableGaussians, default_pipe  # noqa: F401
-from .loss import l1_ssim_loss, l1_loss, ssim  # noqa: F401
+from .loss import l1_ssim_loss, l1_loss, ssim, offset_norm, training_loss  # noqa: F401
 from . import _C, _native, camera, scene, parallel  # noqa: F401
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "se3_deform", "render",
-           "DeformableGaussians", "default_pipe", "l1_ssim_loss", "l1_loss", "ssim"]
+           "DeformableGaussians", "default_pipe", "l1_ssim_loss", "l1_loss", "ssim",
+           "offset_norm", "training_loss"]

@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -87,6 +87,9 @@ SIGNATURES = {
     "gsd_l1_ssim_workspace_bytes": (_sz, [_i32, _i32, _i32]),
     "gsd_l1_ssim": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
     "gsd_l1_ssim_backward": (_i32, [_i32, _i32, _i32, _vp, _vp, _f32, _vp, _f32, _vp, _vp, _vp]),
+    "gsd_offset_norm_workspace_bytes": (_sz, [_i64]),
+    "gsd_offset_norm": (_i32, [_i64, _vp, _f32, _vp, _vp, _vp]),
+    "gsd_offset_norm_backward": (_i32, [_i64, _vp, _vp, _f32, _vp, _vp]),
     "gsd_adam_step": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32),
                              ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32, _vp]),
     "gsd_adam_step_ex": (_i32, [_i64, _vp, _vp, _vp, _vp, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_f32),
@@ -111,7 +114,7 @@ def kernel_times(enable: bool | None = None, reset: bool = False) -> dict:
     Synchronises on the last timed launch.  enable=True/False switches recording."""
     lib = load()
     out = {}
-    n_max = 16
+    n_max = 32
     names = ctypes.create_string_buffer(32 * n_max)
     tot = (ctypes.c_double * n_max)()
     cnt = (_i64 * n_max)()

@@ -11,6 +11,9 @@ trained by ``gsd_amd.optim.FusedAdam``:
   semantics: new points get zero moments, pruned points drop theirs, a replaced tensor gets zero moments.
   They run every ``densification_interval`` (100) views, so they stay torch ops on the GPU; the flat
   parameter / moment / gradient slabs are rebuilt once per call (``FusedAdam.rebuild``).
+- A per-Gaussian SE(3) twist (``DeformableGaussians._twist``, the SE(3) mode's trained parameter) is a
+  per-Gaussian attribute like the rotation: clones and split children inherit their parent's twist with zero
+  moments, pruned points drop it (the reference has no per-Gaussian twist -- its twists come from the network).
 - Data parallel (one view per rank, replicated Gaussians): every rank accumulates the statistics of its own
   views; ``densify_and_prune`` first combines them across ranks (``sync_stats``: sums of the counts and
   gradient norms, max of the radii -- what one process accumulating every view holds), and the split's normal
@@ -69,13 +72,17 @@ class GaussianDensifier:
     # ---- optimizer-state surgery ----
     def _params(self):
         pc = self.pc
-        return [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+        ps = [pc._xyz, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation]
+        return ps + ([pc._twist] if getattr(pc, "_twist", None) is not None else [])
+
+    def _names(self):
+        return _NAMES + (("twist",) if getattr(self.pc, "_twist", None) is not None else ())
 
     def _apply(self, fn):
         """fn(name, data, exp_avg, exp_avg_sq) -> (data, exp_avg, exp_avg_sq) for every Gaussian attribute;
         any other optimizer parameter (e.g. a twist or an offset network) must not change shape."""
         datas, ms, vs = [], [], []
-        gauss = {id(p): n for p, n in zip(self._params(), _NAMES)}
+        gauss = {id(p): n for p, n in zip(self._params(), self._names())}
         for g in self.opt.param_groups:
             for p in g["params"]:
                 m, v = self.opt.moments(p)
@@ -110,6 +117,8 @@ class GaussianDensifier:
         sel = torch.logical_and(sel, torch.max(pc.get_scaling, dim=1).values <= self.percent_dense * scene_extent)
         new = {"xyz": pc._xyz[sel], "f_dc": pc._features_dc[sel], "f_rest": pc._features_rest[sel],
                "opacity": pc._opacity[sel], "scaling": pc._scaling[sel], "rotation": pc._rotation[sel]}
+        if "twist" in self._names():
+            new["twist"] = pc._twist[sel]
         self.densification_postfix({k: v.detach() for k, v in new.items()})
 
     def densify_and_split(self, grads, grad_threshold, scene_extent, N=2):
@@ -128,6 +137,8 @@ class GaussianDensifier:
                    "scaling": torch.log(pc.get_scaling[sel].repeat(N, 1) / (0.8 * N)),
                    "rotation": pc._rotation[sel].repeat(N, 1), "f_dc": pc._features_dc[sel].repeat(N, 1, 1),
                    "f_rest": pc._features_rest[sel].repeat(N, 1, 1), "opacity": pc._opacity[sel].repeat(N, 1)}
+            if "twist" in self._names():
+                new["twist"] = pc._twist[sel].repeat(N, 1)
         self.densification_postfix(new)
         prune = torch.cat((sel, torch.zeros(N * int(sel.sum()), device=sel.device, dtype=torch.bool)))
         self.prune_points(prune)
@@ -160,7 +171,7 @@ class GaussianDensifier:
             stds = scal_s.repeat(N, 1)
             samples = broadcast_(torch.normal(mean=torch.zeros((stds.size(0), 3), device=stds.device), std=stds))
             rots = build_rotation(pc._rotation.index_select(0, split_i)).repeat(N, 1, 1)
-            src = dict(zip(_NAMES, (p.detach() for p in self._params())))
+            src = dict(zip(self._names(), (p.detach() for p in self._params())))
             children = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1)
                         + src["xyz"].index_select(0, split_i).repeat(N, 1),
                         "scaling": torch.log(scal_s.repeat(N, 1) / (0.8 * N))}

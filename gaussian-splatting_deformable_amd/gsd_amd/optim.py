@@ -80,8 +80,16 @@ class FusedAdam(torch.optim.Optimizer):
     def step_count(self, n: int):
         self.steps = [int(n)] * len(self.steps)
 
-    def zero_grad(self, set_to_none: bool = False):
-        self.flat.zero()
+    def zero_grad(self, set_to_none: bool = True):
+        """torch.optim.Optimizer.zero_grad.  set_to_none=True (torch's default; the reference's call,
+        train.py:683) leaves every parameter without a gradient: the slab is marked stale (FlatGrads.invalidate),
+        so a parameter no backward writes before the next step is skipped by it, step count and moments
+        untouched, as torch.optim.Adam skips a grad-None parameter.  set_to_none=False writes zeros: such a
+        parameter is then stepped with a zero gradient, as torch does."""
+        if set_to_none:
+            self.flat.invalidate()
+        else:
+            self.flat.zero()
 
     def _advance(self, missing, done=frozenset()):
         """torch.optim.Adam skips a parameter whose grad is None and keeps state['step'] per parameter: count
@@ -196,9 +204,15 @@ class FusedAdam(torch.optim.Optimizer):
         if self.flat.epilogue is not None:
             raise RuntimeError("step_in_backward: already inside a step_in_backward block")
         self.flat.epilogue = self
+        steps0 = list(self.steps)
         try:
             yield self
         except BaseException:
+            # the step did not happen: step counts back to where they were.  A fused epilogue that was already
+            # queued before the exception may have updated its parameters and moments in place (the device work
+            # cannot be recalled), so after an exception here the optimizer state of the fused parameters is
+            # undefined; the step counts stay torch's (no step taken).
+            self.steps = steps0
             self.flat.epilogue = None
             self.flat.fused = set()
             self.flat.drain_early()

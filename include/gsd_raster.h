@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 11
+#define GSD_ABI_VERSION 12
 
 enum {
     GSD_OK = 0,
@@ -292,6 +292,17 @@ int gsd_l1_ssim(int32_t C, int32_t H, int32_t W, const float* img, const float* 
  * the loss gradient at lambda_dssim = 1 into the gradient of SSIM itself (utils/loss_utils.py:33 ssim). */
 int gsd_l1_ssim_backward(int32_t C, int32_t H, int32_t W, const float* img, const float* gt, float lambda_dssim,
                          const float* grad_out, float sign, float* dL_dimg, const void* workspace, void* stream);
+
+/* Offset-norm regulariser of the training loss (ABI 12; train.py:329-332, added to L1 before the SSIM mix of
+ * :529):  out[0] = mean over the P rows of ||offset[g]||_2, i.e. torch.norm(means3D_offset, dim=-1).mean().
+ * offset (P,3) contiguous float32; out one device float; workspace gsd_offset_norm_workspace_bytes(P) bytes.
+ * The row norms are summed per workgroup and then in a fixed order (deterministic). */
+size_t gsd_offset_norm_workspace_bytes(int64_t P);
+int gsd_offset_norm(int64_t P, const float* offset, float scale, float* out, void* workspace, void* stream);
+/* Backward: d_offset[g] = grad_out[0] * scale * offset[g] / ||offset[g]|| (grad_out: one device float, NULL => 1;
+ * scale = the forward's), zero where the norm is zero (torch's norm backward).  d_offset (P,3) is written. */
+int gsd_offset_norm_backward(int64_t P, const float* offset, const float* grad_out, float scale, float* d_offset,
+                             void* stream);
 
 /* One Adam step (torch.optim.Adam semantics as configured in scene/gaussian_model.py:839-856: per-group
  * learning rate, betas, eps 1e-15, no weight decay / amsgrad) over flat slabs of n floats: param, grad,

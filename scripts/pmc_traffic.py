@@ -2,9 +2,10 @@
 """HBM traffic per launch from rocprofv3 PMC passes (scripts/gpu_pmc.sh with FETCH_SIZE and WRITE_SIZE in
 separate passes), corrected as /opt/skills/guides/MI355X_MICROARCH.md (HBM section) prescribes for gfx950:
 FETCH_SIZE (KB) reports half the bytes of wide coalesced reads -> doubled; WRITE_SIZE (KB) is taken as is.
-Writes a JSON {kernel: {fetch_kb, write_kb, hbm_bytes}} that bench.py reads for roofline.traffic.
+Writes a JSON {kernel: {fetch_kb, write_kb, hbm_bytes, valu}, "_workload": W} that bench.py reads for
+roofline.traffic and the VALU roof -- only for a bench run of the same workload W ("cfg4", "cfg5", ...).
 
-    python scripts/pmc_traffic.py gpurun_out/pmc profiles/round1/pmc_traffic.json
+    python scripts/pmc_traffic.py gpurun_out/pmc profiles/round3/pmc/cfg4/pmc_traffic.json cfg4
 """
 import json
 import os
@@ -20,7 +21,7 @@ def short(name):
     return n[2:] if n.startswith("k_") else n
 
 
-def main(src, dst):
+def main(src, dst, workload):
     s = summarise(src)
     out = {}
     for k, cs in s.items():
@@ -40,7 +41,8 @@ def main(src, dst):
             if cs.get("SQ_WAVE_CYCLES"):
                 e["valu"]["lds_issue_wait_frac"] = round(cs.get("SQ_WAIT_INST_LDS", 0.0) / cs["SQ_WAVE_CYCLES"], 4)
         out[short(k)] = e
-    out["_note"] = ("per-launch means over the profiled launches (scripts/prof_render.py, cfg 4); FETCH_SIZE x2 "
+    out["_workload"] = workload
+    out["_note"] = (f"per-launch means over the profiled launches (scripts/prof_render.py, {workload}); FETCH_SIZE x2 "
                     "per the gfx950 calibration, WRITE_SIZE as is; gathers and atomics are uncalibrated widths; "
                     "valu: SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) against 0.5 per SIMD-cycle")
     with open(dst, "w") as fh:
@@ -49,5 +51,6 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc",
-         sys.argv[2] if len(sys.argv) > 2 else "profiles/round1/pmc_traffic.json")
+    if len(sys.argv) != 4:
+        sys.exit("usage: pmc_traffic.py SRC_DIR DST_JSON WORKLOAD (e.g. cfg4)")
+    main(sys.argv[1], sys.argv[2], sys.argv[3])

@@ -10,7 +10,9 @@ The reference modules are imported by file path, no bytecode written:
   utils/general_utils.py  build_scaling_rotation, strip_symmetric (their hard-coded
                           device="cuda" is redirected to the CPU for this run)
   utils/loss_utils.py     l1_loss, ssim
-Outputs are plain .npz arrays (inputs and expected outputs; no pickles).
+  utils/general_utils.py  get_expon_lr_func (the training loop's learning-rate schedule)
+Outputs are plain .npz arrays (inputs and expected outputs; no pickles).  Arguments name the sections to
+write (default: all): se3 sh camera cov3d loss lr.
 """
 from __future__ import annotations
 
@@ -47,13 +49,36 @@ def cpu_torch_proxy():
     return proxy
 
 
+def lr_schedule(genu):
+    """get_expon_lr_func at the reference's own arguments (gaussian_model.py:857-864 with
+    arguments/__init__.py:74-77) and with a delay, over steps that cover both clips and a negative step."""
+    steps = np.array([-1, 0, 1, 2, 10, 99, 100, 500, 1000, 2999, 3000, 7000, 15000, 29999, 30000, 39999, 40000,
+                      40001, 100000], dtype=np.int64)
+    cases = {"xyz": dict(lr_init=0.00016, lr_final=0.0000016, lr_delay_mult=0.01, max_steps=40_000),
+             "offset": dict(lr_init=8e-4, lr_final=1.6e-6, max_steps=40_000),
+             "delay": dict(lr_init=0.01, lr_final=1e-4, lr_delay_steps=500, lr_delay_mult=0.01, max_steps=30_000),
+             "zero": dict(lr_init=0.0, lr_final=0.0, max_steps=100)}
+    out = {"steps": steps}
+    for name, kw in cases.items():
+        f = genu.get_expon_lr_func(**kw)
+        out[name] = np.array([float(f(int(s))) for s in steps], dtype=np.float64)
+        for k, v in kw.items():
+            out[f"{name}_{k}"] = np.float64(v)
+    np.savez(os.path.join(OUT, "lr.npz"), **out)
+
+
 def main():
+    only = set(sys.argv[1:])
     rb = load("ref_rigid_body", "scene/rigid_body.py")
     shu = load("ref_sh_utils", "utils/sh_utils.py")
     gu = load("ref_graphics_utils", "utils/graphics_utils.py")
     genu = load("ref_general_utils", "utils/general_utils.py")
     genu.torch = cpu_torch_proxy()
     lu = load("ref_loss_utils", "utils/loss_utils.py")
+    if only == {"lr"}:   # the later sections draw nothing from the generator: write them alone
+        lr_schedule(genu)
+        print("wrote lr.npz")
+        return
     g = torch.Generator().manual_seed(1234)
 
     # ---- SE(3): exp_se3 on normalised twists (gaussian_model.py:161-165), float64
@@ -115,6 +140,7 @@ def main():
     im2 = torch.rand(3, 40, 48, generator=g)
     np.savez(os.path.join(OUT, "loss.npz"), img1=im1.numpy(), img2=im2.numpy(),
              l1=lu.l1_loss(im1, im2).numpy(), ssim=lu.ssim(im1, im2).numpy())
+    lr_schedule(genu)
     print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".npz")))
 
 

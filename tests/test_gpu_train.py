@@ -529,3 +529,138 @@ def test_fused_adam_addend_matches_torch_adam():
     for pa, pb in zip(a, b):
         assert float((pa - pb).abs().max()) <= 1e-6
     assert opt_a.flat.addends == {}
+
+
+@pytest.mark.parametrize("P", [1, 37, 100_003, 1_000_000])
+def test_offset_norm_matches_torch(P):
+    """train.py:329 torch.norm(means3D_offset, dim=-1).mean() (the expression itself is the reference) against
+    gsd_offset_norm: value rel 1e-5 (deterministic fixed-order sum vs torch's reduction order), gradient rel L2
+    1e-6, zero rows giving a zero gradient as torch's norm backward does."""
+    from gsd_amd.loss import offset_norm
+    gen = torch.Generator().manual_seed(P)
+    x = torch.randn(P, 3, generator=gen) * 0.05
+    x[::7] = 0.0                                                          # zero offsets (norm 0)
+    a = x.clone().to(DEV).requires_grad_(True)
+    b = x.clone().to(DEV).requires_grad_(True)
+    got = offset_norm(a)
+    ref = torch.norm(b, dim=-1).mean()
+    assert abs(float(got) - float(ref)) <= 1e-5 * max(float(ref), 1e-30)
+    (3.0 * got).backward()
+    (3.0 * ref).backward()
+    assert rel_l2(a.grad, b.grad) <= 1e-6
+    assert float(a.grad[::7].abs().max()) == 0.0
+    assert float(offset_norm(a.detach(), 2.0)) == pytest.approx(2.0 * float(got), rel=1e-6)
+
+
+def test_training_loss_with_offset_regulariser():
+    """The reference's loss of train.py:323-332 and :529 -- (1 - l) (L1 + 0.1 mean||offset||) + l (1 - SSIM) --
+    against its literal torch expression over the loss restatement; the gradient reaches both the image and the
+    offsets.  An undeformed render's offset (an expanded zero row, no gradient) adds exactly 0."""
+    from gsd_amd.loss import l1_ssim_loss, training_loss
+    from oracle import loss_ref
+    gen = torch.Generator().manual_seed(31)
+    gt = torch.rand(3, 60, 80, generator=gen).to(DEV)
+    base = (gt + 0.1 * torch.randn(3, 60, 80, generator=gen).to(DEV)).clamp(0, 1)
+    off0 = (torch.randn(5000, 3, generator=gen) * 0.02).to(DEV)
+    x1, o1 = base.clone().requires_grad_(True), off0.clone().requires_grad_(True)
+    x2, o2 = base.clone().requires_grad_(True), off0.clone().requires_grad_(True)
+    got = training_loss(x1, gt, o1, 0.2)
+    Ll1 = loss_ref.l1_loss(x2, gt) + 0.1 * torch.norm(o2, dim=-1).mean()
+    ref = (1.0 - 0.2) * Ll1 + 0.2 * (1.0 - loss_ref.ssim(x2, gt))
+    assert abs(float(got) - float(ref)) <= 1e-5 * abs(float(ref))
+    got.backward()
+    ref.backward()
+    assert rel_l2(x1.grad, x2.grad) <= 1e-4 and rel_l2(o1.grad, o2.grad) <= 1e-6
+    zero = torch.zeros(1, 3, device=DEV).expand(5000, 3)
+    assert float(training_loss(base, gt, zero)) == float(l1_ssim_loss(base, gt))
+
+
+def test_fused_adam_follows_expon_lr_schedule():
+    """update_learning_rate (scene/gaussian_model.py:875-886) rewriting the xyz and offset_model groups every step,
+    on FusedAdam and on torch.optim.Adam: same parameters after 6 steps (1e-6), through both the plain step and
+    the data-parallel entry at world size 1."""
+    from gsd_amd.schedule import get_expon_lr_func, update_learning_rate
+    a, b, opt_a, opt_b, gen = _adam_pair(seed=17)
+    opt_a.param_groups[0]["name"] = opt_b.param_groups[0]["name"] = "xyz"
+    xyz = get_expon_lr_func(0.00016, 0.0000016, max_steps=10)
+    off = get_expon_lr_func(8e-4, 1.6e-6, max_steps=10)
+    for k in range(6):
+        for opt in (opt_a, opt_b):
+            update_learning_rate(opt, 2 * k, xyz, off)
+        assert opt_a.param_groups[0]["lr"] == xyz(2 * k) and opt_a.param_groups[3]["lr"] == off(2 * k)
+        ws = [torch.randn(p.shape, generator=gen).to(DEV) for p in a]
+        _adam_backward(a, ws, True)
+        _adam_backward(b, ws, True)
+        opt_a.allreduce_step(zero_grad=True) if k % 2 else opt_a.step(zero_grad=True)
+        opt_b.step()
+        opt_b.zero_grad(set_to_none=True)
+    for pa, pb in zip(a, b):
+        assert float((pa - pb).abs().max()) <= 1e-6 * max(1.0, float(pb.abs().max()))
+
+
+def test_zero_grad_set_to_none_skips_parameters_without_grad():
+    """optimizer.zero_grad(set_to_none=True) (train.py:683) then a backward that reaches only the Gaussian groups:
+    torch.optim.Adam skips the network's grad-None parameters (no move, no step count, moments kept); FusedAdam
+    must do the same.  zero_grad(set_to_none=False) leaves zeros instead, which torch steps."""
+    a, b, opt_a, opt_b, gen = _adam_pair(seed=23)
+    for k in range(4):
+        ws = [torch.randn(p.shape, generator=gen).to(DEV) for p in a]
+        with_net = k == 0
+        _adam_backward(a, ws, with_net)
+        _adam_backward(b, ws, with_net)
+        opt_a.step()
+        opt_b.step()
+        opt_a.zero_grad(set_to_none=(k != 1))
+        opt_b.zero_grad(set_to_none=(k != 1))
+        for i, (pa, pb) in enumerate(zip(a, b)):
+            st = opt_b.state.get(pb)
+            assert opt_a.steps[i] == (int(st["step"]) if st else 0), (k, i)
+            assert float((pa - pb).abs().max()) <= 1e-6 * max(1.0, float(pb.abs().max())), (k, i)
+    # the network got a gradient at k = 0 and a zero-filled one at k = 2 (after set_to_none=False): two steps;
+    # none at k = 1 and 3 (after set_to_none=True)
+    assert opt_a.steps[3:] == [2, 2, 2]
+
+
+def test_densify_and_prune_carries_the_se3_twist():
+    """SE(3) mode: the per-Gaussian twist is trained (its own optimizer group) and must follow the densification
+    surgery like the other per-Gaussian attributes -- clones and split children inherit their parent's twist with
+    zero moments, pruned points drop it -- so the next SE(3) render sees a twist of the new length.  The twist is
+    set to a copy of attributes the reference's surgery already carries (rotation, f_dc), so the rows can be
+    checked exactly; its moment rows must be zero exactly where the rotation's are."""
+    from gsd_amd import DeformableGaussians, l1_ssim_loss, render, default_pipe
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.densify import GaussianDensifier
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import make_gaussians
+    P, W, H = 4000, 320, 240
+    prm = make_gaussians(P, W, H, seed=22, se3="random", device=DEV)
+    with torch.no_grad():
+        prm.twist.copy_(torch.cat([prm.rotation, prm.features_dc[:, 0, :2]], 1))
+    pc = DeformableGaussians(prm, sh_degree=3, deform="se3")
+    names = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation", "twist"]
+    opt = FusedAdam([{"params": [p], "lr": 1e-3, "name": n} for p, n in zip(pc.parameters(), names)], lr=0.0,
+                    eps=1e-15)
+    dens = GaussianDensifier(pc, opt)
+    gen = torch.Generator().manual_seed(4)
+    for p in pc.parameters():   # one step with the same gradient rows for rotation and twist: equal moments
+        p.grad.copy_(torch.randn(p.shape, generator=gen).to(DEV) * 1e-3)
+    with torch.no_grad():
+        pc._twist.grad.copy_(torch.cat([pc._rotation.grad, pc._features_dc.grad[:, 0, :2]], 1))
+    opt.step(zero_grad=True)
+    vg = torch.randn(P, 3, generator=gen).to(DEV) * 2e-4
+    holder = torch.zeros(P, 3, device=DEV, requires_grad=True)
+    holder.grad = vg
+    dens.add_densification_stats(holder, torch.randint(1, 30, (P,), generator=gen, dtype=torch.int32).to(DEV))
+    extent = float(torch.exp(pc._scaling).max(dim=1).values.median()) / 0.01
+    dens.densify_and_prune(2e-4, 0.05, extent, 20)
+    Pn = pc._xyz.shape[0]
+    assert Pn != P and pc._twist.shape == (Pn, 6)
+    assert torch.equal(pc._twist[:, :4], pc._rotation) and torch.equal(pc._twist[:, 4:], pc._features_dc[:, 0, :2])
+    mt, vt = opt.moments(pc._twist)
+    mr, vr = opt.moments(pc._rotation)
+    assert torch.equal(mt[:, :4], mr) and torch.equal(vt[:, :4], vr)
+    assert int((mr.abs().sum(1) == 0).sum()) > 0          # new points with zero moments exist
+    cam = synthetic_camera(W, H).to(DEV)
+    out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
+    l1_ssim_loss(out["render"], torch.zeros_like(out["render"])).backward()
+    assert pc._twist.grad.shape == (Pn, 6) and torch.isfinite(pc._twist.grad).all()
