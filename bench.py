@@ -381,6 +381,21 @@ def main():
 
     K_end = int(gsdC.last_forward.get("num_rendered", 0))
     P_end = int(pc._xyz.shape[0])   # densified count at the end of the timed steps
+    # data parallel: the replicated parameters must still be bit-identical on every rank after the timed steps
+    # (every rank applies the same summed gradients): a bit-pattern checksum of the parameter slab, min == max
+    replicas = None
+    if world > 1:
+        with torch.no_grad():
+            ck = opt.param_slab.view(torch.int32).to(torch.int64).sum().reshape(1)
+            lo, hi = ck.clone(), ck.clone()
+            if dist.get_backend() == "nccl":
+                dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+                dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            else:
+                lo, hi = lo.cpu(), hi.cpu()
+                dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+                dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            replicas = bool(int(lo.item()) == int(hi.item()))
     restore()
     # fwd+bwd ms/view: render + loss + backward of one view (no optimizer / collective),
     # hipEvents on the current stream, median over >= 100 views, two ways:
@@ -500,6 +515,8 @@ def main():
         }
         if exchange is not None:
             res["exchange"] = exchange
+        if replicas is not None:
+            res["replicas_identical"] = replicas
         print(json.dumps(res), flush=True)
     if dist.is_initialized():
         dist.barrier()

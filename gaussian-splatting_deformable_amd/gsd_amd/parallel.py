@@ -41,7 +41,22 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
+        signature_group()   # collective: every rank creates the host-side group at the same point
     return rank, local, world
+
+
+_SIG_GROUP = None
+
+
+def signature_group():
+    """The process group of the per-step layout check (FlatGrads.verify_layout): the default group when it is
+    gloo, else a gloo group over the same ranks, so the check is a host-side exchange that never waits on the
+    device.  Creating it is a collective: init_from_env does it on every rank; a caller that initialises the
+    default group itself must call this on every rank before the first data-parallel step."""
+    global _SIG_GROUP
+    if _SIG_GROUP is None:
+        _SIG_GROUP = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+    return _SIG_GROUP
 
 
 def slab_view(slab, off, like=None, shape=None, coef_major=False):
@@ -129,7 +144,44 @@ class FlatGrads:
         self.addends = {}      # id(p) -> tensor: a gradient term already summed over the ranks (add_after_reduce)
         self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
         self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
+        self._sig_pending = None
         self.attach()
+
+    # ---- the layout check of the data-parallel path ----
+    def layout_signature(self):
+        """What every rank's slab must agree on before its collectives: the slab size, the parameters' shapes
+        (a densification that ran on one rank only changes both), the bucket size and the SH-view exchange mode
+        (which decide the collectives' sizes and count)."""
+        shapes = 0
+        for p in self.params:
+            for d in (p.dim(),) + tuple(p.shape):
+                shapes = (shapes * 1000003 + int(d)) % (1 << 61)
+        return [int(self.slab.numel()), len(self.params), shapes, int(BUCKET_FLOATS), int(SH_VIEWS)]
+
+    def post_layout_check(self):
+        """Start this step's layout check: an asynchronous host-side all-gather of layout_signature() on the gloo
+        signature group (its latency overlaps the forward).  Posted at most once between verifications, at the
+        start of a step (invalidate / zero)."""
+        if self._sig_pending is not None or not dp_active():
+            return
+        sig = torch.tensor(self.layout_signature(), dtype=torch.int64)
+        outs = [torch.empty_like(sig) for _ in range(dist.get_world_size())]
+        work = dist.all_gather(outs, sig, group=signature_group(), async_op=True)
+        self._sig_pending = (sig, outs, work)
+
+    def verify_layout(self):
+        """Before the first collective of a step: every rank's signature must equal this rank's -- otherwise every
+        rank raises here (each sees all signatures) instead of entering collectives of different sizes, which
+        would hang or sum unrelated memory."""
+        if self._sig_pending is None:
+            return
+        sig, outs, work = self._sig_pending
+        self._sig_pending = None
+        work.wait()
+        if any(not torch.equal(o, sig) for o in outs):
+            raise RuntimeError("FlatGrads: the data-parallel ranks' gradient slabs differ (per rank [numel, "
+                               f"params, shapes hash, bucket floats, SH views]: {[o.tolist() for o in outs]}); "
+                               "every rank must hold the same Gaussians (densify on every rank) and settings")
 
     def _fused_guard(self, ids):
         if self.fused.intersection(ids) or self.early_ids.intersection(ids):
@@ -165,6 +217,7 @@ class FlatGrads:
         self.reduced = set()
         self.addends = {}
         self.attach()
+        self.post_layout_check()
 
     def invalidate(self):
         """Mark every view stale (no memory traffic): the next gradient producer stores instead of adding."""
@@ -173,6 +226,7 @@ class FlatGrads:
         self.reduced = set()
         self.addends = {}
         self._version = self.slab._version
+        self.post_layout_check()
 
     def add_after_reduce(self, p, t):
         """A term of ``p``'s gradient that is already the sum over every rank (gsd_sh_grad_views_ex's view-direction
@@ -248,6 +302,7 @@ class FlatGrads:
         ids = {id(p) for p in params}
         if not ids <= set(self._view_of) or ids & self.early_ids:
             raise RuntimeError("early_allreduce: parameters not in this slab, or already reduced this step")
+        self.verify_layout()
         keep = [p for p in self.params if id(p) not in ids]
         nccl = dist.get_backend() == "nccl" or not self.slab.is_cuda
         for a, b in self._runs({id(p) for p in keep}):
@@ -293,6 +348,7 @@ class FlatGrads:
         if not dp_active():
             self._apply_addends()
             return None
+        self.verify_layout()
         if async_op and self.addends:
             raise RuntimeError("FlatGrads.allreduce(async_op=True): pending addends need the reduced sums first")
         if not async_op:
@@ -327,6 +383,7 @@ class FlatGrads:
         n = self.slab.numel()
         if not dp_active():
             return [(0, n, None)]
+        self.verify_layout()
         work = list(early)   # ranges whose all-reduce went out inside the backward (early_allreduce)
         nccl = dist.get_backend() == "nccl" or not self.slab.is_cuda
         for a, b in self._runs(reduced):

@@ -283,6 +283,9 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
         binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity)
+    f_flat = getattr(f_dc, "_gsd_flat", None)
+    if f_flat is not None:
+        f_flat.verify_layout()   # every rank's P and settings agree before the P-sized all-gather
     views = torch.empty(world, stride, dtype=torch.float32, device=dev)
     gathered = None
     if dist.get_backend() == "nccl":   # RCCL: one all_gather into the (world, stride) buffer

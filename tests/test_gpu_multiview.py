@@ -200,12 +200,15 @@ def test_one_rank_rccl_matches_single_process(tmp_path):
     assert float((d > 1e-6).float().mean()) <= 1e-4
 
 
-def test_bench_gpus_2_spawns_two_ranks():
+@pytest.mark.parametrize("sh_views", ["1", "0"])
+def test_bench_gpus_2_spawns_two_ranks(sh_views):
     """``bench.py --gpus 2`` without a launcher starts torch.distributed.run with two ranks itself (here both on the
     one GPU, GSD_DIST_BACKEND=gloo: the rehearsal of the data-parallel path); rank 0 prints ONE JSON line with
-    n_gpus 2, the data-parallel exchange timed alone, and value = 2 views per step over the max-over-ranks time."""
+    n_gpus 2, the data-parallel exchange timed alone, and value = 2 views per step over the max-over-ranks time.
+    With the SH gradient exchanged as per-view rows (GSD_SH_VIEWS=1) and all-reduced whole (=0), the replicated
+    parameters must be bit-identical on both ranks after the timed steps (bench.py's replicas_identical)."""
     import json
-    env = dict(os.environ, GSD_DIST_BACKEND="gloo")
+    env = dict(os.environ, GSD_DIST_BACKEND="gloo", GSD_SH_VIEWS=sh_views)
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "2", "--steps",
                         "3", "--warmup", "1", "--cpu-baseline", "off"], env=env, capture_output=True, text=True,
@@ -217,3 +220,4 @@ def test_bench_gpus_2_spawns_two_ranks():
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["config"]["views_per_step"] == 2
     assert res["exchange"]["backend"] == "gloo" and res["exchange"]["allreduce_ms"] > 0
     assert res["value"] == pytest.approx(2 * 3 / (3 * res["ms_per_step"] / 1000.0), rel=1e-2)
+    assert res["replicas_identical"] is True

@@ -346,3 +346,45 @@ def test_single_pass_densify_equals_clone_split_prune():
     assert pa[0].shape[0] not in (300,) and pa[0].shape == pb[0].shape
     for a, b in zip(pa + ma, pb + mb):
         assert torch.equal(a, b)
+
+
+def _worker_divergent(rank, world, port, out_dir):
+    """Ranks whose slabs disagree -- a different Gaussian count (a densification that ran on one rank only), or a
+    different bucket size -- must all raise at their first collective of the step (FlatGrads.verify_layout on
+    the host-side signature exchange), not enter collectives of different sizes and hang."""
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd import parallel
+    from gsd_amd.parallel import FlatGrads, init_from_env
+    r, _, w = init_from_env(backend="gloo")
+    msgs = []
+    for case in ("P", "bucket", "same"):
+        n = 100 + (r if case == "P" else 0)
+        parallel.BUCKET_FLOATS = 1 << (10 + (r if case == "bucket" else 0))
+        params = [torch.nn.Parameter(torch.zeros(n, 3)), torch.nn.Parameter(torch.zeros(n, 1))]
+        fg = FlatGrads(params, device="cpu")
+        fg.invalidate()            # the start of a step: posts the layout check
+        for p in params:
+            p.grad.fill_(1.0)
+        try:
+            for _, _, wk in fg.allreduce_buckets(parallel.BUCKET_FLOATS):
+                if wk is not None:
+                    wk.wait()
+            msgs.append(f"{case}: ok {float(fg.slab.sum()):.1f}")
+        except RuntimeError as e:
+            msgs.append(f"{case}: raised {'differ' in str(e)}")
+    with open(os.path.join(out_dir, f"rank{r}.txt"), "w") as fh:
+        fh.write("\n".join(msgs))
+    dist.destroy_process_group()
+
+
+def test_rank_divergent_layouts_raise_on_every_rank(tmp_path):
+    world = 2
+    mp.spawn(_worker_divergent, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        got = (tmp_path / f"rank{r}.txt").read_text().splitlines()
+        assert got == ["P: raised True", "bucket: raised True", "same: ok 800.0"], (r, got)
