@@ -84,12 +84,15 @@ class FusedAdam(torch.optim.Optimizer):
         """torch.optim.Optimizer.zero_grad.  set_to_none=True (torch's default; the reference's call,
         train.py:683) leaves every parameter without a gradient: the slab is marked stale (FlatGrads.invalidate),
         so a parameter no backward writes before the next step is skipped by it, step count and moments
-        untouched, as torch.optim.Adam skips a grad-None parameter.  set_to_none=False writes zeros: such a
-        parameter is then stepped with a zero gradient, as torch does."""
+        untouched, as torch.optim.Adam skips a grad-None parameter.  set_to_none=False zeroes the gradients that
+        exist and leaves grad-None parameters without one (torch zeroes only existing .grad tensors): a parameter
+        with a zeroed gradient is then stepped with it, as torch does."""
         if set_to_none:
             self.flat.invalidate()
         else:
+            none = set(self.flat.stale)   # the parameters without a gradient (stale views) stay so
             self.flat.zero()
+            self.flat.stale = none
 
     def _advance(self, missing, done=frozenset()):
         """torch.optim.Adam skips a parameter whose grad is None and keeps state['step'] per parameter: count
@@ -99,6 +102,14 @@ class FusedAdam(torch.optim.Optimizer):
         for i in active:
             self.steps[i] += 1
         return set(active)
+
+    def _bump(self, indices):
+        """Advance the autograd version counter of the parameters updated in place through raw pointers (the HIP
+        Adam pass and the fused epilogue write memory torch does not see): caches keyed on (data_ptr, _version)
+        -- the fused deformation-network forward's packed weights -- then repack, and autograd refuses a graph
+        that saved a parameter before this step.  Called once the backward is over."""
+        for i in indices:
+            torch.autograd.graph.increment_version(self._params[i])
 
     def _adam(self, a: int, b: int, active, addends=()):
         """gsd_adam_step over slab elements [a, b) of the parameters in ``active``: one launch per contiguous
@@ -164,6 +175,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.flat.collect()
         active = self._advance(self.flat.settle())
         self._adam(0, self.param_slab.numel(), active, self.flat.addend_ranges())
+        self._bump(active)
         if zero_grad:
             self.flat.invalidate()
         return loss
@@ -188,6 +200,7 @@ class FusedAdam(torch.optim.Optimizer):
             if w is not None:
                 w.wait()
                 self._adam(a, b, active, addends)
+        self._bump(active)
         if zero_grad:
             self.flat.invalidate()
 
@@ -219,6 +232,7 @@ class FusedAdam(torch.optim.Optimizer):
             raise
         self.flat.epilogue = None
         self.allreduce_step(zero_grad=True)
+        self._bump(i for i, p in enumerate(self._params) if id(p) in self.flat.fused)
         self.flat.fused = set()
 
     def fuse(self, named, epi=None, summed=False):

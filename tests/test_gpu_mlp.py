@@ -130,3 +130,26 @@ def test_mlp_training_backward_matches_reference_torch_path():
         grads[name] = [xx.grad] + [p.grad.clone() for p in net.parameters()]
     for a, b in zip(grads["fused"], grads["plain"]):
         assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-7
+
+
+def test_fused_mlp_repacks_after_fused_adam_step():
+    """The fused forward caches its packed weights under the parameters' (data_ptr, _version); FusedAdam updates
+    them in place through raw pointers, so its step must advance their versions: a fused forward after the step
+    uses the new weights (equal to a fresh pack's), not the cached ones."""
+    from gsd_amd.optim import FusedAdam
+    net = _net(15, 2.0)
+    opt = FusedAdam([{"params": list(net.parameters()), "lr": 1e-2, "name": "offset_model"}], lr=0.0, eps=1e-15)
+    x = (torch.rand(300, 3) * 2 - 1).cuda()
+    t = torch.full((300, 1), 0.3, device="cuda")
+    with torch.no_grad():
+        before = torch.cat(net(x, t, 5000), -1)
+    for p in net.parameters():
+        p.grad.copy_(torch.randn_like(p))
+    opt.step(zero_grad=True)
+    with torch.no_grad():
+        after = torch.cat(net(x, t, 5000), -1)
+    net._fused_key = None   # force a fresh pack of the current weights
+    with torch.no_grad():
+        fresh = torch.cat(net(x, t, 5000), -1)
+    assert not torch.equal(after, before)
+    assert torch.equal(after, fresh)

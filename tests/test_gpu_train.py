@@ -601,7 +601,8 @@ def test_fused_adam_follows_expon_lr_schedule():
 def test_zero_grad_set_to_none_skips_parameters_without_grad():
     """optimizer.zero_grad(set_to_none=True) (train.py:683) then a backward that reaches only the Gaussian groups:
     torch.optim.Adam skips the network's grad-None parameters (no move, no step count, moments kept); FusedAdam
-    must do the same.  zero_grad(set_to_none=False) leaves zeros instead, which torch steps."""
+    must do the same.  zero_grad(set_to_none=False) zeroes the gradients that exist (stepped with zeros next) and
+    leaves grad-None parameters without one."""
     a, b, opt_a, opt_b, gen = _adam_pair(seed=23)
     for k in range(4):
         ws = [torch.randn(p.shape, generator=gen).to(DEV) for p in a]
@@ -616,9 +617,9 @@ def test_zero_grad_set_to_none_skips_parameters_without_grad():
             st = opt_b.state.get(pb)
             assert opt_a.steps[i] == (int(st["step"]) if st else 0), (k, i)
             assert float((pa - pb).abs().max()) <= 1e-6 * max(1.0, float(pb.abs().max())), (k, i)
-    # the network got a gradient at k = 0 and a zero-filled one at k = 2 (after set_to_none=False): two steps;
-    # none at k = 1 and 3 (after set_to_none=True)
-    assert opt_a.steps[3:] == [2, 2, 2]
+    # the network got a gradient at k = 0 only: set_to_none=False after k = 1 zeroes existing gradients and leaves
+    # its grad None (torch), so k = 2 skips it as well
+    assert opt_a.steps[3:] == [1, 1, 1] and opt_a.steps[:3] == [4, 4, 4]
 
 
 def test_densify_and_prune_carries_the_se3_twist():
