@@ -255,13 +255,13 @@ hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 // ---- optional per-kernel device timing (gsd_timing_*) ----
 enum KernelId { kPreFwd, kTileHist, kTileScan, kScatter, kTileSort, kRenderFwd, kRenderBwd, kPreBwd, kSe3Fwd,
                 kSe3Bwd, kMarkVis, kActFwd, kActBwd, kLoss, kLossBwd, kShViews, kAdam, kDensify, kKnn, kMlp, kMlpBwd,
-                kOffNorm, kOffNormBwd, kNumKernels };
+                kOffNorm, kOffNormBwd, kMlpTrainFwd, kMlpTrainBwd, kNumKernels };
 const char* const kKernelNames[kNumKernels] = {"preprocess_fwd", "tile_hist",    "tile_scan",    "scatter_keys",
                                                "tile_sort",      "render_fwd",   "render_bwd",   "preprocess_bwd",
                                                "se3_fwd",        "se3_bwd",      "mark_visible", "activate_fwd",
                                                "activate_bwd",   "l1_ssim",      "l1_ssim_bwd",  "sh_grad_views", "adam",         "densify_stats",
                                                "knn",            "deform_mlp",   "deform_mlp_relu_bias",
-                                               "offset_norm",    "offset_norm_bwd"};
+                                               "offset_norm",    "offset_norm_bwd", "deform_mlp_train_fwd", "deform_mlp_train_bwd"};
 struct TimingState {
     bool on = false;
     struct Rec {
@@ -925,6 +925,185 @@ int gsd_relu_backward_bias(int64_t P, int32_t N, int32_t bf16, const void* grad_
     hipStream_t s = as_stream(stream);
     timed(kMlpBwd, s, [&] {
         gsd::launch_relu_bwd_bias(P, N, bf16, grad_out, out, grad_in, bias_partial, rows_per_block, s);
+    });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+// ---- the deformation network's f32-accurate training path (gsd_mlp_train.hip) ----
+}  // extern "C"
+namespace {
+// padded input / output widths of the nine layers (8 hidden + the heads) and the reference's weight widths
+constexpr int kMlpIn[9] = {96, 256, 256, 256, 256, 320, 256, 256, 256};
+constexpr int kMlpOut[9] = {256, 256, 256, 256, 256, 256, 256, 256, 64};
+constexpr int kMlpLdw[9] = {84, 256, 256, 256, 256, 319, 256, 256, 256};
+constexpr int kMlpMap[9] = {1, 0, 0, 0, 0, 2, 0, 0, 0};
+constexpr int kMlpChunk = 2048;   // Gaussians per wave of the weight-gradient kernel
+
+size_t mlp_frag_bytes(int M, int K) { return (size_t)(K / 16) * (M / 32) * 3 * 64 * 16; }
+
+struct MlpWs {
+    int64_t ldp;
+    void* ffrag[9];   // forward A = W
+    void* bfrag[9];   // backward A = W^T
+    float* bias_heads;
+    float *E, *ET, *H[9];   // H[1..8]: the hidden layers' outputs
+    float *Gh, *ga, *gb, *dE;
+    float *partial, *bias_partial;
+};
+size_t carve_mlp(void* base, int64_t P, MlpWs* w) {
+    char* p = base ? align_ptr(base) : nullptr;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* r = p ? p + off : nullptr;
+        off += up(bytes);
+        return r;
+    };
+    MlpWs v{};
+    v.ldp = (P + 255) / 256 * 256;
+    const size_t row = sizeof(float) * (size_t)v.ldp;
+    for (int l = 0; l < 9; ++l) v.ffrag[l] = take(mlp_frag_bytes(kMlpOut[l], kMlpIn[l]));
+    for (int l = 0; l < 9; ++l) v.bfrag[l] = take(mlp_frag_bytes(kMlpIn[l], kMlpOut[l]));
+    v.bias_heads = reinterpret_cast<float*>(take(64 * sizeof(float)));
+    v.E = reinterpret_cast<float*>(take(64 * row));
+    v.ET = reinterpret_cast<float*>(take(32 * row));
+    v.H[0] = nullptr;
+    for (int l = 1; l <= 8; ++l) v.H[l] = reinterpret_cast<float*>(take(256 * row));
+    v.Gh = reinterpret_cast<float*>(take(64 * row));
+    v.ga = reinterpret_cast<float*>(take(256 * row));
+    v.gb = reinterpret_cast<float*>(take(256 * row));
+    v.dE = reinterpret_cast<float*>(take(64 * row));
+    const int64_t chunks = (P + kMlpChunk - 1) / kMlpChunk;
+    v.partial = reinterpret_cast<float*>(take(sizeof(float) * (size_t)chunks * 256 * 320));
+    v.bias_partial = reinterpret_cast<float*>(take(sizeof(float) * (size_t)chunks * 256));
+    if (w) *w = v;
+    return off + kAlign;
+}
+
+gsd::MlpWeightRef mlp_weight(int l, float* const* w, int ldw_override = -1) {
+    gsd::MlpWeightRef r{};
+    if (l < 8) {
+        r.W[0] = w[l];
+        r.row_off[0] = 0;
+        r.row_off[1] = 256;
+        r.n_pieces = 1;
+    } else {   // the heads: dx 3 | d log-scale 3 | d quaternion 4 | dSH 48
+        const int off[5] = {0, 3, 6, 10, 58};
+        for (int i = 0; i < 4; ++i) r.W[i] = w[8 + i];
+        for (int i = 0; i < 5; ++i) r.row_off[i] = off[i];
+        r.n_pieces = 4;
+    }
+    r.ldw = ldw_override >= 0 ? ldw_override : kMlpLdw[l];
+    r.map = ldw_override >= 0 ? 0 : kMlpMap[l];
+    return r;
+}
+
+void mlp_pack_all(float* const* weights, const MlpWs& ws, bool backward, hipStream_t s) {
+    for (int l = 0; l < 9; ++l) {
+        gsd::MlpPackParams pp{};
+        pp.w = mlp_weight(l, weights);
+        pp.transpose = backward ? 1 : 0;
+        pp.M = backward ? kMlpIn[l] : kMlpOut[l];
+        pp.K = backward ? kMlpOut[l] : kMlpIn[l];
+        pp.out = backward ? ws.bfrag[l] : ws.ffrag[l];
+        gsd::launch_mlp_pack(pp, s);
+    }
+}
+}  // namespace
+extern "C" {
+
+size_t gsd_deform_mlp_train_workspace_bytes(int64_t P) { return P > 0 ? carve_mlp(nullptr, P, nullptr) : kAlign; }
+
+int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, const float* const* weights,
+                                 const float* const* biases, void* workspace, float* out, void* stream) {
+    if (P <= 0 || P >= (1ll << 31) - 256) return fail(GSD_ERR_ARG, "deform_mlp_train: need 0 < P < 2^31 - 256");
+    if (!x || !t || !weights || !biases || !workspace || !out) return fail(GSD_ERR_ARG, "null pointer argument");
+    for (int i = 0; i < 12; ++i)
+        if (!weights[i] || !biases[i]) return fail(GSD_ERR_ARG, "deform_mlp_train: 12 weights and 12 biases needed");
+    MlpWs ws;
+    carve_mlp(workspace, P, &ws);
+    hipStream_t s = as_stream(stream);
+    float* const* W = const_cast<float* const*>(weights);
+    float* const* B = const_cast<float* const*>(biases);
+    timed(kMlpTrainFwd, s, [&] {
+        mlp_pack_all(W, ws, false, s);
+        gsd::launch_mlp_gather_bias(mlp_weight(8, B, 1), ws.bias_heads, 64, s);
+        gsd::launch_mlp_encode((int)P, (int)ws.ldp, x, t, ws.E, ws.ET, s);
+        for (int l = 0; l < 9; ++l) {
+            gsd::MlpGemmParams g{};
+            g.P = (int)P;
+            g.ldp = (int)ws.ldp;
+            g.frags = ws.ffrag[l];
+            g.rb = kMlpOut[l] / 32;
+            if (l == 0) {
+                g.src0 = ws.E; g.ks0 = 4; g.src1 = ws.ET; g.ks1 = 2;
+            } else if (l == 5) {
+                g.src0 = ws.E; g.ks0 = 4; g.src1 = ws.H[5]; g.ks1 = 16;
+            } else {
+                g.src0 = ws.H[l]; g.ks0 = 16;
+            }
+            if (l < 8) {
+                g.bias = B[l];
+                g.dst = ws.H[l + 1];
+                gsd::launch_mlp_gemm(g, gsd::kMlpFwdRelu, s);
+            } else {
+                g.bias = ws.bias_heads;
+                g.dst = out;
+                g.n_out = 58;
+                gsd::launch_mlp_gemm(g, gsd::kMlpFwdHeads, s);
+            }
+        }
+    });
+    GSD_CHECK(false, s);
+    return GSD_OK;
+}
+
+int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float* const* weights, void* workspace,
+                                  float* dx, float* const* d_weights, float* const* d_biases, void* stream) {
+    if (P <= 0 || P >= (1ll << 31) - 256) return fail(GSD_ERR_ARG, "deform_mlp_train: need 0 < P < 2^31 - 256");
+    if (!grad_out || !weights || !workspace || !d_weights || !d_biases) return fail(GSD_ERR_ARG, "null pointer argument");
+    for (int i = 0; i < 12; ++i)
+        if (!weights[i] || !d_weights[i] || !d_biases[i])
+            return fail(GSD_ERR_ARG, "deform_mlp_train: 12 weights and 12 weight / bias gradients needed");
+    MlpWs ws;
+    carve_mlp(workspace, P, &ws);
+    hipStream_t s = as_stream(stream);
+    float* const* W = const_cast<float* const*>(weights);
+    const int ldp = (int)ws.ldp;
+    const int chunks = (int)((P + kMlpChunk - 1) / kMlpChunk);
+    auto wgrad = [&](int l, const float* G, int n_rb, const float* X0, const float* X1, int k_rb, int k_rb0) {
+        gsd::MlpWgradParams q{};
+        q.P = (int)P; q.ldp = ldp; q.G = G; q.n_rb = n_rb; q.X0 = X0; q.X1 = X1; q.k_rb = k_rb; q.k_rb0 = k_rb0;
+        q.tiles_n = (n_rb + 3) / 4; q.tiles_k = (k_rb + 3) / 4; q.chunk = kMlpChunk;
+        q.partial = ws.partial; q.bias_partial = ws.bias_partial;
+        gsd::launch_mlp_wgrad(q, mlp_weight(l, d_weights), mlp_weight(l, d_biases, 1), s);
+    };
+    auto dgemm = [&](int l, const float* G, int ks, const float* mask, float* dst, int n_a, int acc_a) {
+        gsd::MlpGemmParams g{};
+        g.P = (int)P; g.ldp = ldp; g.src0 = G; g.ks0 = ks; g.frags = ws.bfrag[l]; g.rb = kMlpIn[l] / 32;
+        g.mask = mask; g.dst = dst; g.n_a = n_a; g.dst_a = ws.dE; g.accumulate_a = acc_a;
+        gsd::launch_mlp_gemm(g, gsd::kMlpBwdMask, s);
+    };
+    (void)chunks;
+    timed(kMlpTrainBwd, s, [&] {
+        mlp_pack_all(W, ws, true, s);
+        gsd::launch_mlp_rows_to_features((int)P, ldp, 58, grad_out, ws.Gh, 64, s);
+        wgrad(8, ws.Gh, 2, ws.H[8], nullptr, 8, 8);
+        dgemm(8, ws.Gh, 4, ws.H[8], ws.ga, 0, 0);   // g of layer 7's pre-activation
+        float* g = ws.ga;
+        float* other = ws.gb;
+        for (int l = 7; l >= 0; --l) {
+            if (l == 0) wgrad(0, g, 8, ws.E, ws.ET, 3, 2);
+            else if (l == 5) wgrad(5, g, 8, ws.E, ws.H[5], 10, 2);
+            else wgrad(l, g, 8, ws.H[l], nullptr, 8, 8);
+            if (l == 5) dgemm(5, g, 16, ws.H[5], other, 64, 0);   // rows 0-63: d enc(x); the rest masked by h5
+            else if (l > 0) dgemm(l, g, 16, ws.H[l], other, 0, 0);
+            else if (dx) dgemm(0, g, 16, nullptr, nullptr, 64, 1);   // d enc(x) += W0^T g (the t rows dropped)
+            float* tmp = g;
+            g = other;
+            other = tmp;
+        }
+        if (dx) gsd::launch_mlp_encode_bwd((int)P, ldp, ws.E, ws.dE, dx, 0, s);
     });
     GSD_CHECK(false, s);
     return GSD_OK;

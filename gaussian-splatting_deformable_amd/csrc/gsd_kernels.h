@@ -303,6 +303,58 @@ int relu_bwd_bias_blocks(long long P, int rows);
 void launch_relu_bwd_bias(long long P, int N, int bf16, const void* gy, const void* y, void* g, float* part,
                           int rows, hipStream_t s);
 
+// the deformation network's f32-accurate training path (gsd_mlp_train.hip)
+// A layer's weight as the reference stores it: up to 4 row pieces (the four heads) of ldw columns each; `map` names
+// the padded input layout: 0 identity, 1 layer 0 [enc(x) 63 | 0 | enc(t) 21 | 0 x 11], 2 layer 5 [enc(x) 63 | 0 | h 256]
+struct MlpWeightRef {
+    float* W[4];
+    int row_off[5];      // piece i holds rows [row_off[i], row_off[i + 1])
+    int n_pieces, ldw, map;
+};
+struct MlpPackParams {
+    MlpWeightRef w;
+    int M, K;              // packed A is M x K (multiples of 32 / 16); forward A = W, backward A = W^T
+    int transpose;
+    void* out;             // (K / 16) x (M / 32) x 3 x 64 fragments of 16 B
+};
+enum { kMlpFwdRelu = 0, kMlpFwdHeads = 1, kMlpBwdMask = 2 };
+struct MlpGemmParams {
+    int P, ldp;                     // Gaussians; row stride of the feature-major matrices (P rounded up to 256)
+    const float* src0;              // X^T rows 0 .. 16 ks0 - 1: [16 ks0][ldp]
+    int ks0;
+    const float* src1;              // the rest: [16 ks1][ldp] (the concatenated inputs of layers 0 and 5)
+    int ks1;
+    const void* frags;              // k_mlp_pack output: [ks][rb][split][lane]
+    int rb;                         // output row blocks of 32
+    const float* bias;              // forward: 32 rb floats
+    float* dst;                     // forward hidden: [32 rb][ldp]; heads: (P, n_out) row-major; backward: g rows
+    int n_out;                      // heads: outputs written (58)
+    int n_a;                        // backward: rows below n_a go to dst_a (the encoding's gradient, no ReLU)
+    float* dst_a;
+    int accumulate_a;
+    const float* mask;              // backward: h of the rows >= n_a ([rows - n_a][ldp]); NULL: those rows dropped
+};
+struct MlpWgradParams {
+    int P, ldp;
+    const float* G;                 // [32 n_rb][ldp]
+    int n_rb;
+    const float* X0;                // [32 k_rb0][ldp], then X1: [32 (k_rb - k_rb0)][ldp]
+    const float* X1;
+    int k_rb, k_rb0;
+    int tiles_n, tiles_k;           // 128 x 128 output tiles
+    int chunk;                      // Gaussians per wave (multiple of 16)
+    float* partial;                 // [chunks][32 n_rb][32 k_rb]
+    float* bias_partial;            // [chunks][32 n_rb]
+};
+void launch_mlp_pack(const MlpPackParams& p, hipStream_t s);
+void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E, float* ET, hipStream_t s);
+void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, float* dx, int accumulate, hipStream_t s);
+void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s);
+// dW scattered into the reference-shaped weight pieces (dst.W; map/rows as the forward weight), db into dst_b
+void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s);
+void launch_mlp_rows_to_features(int P, int ldp, int n, const float* src, float* dst, int dst_rows, hipStream_t s);
+void launch_mlp_gather_bias(const MlpWeightRef& b, float* dst, int n_pad, hipStream_t s);
+
 constexpr int kAdamMaxGroups = 16;
 struct AdamArgs {
     long long n;                        // elements in the slabs

@@ -1,0 +1,379 @@
+// gsd_mlp_train.hip -- the deformation network's TRAINING path (DirectTemporalNeRF, scene/gaussian_model.py:242-316,
+// positional encoding :33-82) at float32 accuracy on the bf16 matrix cores.
+//
+// The reference trains the network in float32 with autograd (torch GEMMs).  gfx950 has no TF32/xf32 and its f32
+// MFMA runs at the f32 vector rate (157 TF), 1/16 of bf16.  Every f32 operand here is split into three bf16 terms,
+// a = hi + mid + lo (hi = bf16(a), mid = bf16(a - hi), lo = bf16(a - hi - mid): 24 bits of mantissa, the f32 value
+// to 2^-25), and a product a.b is formed from the six leading partial products hi.hi + hi.mid + mid.hi + hi.lo +
+// mid.mid + lo.hi (the three dropped ones are below 2^-24 of |a b|, under f32's own rounding), each exact in the f32
+// accumulator of v_mfma_f32_32x32x16_bf16: "BF16x6".  Six bf16 MFMAs cost 6/16 of the f32 MFMA time for the same
+// product, so the f32-accurate GEMMs run on a 2.67x higher roof (419 TF).
+//
+// Layout.  Activations live FEATURE-MAJOR in HBM, [feature][ldp] (ldp = P rounded up to 256): the forward writes
+// every layer's post-ReLU output h_l (the backward's ReLU masks and weight-gradient operands), the backward writes
+// the pre-activation gradients g_l.  The MFMA operand maps then need no transposes:
+//   k_mlp_gemm   Y^T = A . X^T for a tile of 256 Gaussians (4 waves x 2 column blocks of 32): A = the layer's
+//                weights W (forward) or W^T (backward), pre-split and packed fragment-major by k_mlp_pack; X^T loaded
+//                straight from the feature-major activations (lane (h, c): features 16 ks + 8 h + j of Gaussian c,
+//                each load a coalesced 128-B row segment per half-wave) and split in registers.  Epilogues: bias +
+//                ReLU -> h_l (forward), bias -> the heads' (P, 58) outputs, or the ReLU mask of h_l -> g_l and the
+//                encoding's gradient rows (backward).
+//   k_mlp_wgrad  dW = g . X^T over the Gaussians: both operands feature-major, so lane (h, c) reads 8 consecutive
+//                Gaussians of one feature row (32 B); split-K over Gaussian chunks into per-wave partials, plus the
+//                bias gradient's row sums of g; k_mlp_wgrad_reduce sums the partials in a fixed order.
+//   k_mlp_encode / k_mlp_encode_bwd   enc(x), enc(t) feature-major; dL/dx from dL/d enc(x) through the stored
+//                sin / cos (d sin(2^i x) = 2^i cos(2^i x) dx: no trig in the backward).
+#include "gsd_kernels.h"
+
+namespace gsd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ---- the three-term split ----
+struct Split8 {
+    bf16x8 hi, mid, lo;
+};
+__device__ __forceinline__ Split8 split8(const float (&v)[8]) {
+    Split8 s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 h = (__bf16)v[j];
+        const float r1 = v[j] - (float)h;   // exact: v and h share their leading bits
+        const __bf16 m = (__bf16)r1;
+        const float r2 = r1 - (float)m;     // exact
+        s.hi[j] = h;
+        s.mid[j] = m;
+        s.lo[j] = (__bf16)r2;
+    }
+    return s;
+}
+
+// acc += A . B to f32 accuracy from the splits (the six leading products, smallest first)
+__device__ __forceinline__ f32x16 mfma_x6(const Split8& a, const Split8& b, f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, acc, 0, 0, 0);
+    return acc;
+}
+
+// ---- weights: the reference's pieces, the padded input layout ----
+__device__ __forceinline__ int mlp_col(int map, int k) {
+    if (map == 1) return k < 63 ? k : (k == 63 ? -1 : (k < 85 ? k - 1 : -1));
+    if (map == 2) return k < 63 ? k : (k == 63 ? -1 : k - 1);
+    return k;
+}
+// pointer to element (row, col) of the piece holding `row`, or null past the rows
+__device__ __forceinline__ float* mlp_elem(const MlpWeightRef& w, int row, int col) {
+    if (row < 0 || col < 0 || row >= w.row_off[w.n_pieces]) return nullptr;
+    int i = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q) i += (q < w.n_pieces && row >= w.row_off[q]) ? 1 : 0;
+    return w.W[i] + (size_t)(row - w.row_off[i]) * w.ldw + col;
+}
+
+// ---- weight packing: A[m][k] of a layer (W or W^T, zero-padded, input columns mapped) into split fragments ----
+// out[((ks * RB + rb) * 3 + s) * 64 + lane] = split s of A[32 rb + (lane & 31)][16 ks + 8 (lane >> 5) + 0..7]
+__global__ __launch_bounds__(256) void k_mlp_pack(MlpPackParams p) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int RB = p.M / 32, KS = p.K / 16;
+    if (t >= KS * RB * 64) return;
+    const int lane = t & 63, rb = (t >> 6) % RB, ks = (t >> 6) / RB;
+    const int m = 32 * rb + (lane & 31);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 16 * ks + 8 * (lane >> 5) + j;
+        // forward: A = W, rows m = output features, columns k = (padded) input features; backward: A = W^T
+        const float* e = p.transpose ? mlp_elem(p.w, k, mlp_col(p.w.map, m)) : mlp_elem(p.w, m, mlp_col(p.w.map, k));
+        v[j] = e ? *e : 0.f;
+    }
+    const Split8 s = split8(v);
+    bf16x8* o = reinterpret_cast<bf16x8*>(p.out) + (size_t)((ks * RB + rb) * 3) * 64 + lane;
+    o[0] = s.hi;
+    o[64] = s.mid;
+    o[128] = s.lo;
+}
+
+// the heads' four biases (or any pieces) gathered into one padded vector
+__global__ void k_mlp_gather_bias(MlpWeightRef b, float* __restrict__ dst, int n_pad) {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n >= n_pad) return;
+    const float* e = mlp_elem(b, n, 0);
+    dst[n] = e ? *e : 0.f;
+}
+
+// (P, n) row-major -> [dst_rows][ldp] feature-major (rows past n zero): the heads' incoming gradient
+__global__ __launch_bounds__(256) void k_mlp_rows_to_features(int P, int ldp, int n, const float* __restrict__ src,
+                                                              float* __restrict__ dst, int dst_rows) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= ldp) return;
+#pragma unroll 1
+    for (int r = 0; r < dst_rows; ++r) dst[(size_t)r * ldp + g] = (g < P && r < n) ? src[(size_t)g * n + r] : 0.f;
+}
+
+// ---- the positional encoding (gaussian_model.py:33-82), feature-major ----
+// E rows: 0-2 x, then per frequency i the sin of the 3 coordinates and their cos (3 + 6 i + 3 s + d), 63 = 0;
+// ET rows: 0 t, 1 + 2 i sin(2^i t), 2 + 2 i cos(2^i t), 21-31 = 0.
+__global__ __launch_bounds__(256) void k_mlp_encode(int P, int ldp, const float* __restrict__ x,
+                                                    const float* __restrict__ t, float* __restrict__ E,
+                                                    float* __restrict__ ET) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= ldp) return;
+    const bool in = g < P;
+    const float v[3] = {in ? x[3 * g] : 0.f, in ? x[3 * g + 1] : 0.f, in ? x[3 * g + 2] : 0.f};
+    const float tv = in ? t[g] : 0.f;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) E[(size_t)d * ldp + g] = v[d];
+#pragma unroll 1
+    for (int i = 0; i < 10; ++i) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float a = ldexpf(v[d], i);   // x * 2^i, exact as torch's x * freqs
+            E[(size_t)(3 + 6 * i + d) * ldp + g] = sinf(a);
+            E[(size_t)(6 + 6 * i + d) * ldp + g] = cosf(a);
+        }
+        const float a = ldexpf(tv, i);
+        ET[(size_t)(1 + 2 * i) * ldp + g] = sinf(a);
+        ET[(size_t)(2 + 2 * i) * ldp + g] = cosf(a);
+    }
+    E[(size_t)63 * ldp + g] = 0.f;
+    ET[g] = tv;
+#pragma unroll 1
+    for (int r = 21; r < 32; ++r) ET[(size_t)r * ldp + g] = 0.f;
+}
+
+// dL/dx = dL/dE[identity rows] + sum_i 2^i (dL/dsin_i cos_i - dL/dcos_i sin_i), the sin / cos read back from E
+__global__ __launch_bounds__(256) void k_mlp_encode_bwd(int P, int ldp, const float* __restrict__ E,
+                                                        const float* __restrict__ dE, float* __restrict__ dx,
+                                                        int accumulate) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= P) return;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float s = dE[(size_t)d * ldp + g];
+#pragma unroll 1
+        for (int i = 0; i < 10; ++i) {
+            const size_t rs = (size_t)(3 + 6 * i + d) * ldp + g, rc = (size_t)(6 + 6 * i + d) * ldp + g;
+            s += ldexpf(dE[rs] * E[rc] - dE[rc] * E[rs], i);
+        }
+        dx[3 * g + d] = accumulate ? dx[3 * g + d] + s : s;
+    }
+}
+
+// ---- Y^T = A X^T over a 256-Gaussian tile, kRbg row blocks of 32 per workgroup (grid.y) ----
+constexpr int kGemmRbg = 4;
+
+__device__ __forceinline__ void load_x8(const MlpGemmParams& p, int ks, int h, int g, float (&v)[8]) {
+    const float* src = ks < p.ks0 ? p.src0 + (size_t)(16 * ks + 8 * h) * p.ldp
+                                  : p.src1 + (size_t)(16 * (ks - p.ks0) + 8 * h) * p.ldp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = src[(size_t)j * p.ldp + g];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_gemm(MlpGemmParams p) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
+    const int wave = threadIdx.x >> 6;
+    const int g0 = blockIdx.x * 256 + wave * 64 + c;   // column block cb: Gaussian g0 + 32 cb (always < ldp)
+    const int rb0 = blockIdx.y * kGemmRbg;
+    const int nrb = min(kGemmRbg, p.rb - rb0);         // workgroup-uniform
+    const int KS = p.ks0 + p.ks1;
+    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags) + lane;
+    f32x16 acc[kGemmRbg][2];
+#pragma unroll
+    for (int r = 0; r < kGemmRbg; ++r) acc[r][0] = acc[r][1] = f32x16{};
+    float xn[2][8];
+    load_x8(p, 0, h, g0, xn[0]);
+    load_x8(p, 0, h, g0 + 32, xn[1]);
+    for (int ks = 0; ks < KS; ++ks) {
+        const Split8 b0 = split8(xn[0]), b1 = split8(xn[1]);
+        if (ks + 1 < KS) {   // the next k-step's activations in flight while this one's MFMAs run
+            load_x8(p, ks + 1, h, g0, xn[0]);
+            load_x8(p, ks + 1, h, g0 + 32, xn[1]);
+        }
+#pragma unroll
+        for (int r = 0; r < kGemmRbg; ++r) {
+            if (r >= nrb) break;
+            const bf16x8* f = F + (size_t)((ks * p.rb + rb0 + r) * 3) * 64;
+            Split8 a;
+            a.hi = f[0];
+            a.mid = f[64];
+            a.lo = f[128];
+            acc[r][0] = mfma_x6(a, b0, acc[r][0]);
+            acc[r][1] = mfma_x6(a, b1, acc[r][1]);
+        }
+    }
+    // accumulator register q of row block r: row n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian
+#pragma unroll
+    for (int r = 0; r < kGemmRbg; ++r) {
+        if (r >= nrb) break;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            const int g = g0 + 32 * cb;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int n = 32 * (rb0 + r) + 8 * (q >> 2) + 4 * h + (q & 3);
+                const float a = acc[r][cb][q];
+                if (MODE == kMlpFwdRelu) {
+                    p.dst[(size_t)n * p.ldp + g] = fmaxf(a + p.bias[n], 0.f);
+                } else if (MODE == kMlpFwdHeads) {
+                    if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + p.bias[n];
+                } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
+                    if (n < p.n_a) {
+                        float* d = p.dst_a + (size_t)n * p.ldp + g;
+                        *d = p.accumulate_a ? *d + a : a;
+                    } else if (p.mask) {
+                        const size_t o = (size_t)(n - p.n_a) * p.ldp + g;
+                        p.dst[o] = p.mask[o] > 0.f ? a : 0.f;   // threshold_backward(g, h, 0)
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
+// One wave per (chunk, 128 x 128 output tile): 4 x 4 blocks of 32 x 32, 96 MFMAs per 16-Gaussian step.
+constexpr int kWgTile = 4;
+
+__device__ __forceinline__ void load_rows8(const float* __restrict__ row, int pbase, int P, float (&v)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(row + pbase);
+    const float4 b = *reinterpret_cast<const float4*>(row + pbase + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (pbase + j >= P) v[j] = 0.f;   // Gaussians past P hold whatever the tail columns hold
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_wgrad(MlpWgradParams p) {
+    const int lane = threadIdx.x, h = lane >> 5, c = lane & 31;
+    const int chunk = blockIdx.x;
+    const int tn = blockIdx.y / p.tiles_k, tk = blockIdx.y % p.tiles_k;
+    const int nb = min(kWgTile, p.n_rb - kWgTile * tn), kb = min(kWgTile, p.k_rb - kWgTile * tk);
+    const int p_lo = chunk * p.chunk, p_hi = min(p.P, p_lo + p.chunk);
+    f32x16 acc[kWgTile][kWgTile];
+#pragma unroll
+    for (int i = 0; i < kWgTile; ++i)
+#pragma unroll
+        for (int j = 0; j < kWgTile; ++j) acc[i][j] = f32x16{};
+    float bsum[kWgTile] = {0.f, 0.f, 0.f, 0.f};
+    const float* grow[kWgTile];
+    const float* xrow[kWgTile];
+#pragma unroll
+    for (int i = 0; i < kWgTile; ++i) {
+        const int n = 32 * (kWgTile * tn + min(i, nb - 1)) + c;
+        grow[i] = p.G + (size_t)n * p.ldp;
+        const int k = 32 * (kWgTile * tk + min(i, kb - 1)) + c;
+        xrow[i] = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
+    }
+    for (int pb = p_lo; pb < p_hi; pb += 16) {
+        const int pbase = pb + 8 * h;
+        Split8 a[kWgTile], b[kWgTile];
+#pragma unroll
+        for (int i = 0; i < kWgTile; ++i) {
+            float v[8];
+            load_rows8(grow[i], pbase, p_hi, v);
+            if (tk == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum[i] += v[j];
+            }
+            a[i] = split8(v);
+            load_rows8(xrow[i], pbase, p_hi, v);
+            b[i] = split8(v);
+        }
+#pragma unroll
+        for (int i = 0; i < kWgTile; ++i) {
+            if (i >= nb) break;
+#pragma unroll
+            for (int j = 0; j < kWgTile; ++j) {
+                if (j >= kb) break;
+                acc[i][j] = mfma_x6(a[i], b[j], acc[i][j]);
+            }
+        }
+    }
+    // partial[chunk][n][k], n = 32 (4 tn + i) + 8 (q >> 2) + 4 h + (q & 3), k = 32 (4 tk + j) + c
+    float* out = p.partial + (size_t)chunk * (32 * p.n_rb) * (32 * p.k_rb);
+#pragma unroll
+    for (int i = 0; i < kWgTile; ++i) {
+        if (i >= nb) break;
+#pragma unroll
+        for (int j = 0; j < kWgTile; ++j) {
+            if (j >= kb) break;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int n = 32 * (kWgTile * tn + i) + 8 * (q >> 2) + 4 * h + (q & 3);
+                const int k = 32 * (kWgTile * tk + j) + c;
+                out[(size_t)n * (32 * p.k_rb) + k] = acc[i][j][q];
+            }
+        }
+    }
+    if (tk == 0) {   // the bias gradient: this lane's row (n = 32 (4 tn + i) + c) over its half's Gaussians
+#pragma unroll
+        for (int i = 0; i < kWgTile; ++i) {
+            if (i >= nb) break;
+            const float s = bsum[i] + __shfl_xor(bsum[i], 32);
+            if (h == 0) p.bias_partial[(size_t)chunk * (32 * p.n_rb) + 32 * (kWgTile * tn + i) + c] = s;
+        }
+    }
+}
+
+// dW[n][k] = sum over the chunks of partial[chunk][n][k], in chunk order (deterministic), scattered into the
+// reference-shaped pieces (padded columns and rows dropped); the bias gradient likewise (k_cols = 1)
+__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_rows, int k_cols,
+                                                          const float* __restrict__ partial, MlpWeightRef dst) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long n_el = (long long)n_rows * k_cols;
+    if (e >= n_el) return;
+    const int n = (int)(e / k_cols), k = (int)(e - (long long)n * k_cols);
+    float* d = mlp_elem(dst, n, mlp_col(dst.map, k));
+    if (!d) return;
+    float s = 0.f;
+    for (int c = 0; c < n_chunks; ++c) s += partial[(size_t)c * n_el + e];
+    *d = s;
+}
+
+void launch_mlp_pack(const MlpPackParams& p, hipStream_t s) {
+    const int n = (p.K / 16) * (p.M / 32) * 64;
+    hipLaunchKernelGGL(k_mlp_pack, dim3((n + 255) / 256), dim3(256), 0, s, p);
+}
+
+void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E, float* ET, hipStream_t s) {
+    hipLaunchKernelGGL(k_mlp_encode, dim3((ldp + 255) / 256), dim3(256), 0, s, P, ldp, x, t, E, ET);
+}
+
+void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, float* dx, int accumulate, hipStream_t s) {
+    if (P > 0) hipLaunchKernelGGL(k_mlp_encode_bwd, dim3((P + 255) / 256), dim3(256), 0, s, P, ldp, E, dE, dx, accumulate);
+}
+
+void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s) {
+    const dim3 grid(p.ldp / 256, (p.rb + kGemmRbg - 1) / kGemmRbg);
+    if (mode == kMlpFwdRelu) hipLaunchKernelGGL(k_mlp_gemm<kMlpFwdRelu>, grid, dim3(256), 0, s, p);
+    else if (mode == kMlpFwdHeads) hipLaunchKernelGGL(k_mlp_gemm<kMlpFwdHeads>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_mlp_gemm<kMlpBwdMask>, grid, dim3(256), 0, s, p);
+}
+
+void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s) {
+    const int n_chunks = (p.P + p.chunk - 1) / p.chunk;
+    const dim3 grid(n_chunks, p.tiles_n * p.tiles_k);
+    hipLaunchKernelGGL(k_mlp_wgrad, grid, dim3(64), 0, s, p);
+    const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
+    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
+                       32 * p.k_rb, (const float*)p.partial, dst);
+    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 255) / 256), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1,
+                       (const float*)p.bias_partial, dst_b);
+}
+
+void launch_mlp_rows_to_features(int P, int ldp, int n, const float* src, float* dst, int dst_rows, hipStream_t s) {
+    hipLaunchKernelGGL(k_mlp_rows_to_features, dim3(ldp / 256), dim3(256), 0, s, P, ldp, n, src, dst, dst_rows);
+}
+
+void launch_mlp_gather_bias(const MlpWeightRef& b, float* dst, int n_pad, hipStream_t s) {
+    hipLaunchKernelGGL(k_mlp_gather_bias, dim3((n_pad + 255) / 256), dim3(256), 0, s, b, dst, n_pad);
+}
+
+}  // namespace gsd

@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -103,6 +103,10 @@ SIGNATURES = {
     "gsd_deform_mlp_forward_bf16": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsd_relu_backward_bias_blocks": (_i32, [_i64, _i32]),
     "gsd_relu_backward_bias": (_i32, [_i64, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "gsd_deform_mlp_train_workspace_bytes": (_sz, [_i64]),
+    "gsd_deform_mlp_train_forward": (_i32, [_i64, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp, _vp]),
+    "gsd_deform_mlp_train_backward": (_i32, [_i64, _vp, ctypes.POINTER(_vp), _vp, _vp, ctypes.POINTER(_vp),
+                                             ctypes.POINTER(_vp), _vp]),
     "gsd_timing_enable": (_i32, [_i32]),
     "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "gsd_timing_reset": (None, []),

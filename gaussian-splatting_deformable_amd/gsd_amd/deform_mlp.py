@@ -10,9 +10,11 @@ parameter names and shapes (``_time.{0..7}``, ``_time_out``, ``_time_out_scale``
 weights_only=True)``).  Its output plugs into ``render()`` as ``pc.offset_model`` and reaches the fused
 preamble / split-SH rasterizer directly.
 
-The ≈511k multiply-adds per Gaussian are plain GEMMs, so they go to hipBLASLt through torch.matmul (f32 by
-default, like the reference; ``dtype=torch.bfloat16`` runs the hidden layers in bf16 on the MFMA cores with
-f32 accumulation).  The encoding is one fused elementwise HIP-friendly torch expression.
+The ≈511k multiply-adds per Gaussian are GEMMs.  In float32 (the reference's training precision) on a HIP device
+they run on the hand-written training path (gsd_mlp_train.hip): forward and backward, each GEMM on the bf16
+matrix cores with its f32 operands split into three bf16 terms (BF16x6, f32-level accuracy).  ``dtype=
+torch.bfloat16`` keeps autocast semantics: the fused bf16 forward kernel without autograd (gsd_mlp.hip), torch /
+hipBLASLt GEMMs with autograd.  GSD_MLP_TORCH=1 forces the torch path (the reference's structure, f32 GEMMs).
 """
 from __future__ import annotations
 
@@ -168,6 +170,70 @@ def _fused_forward(net: "DirectTemporalNeRF", x: torch.Tensor, ts: torch.Tensor)
     return outs
 
 
+# ---- the f32-accurate training path (gsd_mlp_train.hip via gsd_deform_mlp_train_forward / _backward) ----
+def _param_list(net: "DirectTemporalNeRF"):
+    """The reference's 12 weights and 12 biases in the C-ABI's order (_time.0-7, _time_out, _scale, _rot, _shs)."""
+    mods = list(net._time) + [net._time_out, net._time_out_scale, net._time_out_rot, net._time_out_shs]
+    return [m.weight for m in mods], [m.bias for m in mods]
+
+
+def _ptr_array(ts):
+    import ctypes
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+class _MLPTrainF32(torch.autograd.Function):
+    """DirectTemporalNeRF forward + backward as the reference trains it (float32 with autograd), each GEMM on the
+    bf16 matrix cores with the operands split into three bf16 terms (BF16x6, f32-level accuracy): three HIP
+    kernels per layer direction instead of torch's GEMMs, every activation kept feature-major in one workspace."""
+
+    @staticmethod
+    def forward(ctx, x, t, *params):
+        from . import _native
+        from ._C import _ptr, _stream
+        lib = _native.load()
+        P = int(x.shape[0])
+        dev = x.device
+        ws_, bs_ = list(params[:12]), list(params[12:])
+        wc = [w.detach().contiguous() for w in ws_]
+        bc = [b.detach().contiguous() for b in bs_]
+        if any(w.dtype != torch.float32 or w.device != dev for w in wc + bc):
+            raise RuntimeError("deform_mlp: the f32 training path needs float32 parameters on the input's device")
+        xc = x.detach().to(torch.float32).contiguous()
+        tc = t.detach().to(torch.float32).reshape(-1).expand(P).contiguous()
+        ws = torch.empty(lib.gsd_deform_mlp_train_workspace_bytes(P), dtype=torch.uint8, device=dev)
+        out = torch.empty(P, 58, dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_deform_mlp_train_forward(P, _ptr(xc), _ptr(tc), _ptr_array(wc), _ptr_array(bc),
+                                                           _ptr(ws), _ptr(out), _stream(dev)))
+        ctx.ws, ctx.wc, ctx.P = ws, wc, P
+        ctx.shapes = [w.shape for w in wc] + [b.shape for b in bc]
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        from . import _native
+        from ._C import _ptr, _stream
+        lib = _native.load()
+        P, dev = ctx.P, ctx.ws.device
+        g = gout.detach().to(torch.float32).contiguous()
+        dx = torch.empty(P, 3, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        dW = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in ctx.shapes[:12]]
+        db = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in ctx.shapes[12:]]
+        with torch.cuda.device(dev):
+            _native.check(lib.gsd_deform_mlp_train_backward(P, _ptr(g), _ptr_array(ctx.wc), _ptr(ctx.ws),
+                                                            None if dx is None else _ptr(dx), _ptr_array(dW),
+                                                            _ptr_array(db), _stream(dev)))
+        ctx.ws = None
+        return (dx, None, *dW, *db)
+
+
+def _train_forward(net: "DirectTemporalNeRF", x: torch.Tensor, ts: torch.Tensor):
+    ws, bs = _param_list(net)
+    out = _MLPTrainF32.apply(x, ts, *ws, *bs)
+    return tuple(o.contiguous() for o in out.split([3, 3, 4, 48], dim=-1))
+
+
 def positional_encoding(x: torch.Tensor, n_freqs: int = 10) -> torch.Tensor:
     """[x, sin(x 2^0), cos(x 2^0), ..., sin(x 2^(n-1)), cos(x 2^(n-1))] (gaussian_model.py:33-82, log sampling)."""
     freqs = 2.0 ** torch.linspace(0.0, n_freqs - 1, steps=n_freqs, device=x.device)
@@ -194,6 +260,15 @@ class DirectTemporalNeRF(nn.Module):
         self._time_out_rot = nn.Linear(W, 4)
         self._time_out_shs = nn.Linear(W, 48)
 
+    def _reference_arch(self) -> bool:
+        return (self.D, self.W, self.n_freqs, self.skips) == (8, 256, 10, (4,))
+
+    def _use_train_f32(self, x: torch.Tensor) -> bool:
+        """The f32 network on a HIP device (the reference's training precision) runs the hand-written training
+        path (gsd_mlp_train.hip: BF16x6 on the matrix cores, forward and backward); GSD_MLP_TORCH=1 keeps torch."""
+        return (self.compute_dtype == torch.float32 and x.device.type == "cuda" and self._reference_arch()
+                and not os.environ.get("GSD_MLP_TORCH") and all(p.dtype == torch.float32 for p in self.parameters()))
+
     def _use_fused(self, x: torch.Tensor) -> bool:
         """The fused bf16 kernel (gsd_mlp.hip) serves the bf16 evaluation without autograd on a HIP device, for
         the reference architecture (8 x 256, skip after layer 4, 10 frequencies); GSD_MLP_TORCH=1 keeps torch."""
@@ -211,6 +286,8 @@ class DirectTemporalNeRF(nn.Module):
             return z(P, 3), z(P, 3), z(P, 4), z(P, 48)
         if self._use_fused(x):
             return _fused_forward(self, x, ts)
+        if self._use_train_f32(x):
+            return _train_forward(self, x, ts)
         ex = positional_encoding(x, self.n_freqs)
         et = positional_encoding(ts, self.n_freqs)
         dt = self.compute_dtype if self.compute_dtype != torch.float32 else ex.dtype  # f32: the input's own

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 12
+#define GSD_ABI_VERSION 13
 
 enum {
     GSD_OK = 0,
@@ -358,6 +358,25 @@ int gsd_deform_mlp_forward_bf16(int32_t P, const float* x, const float* t, const
 int32_t gsd_relu_backward_bias_blocks(int64_t P, int32_t rows_per_block);
 int gsd_relu_backward_bias(int64_t P, int32_t N, int32_t bf16, const void* grad_out, const void* out, void* grad_in,
                            float* bias_partial, int32_t rows_per_block, void* stream);
+
+/* The deformation network's TRAINING path at float32 accuracy (ABI 13; gsd_mlp_train.hip): DirectTemporalNeRF
+ * (scene/gaussian_model.py:242-316, positional encoding :33-82) forward and backward as the reference trains it
+ * (float32, autograd), on the bf16 matrix cores with every f32 operand split into three bf16 terms and the six
+ * leading partial products accumulated in f32 ("BF16x6": f32-level accuracy; gfx950 has no TF32 and its f32 MFMA
+ * runs at 1/16 of the bf16 rate).  weights[12] / biases[12]: device float32, the reference's parameters in order
+ * _time.0 .. _time.7, _time_out, _time_out_scale, _time_out_rot, _time_out_shs (shapes (256,84), (256,256) x 4,
+ * (256,319), (256,256) x 2, (3,256), (3,256), (4,256), (48,256) and their biases).  x (P,3), t (P) float32.
+ * out (P,58) = [dx 3 | d log-scale 3 | d quaternion 4 | dSH 48] row-major.  workspace:
+ * gsd_deform_mlp_train_workspace_bytes(P) bytes; the forward leaves in it what the backward of the same call
+ * reads (the encoding and every hidden activation, feature-major: ~10.6 KB per Gaussian).  Replaces the module's
+ * forward + autograd backward (torch GEMMs). */
+size_t gsd_deform_mlp_train_workspace_bytes(int64_t P);
+int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, const float* const* weights,
+                                 const float* const* biases, void* workspace, float* out, void* stream);
+/* Backward: grad_out (P,58) = dL/d out.  Writes dL/dx (P,3) when dx != NULL and every weight / bias gradient
+ * (d_weights[12], d_biases[12], the parameters' shapes; stored, not accumulated).  weights: the forward's. */
+int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float* const* weights, void* workspace,
+                                  float* dx, float* const* d_weights, float* const* d_biases, void* stream);
 
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead

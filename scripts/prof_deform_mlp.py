@@ -43,6 +43,7 @@ def main():
     x = (torch.rand(a.P, 3, generator=g) * 2 - 1).to(dev)
     t = torch.full((a.P, 1), 0.3, device=dev)
     peaks = {torch.float32: 157.3, torch.bfloat16: 2516.6}
+    xg = x.clone().requires_grad_(True)   # the reference feeds the trained means (dL/dx computed)
     for dt in (torch.float32, torch.bfloat16):
         net = DirectTemporalNeRF(dtype=dt).to(dev)
         fpg = flops_per_gaussian(net)
@@ -52,8 +53,16 @@ def main():
                 net(x, t, 10_000)
 
         def fwd_bwd():
-            outs = net(x, t, 10_000)
+            outs = net(xg, t, 10_000)
             sum(o.float().sum() for o in outs).backward()
+
+        if dt == torch.float32:   # the HIP training path (BF16x6) vs torch's f32 GEMMs (GSD_MLP_TORCH=1)
+            os.environ["GSD_MLP_TORCH"] = "1"
+            for _ in range(2):
+                fwd_bwd()
+            tf_ms, tfb_ms = median_ms(fwd, a.iters), median_ms(fwd_bwd, a.iters)
+            del os.environ["GSD_MLP_TORCH"]
+            print("float32   P=%d  torch f32 GEMMs: fwd %.3f ms  fwd+bwd %.3f ms" % (a.P, tf_ms, tfb_ms), flush=True)
 
         for _ in range(3):
             fwd_bwd()
@@ -71,6 +80,9 @@ def main():
         print("%-9s P=%d  fwd %.3f ms (%.1f TFLOP/s, %.1f %% of %.0f)  fwd+bwd %.3f ms (%.1f TFLOP/s, %.1f %%)"
               % (str(dt).replace("torch.", ""), a.P, f_ms, f_tf, 100 * f_tf / peaks[dt], peaks[dt], fb_ms, fb_tf,
                  100 * fb_tf / peaks[dt]), flush=True)
+        if dt == torch.float32:   # BF16x6: six bf16 MFMAs per f32 product -> the f32-accurate roof is 2516.6 / 6
+            print("          HIP f32 path vs its BF16x6 roof (419.4 TFLOP/s): fwd %.1f %%  fwd+bwd %.1f %%"
+                  % (100 * f_tf / 419.4, 100 * fb_tf / 419.4), flush=True)
 
 
 if __name__ == "__main__":

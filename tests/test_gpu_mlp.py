@@ -1,6 +1,12 @@
-"""The fused deformation-network forward (gsd_mlp.hip, gsd_deform_mlp_forward_bf16) on the GPU against the
-module's torch bf16 path (the same rounding points, hipBLASLt's accumulation order), its float32 forward, and the
-lane-level CPU emulation of the kernel (tests/test_deform_mlp.py).  P off the 32- and 128-Gaussian grains."""
+"""The deformation network on the GPU.
+
+- The fused bf16 forward (gsd_mlp.hip, gsd_deform_mlp_forward_bf16) against the module's torch bf16 path (the same
+  rounding points, hipBLASLt's accumulation order: 2 % of the output scale), the float32 forward (4 %: bf16's own
+  error) and the lane-level CPU emulation of the kernel (tests/test_deform_mlp.py).
+- The float32 training path (gsd_mlp_train.hip, gsd_deform_mlp_train_forward / _backward: BF16x6 GEMMs) against the
+  float64 restatement oracle/deform_mlp_ref.py and its autograd: outputs and every gradient within 2e-5 of each
+  tensor's scale (f32-level), and against torch's own f32 GEMMs within 1e-5.
+P off the 32-, 128- and 256-Gaussian grains."""
 from __future__ import annotations
 
 import os
@@ -153,3 +159,85 @@ def test_fused_mlp_repacks_after_fused_adam_step():
         fresh = torch.cat(net(x, t, 5000), -1)
     assert not torch.equal(after, before)
     assert torch.equal(after, fresh)
+
+
+def _launched(fn):
+    """Run fn with the library's kernel timing on; the names of the C-ABI kernels it launched."""
+    import ctypes
+
+    from gsd_amd import _native
+    lib = _native.load()
+    lib.gsd_timing_enable(1)
+    lib.gsd_timing_reset()
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        buf = ctypes.create_string_buffer(32 * 64)
+        n = lib.gsd_timing_collect(64, buf, None, None)
+    finally:
+        lib.gsd_timing_enable(0)
+    return out, {buf.raw[32 * i: 32 * i + 32].split(b"\0")[0].decode() for i in range(n)}
+
+
+@pytest.mark.parametrize("P", [1, 77, 5003, 70_001])
+def test_train_f32_forward_and_backward_match_float64_oracle(P):
+    """The f32 training path (gsd_mlp_train.hip: BF16x6 GEMMs on the matrix cores, forward and backward) against
+    the float64 restatement of DirectTemporalNeRF (oracle/deform_mlp_ref.py) and its float64 autograd.  Bars
+    (f32-level, as torch's own f32 GEMMs meet them): outputs max |err| <= 2e-5 of the output scale; dL/dx and every
+    weight / bias gradient max |err| <= 2e-5 of that tensor's scale.  (The bf16 path is ~1e-2 off.)"""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    from oracle import deform_mlp_ref
+    torch.manual_seed(40 + P % 7)
+    net = DirectTemporalNeRF()
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(2.0)   # every layer's ReLU pattern matters
+    g = torch.Generator().manual_seed(P)
+    x = torch.rand(P, 3, generator=g) * 4 - 2
+    t = torch.full((P, 1), 0.35)
+    w = [torch.randn(P, n, generator=g) for n in (3, 3, 4, 48)]
+    netc = net.cuda()
+    xc = x.cuda().requires_grad_(True)
+    outs, names = _launched(lambda: netc(xc, t.cuda(), 5000))
+    assert "deform_mlp_train_fwd" in names   # the HIP path ran, not torch
+    _, names = _launched(lambda: sum((o * wi.cuda()).sum() for o, wi in zip(outs, w)).backward())
+    assert "deform_mlp_train_bwd" in names
+    sd = {k: v.detach().double().cpu().requires_grad_(True) for k, v in net.state_dict().items()}
+    x64 = x.double().requires_grad_(True)
+    ref = deform_mlp_ref.forward(sd, x64, t.double(), 5000)
+    sum((o * wi.double()).sum() for o, wi in zip(ref, w)).backward()
+    for o, r in zip(outs, ref):
+        scale = float(r.abs().max())
+        assert float((o.detach().cpu().double() - r.detach()).abs().max()) <= 2e-5 * scale
+    pairs = [("x", xc.grad, x64.grad)] + [(k, dict(netc.named_parameters())[k].grad, v.grad) for k, v in sd.items()]
+    for name, got, want in pairs:
+        assert got is not None, name
+        scale = max(float(want.abs().max()), 1e-30)
+        err = float((got.cpu().double() - want).abs().max())
+        assert err <= 2e-5 * scale, (name, err / scale)
+
+
+def test_train_f32_matches_torch_f32_path():
+    """The same network through the HIP training path and through torch's f32 GEMMs (GSD_MLP_TORCH=1): outputs
+    and gradients agree to f32 rounding (1e-5 of each tensor's scale)."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    torch.manual_seed(41)
+    net = DirectTemporalNeRF().cuda()
+    P = 20_000
+    x = (torch.rand(P, 3, device="cuda") * 2 - 1)
+    t = torch.full((P, 1), 0.2, device="cuda")
+    w = [torch.randn(P, n, device="cuda") for n in (3, 3, 4, 48)]
+    res = {}
+    for mode in ("hip", "torch"):
+        if mode == "torch":
+            os.environ["GSD_MLP_TORCH"] = "1"
+        try:
+            net.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_(True)
+            outs = net(xx, t, 5000)
+            sum((o * wi).sum() for o, wi in zip(outs, w)).backward()
+            res[mode] = [torch.cat(outs, -1).detach(), xx.grad] + [p.grad.clone() for p in net.parameters()]
+        finally:
+            os.environ.pop("GSD_MLP_TORCH", None)
+    for a, b in zip(res["hip"], res["torch"]):
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
