@@ -271,20 +271,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_
         const int k = 32 * (kWgTile * tk + min(i, kb - 1)) + c;
         xrow[i] = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
     }
+    // software pipeline: the next step's rows are loaded while this step's MFMAs run (one wave per SIMD)
+    float gv[kWgTile][8], xv[kWgTile][8];
+#pragma unroll
+    for (int i = 0; i < kWgTile; ++i) {
+        load_rows8(grow[i], p_lo + 8 * h, p_hi, gv[i]);
+        load_rows8(xrow[i], p_lo + 8 * h, p_hi, xv[i]);
+    }
     for (int pb = p_lo; pb < p_hi; pb += 16) {
-        const int pbase = pb + 8 * h;
         Split8 a[kWgTile], b[kWgTile];
 #pragma unroll
         for (int i = 0; i < kWgTile; ++i) {
-            float v[8];
-            load_rows8(grow[i], pbase, p_hi, v);
             if (tk == 0) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) bsum[i] += v[j];
+                for (int j = 0; j < 8; ++j) bsum[i] += gv[i][j];
             }
-            a[i] = split8(v);
-            load_rows8(xrow[i], pbase, p_hi, v);
-            b[i] = split8(v);
+            a[i] = split8(gv[i]);
+            b[i] = split8(xv[i]);
+        }
+        if (pb + 16 < p_hi) {
+#pragma unroll
+            for (int i = 0; i < kWgTile; ++i) {
+                load_rows8(grow[i], pb + 16 + 8 * h, p_hi, gv[i]);
+                load_rows8(xrow[i], pb + 16 + 8 * h, p_hi, xv[i]);
+            }
         }
 #pragma unroll
         for (int i = 0; i < kWgTile; ++i) {
