@@ -164,9 +164,11 @@ __global__ __launch_bounds__(256) void k_mlp_encode_bwd(int P, int ldp, const fl
     }
 }
 
-// ---- Y^T = A X^T over a 256-Gaussian tile, kRbg row blocks of 32 per workgroup (grid.y) ----
-constexpr int kGemmRbg = 4;
-
+// ---- Y^T = A X^T for a tile of 128 Gaussians and ALL of the layer's output rows ----
+// One wave per 32 Gaussians (the B operand's columns), the workgroup's four waves sharing each k-step's A
+// fragments (RB row blocks x 3 splits x 1 KB) through an LDS double buffer: the fragments of k-step ks + 1 are
+// fetched into registers while ks's MFMAs run and written to the other buffer behind them, one barrier per k-step.
+// Each activation is read from HBM once per layer (all rows in one workgroup) and its loads run two k-steps ahead.
 __device__ __forceinline__ void load_x8(const MlpGemmParams& p, int ks, int h, int g, float (&v)[8]) {
     const float* src = ks < p.ks0 ? p.src0 + (size_t)(16 * ks + 8 * h) * p.ldp
                                   : p.src1 + (size_t)(16 * (ks - p.ks0) + 8 * h) * p.ldp;
@@ -174,62 +176,71 @@ __device__ __forceinline__ void load_x8(const MlpGemmParams& p, int ks, int h, i
     for (int j = 0; j < 8; ++j) v[j] = src[(size_t)j * p.ldp + g];
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_gemm(MlpGemmParams p) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, c = lane & 31;
-    const int wave = threadIdx.x >> 6;
-    const int g0 = blockIdx.x * 256 + wave * 64 + c;   // column block cb: Gaussian g0 + 32 cb (always < ldp)
-    const int rb0 = blockIdx.y * kGemmRbg;
-    const int nrb = min(kGemmRbg, p.rb - rb0);         // workgroup-uniform
+template <int MODE, int RB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 : 2))) void k_mlp_gemm(MlpGemmParams p) {
+    constexpr int NF = RB * 3 * 64;               // 16-B fragments per k-step
+    constexpr int PER = (NF + 255) / 256;         // per thread
+    __shared__ bf16x8 s_a[2][NF];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
+    const int g = blockIdx.x * 128 + wave * 32 + c;   // always < ldp
     const int KS = p.ks0 + p.ks1;
-    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags) + lane;
-    f32x16 acc[kGemmRbg][2];
+    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags);
+    f32x16 acc[RB];
 #pragma unroll
-    for (int r = 0; r < kGemmRbg; ++r) acc[r][0] = acc[r][1] = f32x16{};
-    float xn[2][8];
-    load_x8(p, 0, h, g0, xn[0]);
-    load_x8(p, 0, h, g0 + 32, xn[1]);
+    for (int r = 0; r < RB; ++r) acc[r] = f32x16{};
+    bf16x8 stage[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+        if (tid + 256 * i < NF) s_a[0][tid + 256 * i] = F[tid + 256 * i];
+    float x0[8], x1[8];
+    load_x8(p, 0, h, g, x0);
+    if (KS > 1) load_x8(p, 1, h, g, x1);
+    __syncthreads();
     for (int ks = 0; ks < KS; ++ks) {
-        const Split8 b0 = split8(xn[0]), b1 = split8(xn[1]);
-        if (ks + 1 < KS) {   // the next k-step's activations in flight while this one's MFMAs run
-            load_x8(p, ks + 1, h, g0, xn[0]);
-            load_x8(p, ks + 1, h, g0 + 32, xn[1]);
-        }
+        const int buf = ks & 1;
+        if (ks + 1 < KS) {   // the next k-step's fragments into registers (written to LDS after the MFMAs)
+            const bf16x8* src = F + (size_t)(ks + 1) * NF;
 #pragma unroll
-        for (int r = 0; r < kGemmRbg; ++r) {
-            if (r >= nrb) break;
-            const bf16x8* f = F + (size_t)((ks * p.rb + rb0 + r) * 3) * 64;
+            for (int i = 0; i < PER; ++i)
+                if (tid + 256 * i < NF) stage[i] = src[tid + 256 * i];
+        }
+        const Split8 b = split8(x0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x0[j] = x1[j];
+        if (ks + 2 < KS) load_x8(p, ks + 2, h, g, x1);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
             Split8 a;
-            a.hi = f[0];
-            a.mid = f[64];
-            a.lo = f[128];
-            acc[r][0] = mfma_x6(a, b0, acc[r][0]);
-            acc[r][1] = mfma_x6(a, b1, acc[r][1]);
+            a.hi = s_a[buf][(r * 3) * 64 + lane];
+            a.mid = s_a[buf][(r * 3 + 1) * 64 + lane];
+            a.lo = s_a[buf][(r * 3 + 2) * 64 + lane];
+            acc[r] = mfma_x6(a, b, acc[r]);
         }
+        if (ks + 1 < KS) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i)
+                if (tid + 256 * i < NF) s_a[buf ^ 1][tid + 256 * i] = stage[i];
+        }
+        __syncthreads();
     }
-    // accumulator register q of row block r: row n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian
+    // accumulator register q of row block r: row n = 32 r + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g
 #pragma unroll
-    for (int r = 0; r < kGemmRbg; ++r) {
-        if (r >= nrb) break;
+    for (int r = 0; r < RB; ++r) {
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-            const int g = g0 + 32 * cb;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int n = 32 * (rb0 + r) + 8 * (q >> 2) + 4 * h + (q & 3);
-                const float a = acc[r][cb][q];
-                if (MODE == kMlpFwdRelu) {
-                    p.dst[(size_t)n * p.ldp + g] = fmaxf(a + p.bias[n], 0.f);
-                } else if (MODE == kMlpFwdHeads) {
-                    if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + p.bias[n];
-                } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
-                    if (n < p.n_a) {
-                        float* d = p.dst_a + (size_t)n * p.ldp + g;
-                        *d = p.accumulate_a ? *d + a : a;
-                    } else if (p.mask) {
-                        const size_t o = (size_t)(n - p.n_a) * p.ldp + g;
-                        p.dst[o] = p.mask[o] > 0.f ? a : 0.f;   // threshold_backward(g, h, 0)
-                    }
+        for (int q = 0; q < 16; ++q) {
+            const int n = 32 * r + 8 * (q >> 2) + 4 * h + (q & 3);
+            const float a = acc[r][q];
+            if (MODE == kMlpFwdRelu) {
+                p.dst[(size_t)n * p.ldp + g] = fmaxf(a + p.bias[n], 0.f);
+            } else if (MODE == kMlpFwdHeads) {
+                if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + p.bias[n];
+            } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
+                if (n < p.n_a) {
+                    float* d = p.dst_a + (size_t)n * p.ldp + g;
+                    *d = p.accumulate_a ? *d + a : a;
+                } else if (p.mask) {
+                    const size_t o = (size_t)(n - p.n_a) * p.ldp + g;
+                    p.dst[o] = p.mask[o] > 0.f ? a : 0.f;   // threshold_backward(g, h, 0)
                 }
             }
         }
@@ -237,98 +248,121 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 }
 
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
-// One wave per (chunk, 128 x 128 output tile): 4 x 4 blocks of 32 x 32, 96 MFMAs per 16-Gaussian step.
-constexpr int kWgTile = 4;
+// One workgroup per Gaussian chunk computes the whole (32 NRB) x (32 KRB) output, one wave per tile of TNB x TKB
+// blocks of 32 x 32 (at most four waves: one per SIMD, 512 registers each).  Each 16-Gaussian step, every thread loads 64 B of one or two feature rows (of G or X), splits
+// them into the three bf16 planes ONCE and writes them to LDS in the MFMA operand layout; the waves then read their
+// A (G) and B (X) fragments from there: [row][plane * 2 + h] slots of 16 B, 7 slots per row (112 B: the 16 lanes
+// of a b128 read hit 16 distinct bank quads).  Double-buffered: step s + 1 is staged while step s is multiplied.
+constexpr int kWgSlots = 7;
 
-__device__ __forceinline__ void load_rows8(const float* __restrict__ row, int pbase, int P, float (&v)[8]) {
-    const float4 a = *reinterpret_cast<const float4*>(row + pbase);
-    const float4 b = *reinterpret_cast<const float4*>(row + pbase + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+template <int NRB, int KRB, int TNB, int TKB>
+struct WgradShape {
+    static constexpr int TN = NRB / TNB, TK = KRB / TKB, WAVES = TN * TK;
+    static_assert(TN * TNB == NRB && TK * TKB == KRB && WAVES <= 4, "wgrad tiling");
+    static constexpr int ROWS = 32 * (NRB + KRB);                       // G rows then X rows
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int RPT = (ROWS + THREADS - 1) / THREADS;          // rows staged per thread
+};
+
+__device__ __forceinline__ void stage_row(const float* __restrict__ row, int p0, int P, bf16x8* __restrict__ slot,
+                                          float* bsum) {
+    float v[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (pbase + j >= P) v[j] = 0.f;   // Gaussians past P hold whatever the tail columns hold
+    for (int q = 0; q < 4; ++q) {
+        const float4 f = *reinterpret_cast<const float4*>(row + p0 + 4 * q);
+        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if (p0 + j >= P) v[j] = 0.f;   // Gaussians past P (the chunk tail) contribute nothing
+    if (bsum) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) *bsum += v[j];
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+        float w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = v[8 * hh + j];
+        const Split8 sp = split8(w);
+        slot[0 + hh] = sp.hi;
+        slot[2 + hh] = sp.mid;
+        slot[4 + hh] = sp.lo;
+    }
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_wgrad(MlpWgradParams p) {
-    const int lane = threadIdx.x, h = lane >> 5, c = lane & 31;
-    const int chunk = blockIdx.x;
-    const int tn = blockIdx.y / p.tiles_k, tk = blockIdx.y % p.tiles_k;
-    const int nb = min(kWgTile, p.n_rb - kWgTile * tn), kb = min(kWgTile, p.k_rb - kWgTile * tk);
-    const int p_lo = chunk * p.chunk, p_hi = min(p.P, p_lo + p.chunk);
-    f32x16 acc[kWgTile][kWgTile];
+template <int NRB, int KRB, int TNB, int TKB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_wgrad(MlpWgradParams p) {
+    typedef WgradShape<NRB, KRB, TNB, TKB> S;
+    __shared__ bf16x8 s_op[2][S::ROWS][kWgSlots];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
+    const int tn = wave / S::TK, tk = wave % S::TK;
+    const int p_lo = blockIdx.x * p.chunk, p_hi = min(p.P, p_lo + p.chunk);
+    // the rows this thread stages: r = tid + THREADS i; G row r (< 32 NRB) or X row r - 32 NRB
+    const float* src[S::RPT];
+    float bsum[S::RPT];
 #pragma unroll
-    for (int i = 0; i < kWgTile; ++i)
-#pragma unroll
-        for (int j = 0; j < kWgTile; ++j) acc[i][j] = f32x16{};
-    float bsum[kWgTile] = {0.f, 0.f, 0.f, 0.f};
-    const float* grow[kWgTile];
-    const float* xrow[kWgTile];
-#pragma unroll
-    for (int i = 0; i < kWgTile; ++i) {
-        const int n = 32 * (kWgTile * tn + min(i, nb - 1)) + c;
-        grow[i] = p.G + (size_t)n * p.ldp;
-        const int k = 32 * (kWgTile * tk + min(i, kb - 1)) + c;
-        xrow[i] = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
-    }
-    // software pipeline: the next step's rows are loaded while this step's MFMAs run (one wave per SIMD)
-    float gv[kWgTile][8], xv[kWgTile][8];
-#pragma unroll
-    for (int i = 0; i < kWgTile; ++i) {
-        load_rows8(grow[i], p_lo + 8 * h, p_hi, gv[i]);
-        load_rows8(xrow[i], p_lo + 8 * h, p_hi, xv[i]);
-    }
-    for (int pb = p_lo; pb < p_hi; pb += 16) {
-        Split8 a[kWgTile], b[kWgTile];
-#pragma unroll
-        for (int i = 0; i < kWgTile; ++i) {
-            if (tk == 0) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) bsum[i] += gv[i][j];
-            }
-            a[i] = split8(gv[i]);
-            b[i] = split8(xv[i]);
-        }
-        if (pb + 16 < p_hi) {
-#pragma unroll
-            for (int i = 0; i < kWgTile; ++i) {
-                load_rows8(grow[i], pb + 16 + 8 * h, p_hi, gv[i]);
-                load_rows8(xrow[i], pb + 16 + 8 * h, p_hi, xv[i]);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < kWgTile; ++i) {
-            if (i >= nb) break;
-#pragma unroll
-            for (int j = 0; j < kWgTile; ++j) {
-                if (j >= kb) break;
-                acc[i][j] = mfma_x6(a[i], b[j], acc[i][j]);
-            }
+    for (int i = 0; i < S::RPT; ++i) {
+        const int r = tid + S::THREADS * i;
+        bsum[i] = 0.f;
+        if (r < 32 * NRB) src[i] = p.G + (size_t)r * p.ldp;
+        else {
+            const int k = r - 32 * NRB;
+            src[i] = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
         }
     }
-    // partial[chunk][n][k], n = 32 (4 tn + i) + 8 (q >> 2) + 4 h + (q & 3), k = 32 (4 tk + j) + c
-    float* out = p.partial + (size_t)chunk * (32 * p.n_rb) * (32 * p.k_rb);
+    auto stage = [&](int p0, int buf) {
 #pragma unroll
-    for (int i = 0; i < kWgTile; ++i) {
-        if (i >= nb) break;
+        for (int i = 0; i < S::RPT; ++i) {
+            const int r = tid + S::THREADS * i;
+            if (r < S::ROWS) stage_row(src[i], p0, p_hi, s_op[buf][r], r < 32 * NRB ? &bsum[i] : nullptr);
+        }
+    };
+    f32x16 acc[TNB][TKB];
 #pragma unroll
-        for (int j = 0; j < kWgTile; ++j) {
-            if (j >= kb) break;
+    for (int i = 0; i < TNB; ++i)
+#pragma unroll
+        for (int j = 0; j < TKB; ++j) acc[i][j] = f32x16{};
+    stage(p_lo, 0);
+    __syncthreads();
+    int buf = 0;
+    for (int pb = p_lo; pb < p_hi; pb += 16, buf ^= 1) {
+        if (pb + 16 < p_hi) stage(pb + 16, buf ^ 1);
+        Split8 a[TNB], b[TKB];
+#pragma unroll
+        for (int i = 0; i < TNB; ++i) {
+            const bf16x8* sl = s_op[buf][32 * (TNB * tn + i) + c];
+            a[i].hi = sl[0 + h]; a[i].mid = sl[2 + h]; a[i].lo = sl[4 + h];
+        }
+#pragma unroll
+        for (int j = 0; j < TKB; ++j) {
+            const bf16x8* sl = s_op[buf][32 * NRB + 32 * (TKB * tk + j) + c];
+            b[j].hi = sl[0 + h]; b[j].mid = sl[2 + h]; b[j].lo = sl[4 + h];
+        }
+#pragma unroll
+        for (int i = 0; i < TNB; ++i)
+#pragma unroll
+            for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6(a[i], b[j], acc[i][j]);
+        __syncthreads();
+    }
+    // partial[chunk][n][k], n = 32 (TNB tn + i) + 8 (q >> 2) + 4 h + (q & 3), k = 32 (TKB tk + j) + c
+    float* out = p.partial + (size_t)blockIdx.x * (32 * NRB) * (32 * KRB);
+#pragma unroll
+    for (int i = 0; i < TNB; ++i) {
+#pragma unroll
+        for (int j = 0; j < TKB; ++j) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int n = 32 * (kWgTile * tn + i) + 8 * (q >> 2) + 4 * h + (q & 3);
-                const int k = 32 * (kWgTile * tk + j) + c;
-                out[(size_t)n * (32 * p.k_rb) + k] = acc[i][j][q];
+                const int n = 32 * (TNB * tn + i) + 8 * (q >> 2) + 4 * h + (q & 3);
+                const int k = 32 * (TKB * tk + j) + c;
+                out[(size_t)n * (32 * KRB) + k] = acc[i][j][q];
             }
         }
     }
-    if (tk == 0) {   // the bias gradient: this lane's row (n = 32 (4 tn + i) + c) over its half's Gaussians
 #pragma unroll
-        for (int i = 0; i < kWgTile; ++i) {
-            if (i >= nb) break;
-            const float s = bsum[i] + __shfl_xor(bsum[i], 32);
-            if (h == 0) p.bias_partial[(size_t)chunk * (32 * p.n_rb) + 32 * (kWgTile * tn + i) + c] = s;
-        }
+    for (int i = 0; i < S::RPT; ++i) {   // the bias gradient: the G rows' sums over this chunk
+        const int r = tid + S::THREADS * i;
+        if (r < 32 * NRB) p.bias_partial[(size_t)blockIdx.x * (32 * NRB) + r] = bsum[i];
     }
 }
 
@@ -360,17 +394,32 @@ void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, floa
     if (P > 0) hipLaunchKernelGGL(k_mlp_encode_bwd, dim3((P + 255) / 256), dim3(256), 0, s, P, ldp, E, dE, dx, accumulate);
 }
 
+template <int MODE>
+static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
+    const dim3 grid(p.ldp / 128);
+    switch (p.rb) {
+        case 2: hipLaunchKernelGGL((k_mlp_gemm<MODE, 2>), grid, dim3(256), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_mlp_gemm<MODE, 3>), grid, dim3(256), 0, s, p); break;
+        case 8: hipLaunchKernelGGL((k_mlp_gemm<MODE, 8>), grid, dim3(256), 0, s, p); break;
+        case 10: hipLaunchKernelGGL((k_mlp_gemm<MODE, 10>), grid, dim3(256), 0, s, p); break;
+        default: break;
+    }
+}
+
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s) {
-    const dim3 grid(p.ldp / 256, (p.rb + kGemmRbg - 1) / kGemmRbg);
-    if (mode == kMlpFwdRelu) hipLaunchKernelGGL(k_mlp_gemm<kMlpFwdRelu>, grid, dim3(256), 0, s, p);
-    else if (mode == kMlpFwdHeads) hipLaunchKernelGGL(k_mlp_gemm<kMlpFwdHeads>, grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(k_mlp_gemm<kMlpBwdMask>, grid, dim3(256), 0, s, p);
+    if (mode == kMlpFwdRelu) launch_gemm_rb<kMlpFwdRelu>(p, s);
+    else if (mode == kMlpFwdHeads) launch_gemm_rb<kMlpFwdHeads>(p, s);
+    else launch_gemm_rb<kMlpBwdMask>(p, s);
 }
 
 void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s) {
     const int n_chunks = (p.P + p.chunk - 1) / p.chunk;
-    const dim3 grid(n_chunks, p.tiles_n * p.tiles_k);
-    hipLaunchKernelGGL(k_mlp_wgrad, grid, dim3(64), 0, s, p);
+    const dim3 grid(n_chunks);
+#define GSD_WGRAD(N, K, TN, TK)                                                                            \
+    if (p.n_rb == N && p.k_rb == K)                                                                        \
+        hipLaunchKernelGGL((k_mlp_wgrad<N, K, TN, TK>), grid, dim3(64 * WgradShape<N, K, TN, TK>::WAVES), 0, s, p);
+    GSD_WGRAD(8, 8, 4, 4) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 4, 3) else GSD_WGRAD(2, 8, 2, 4)
+#undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
     hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
                        32 * p.k_rb, (const float*)p.partial, dst);
