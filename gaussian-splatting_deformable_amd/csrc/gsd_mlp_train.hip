@@ -106,13 +106,25 @@ __global__ void k_mlp_gather_bias(MlpWeightRef b, float* __restrict__ dst, int n
     dst[n] = e ? *e : 0.f;
 }
 
-// (P, n) row-major -> [dst_rows][ldp] feature-major (rows past n zero): the heads' incoming gradient
+// (P, n) row-major -> [dst_rows][ldp] feature-major (rows past n zero): the heads' incoming gradient.  A workgroup
+// takes 64 Gaussians: their n-float rows are one contiguous run, read coalesced into LDS, then written per feature.
 __global__ __launch_bounds__(256) void k_mlp_rows_to_features(int P, int ldp, int n, const float* __restrict__ src,
                                                               float* __restrict__ dst, int dst_rows) {
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= ldp) return;
-#pragma unroll 1
-    for (int r = 0; r < dst_rows; ++r) dst[(size_t)r * ldp + g] = (g < P && r < n) ? src[(size_t)g * n + r] : 0.f;
+    __shared__ float tile[64][65];
+    const int g0 = blockIdx.x * 64;
+    const int cnt = min(64, P - g0) * n;   // floats of the run (<= 0 past P)
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int gg = i / 64, r = i % 64;
+        tile[gg][r] = 0.f;
+        (void)r;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += 256) tile[i / n][i % n] = src[(size_t)g0 * n + i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * dst_rows; i += 256) {
+        const int r = i / 64, gg = i % 64;
+        dst[(size_t)r * ldp + g0 + gg] = r < 64 ? tile[gg][r] : 0.f;
+    }
 }
 
 // ---- the positional encoding (gaussian_model.py:33-82), feature-major ----
@@ -264,17 +276,19 @@ struct WgradShape {
     static constexpr int RPT = (ROWS + THREADS - 1) / THREADS;          // rows staged per thread
 };
 
-__device__ __forceinline__ void stage_row(const float* __restrict__ row, int p0, int P, bf16x8* __restrict__ slot,
-                                          float* bsum) {
-    float v[16];
+__device__ __forceinline__ void load_row16(const float* __restrict__ row, int p0, float (&v)[16]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float4 f = *reinterpret_cast<const float4*>(row + p0 + 4 * q);
         v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
     }
+}
+
+__device__ __forceinline__ void stage_row(const float (&raw)[16], int p0, int P, bf16x8* __restrict__ slot,
+                                          float* bsum) {
+    float v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-        if (p0 + j >= P) v[j] = 0.f;   // Gaussians past P (the chunk tail) contribute nothing
+    for (int j = 0; j < 16; ++j) v[j] = p0 + j < P ? raw[j] : 0.f;   // Gaussians past P contribute nothing
     if (bsum) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) *bsum += v[j];
@@ -311,11 +325,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
             src[i] = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
         }
     }
-    auto stage = [&](int p0, int buf) {
+    // rows of step s + 2 in registers while step s multiplies; split and written to LDS one step ahead
+    float raw[S::RPT][16];
+    auto load = [&](int p0) {
+#pragma unroll
+        for (int i = 0; i < S::RPT; ++i)
+            if (tid + S::THREADS * i < S::ROWS) load_row16(src[i], p0, raw[i]);
+    };
+    auto write = [&](int p0, int buf) {
 #pragma unroll
         for (int i = 0; i < S::RPT; ++i) {
             const int r = tid + S::THREADS * i;
-            if (r < S::ROWS) stage_row(src[i], p0, p_hi, s_op[buf][r], r < 32 * NRB ? &bsum[i] : nullptr);
+            if (r < S::ROWS) stage_row(raw[i], p0, p_hi, s_op[buf][r], r < 32 * NRB ? &bsum[i] : nullptr);
         }
     };
     f32x16 acc[TNB][TKB];
@@ -323,11 +344,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     for (int i = 0; i < TNB; ++i)
 #pragma unroll
         for (int j = 0; j < TKB; ++j) acc[i][j] = f32x16{};
-    stage(p_lo, 0);
+    load(p_lo);
+    write(p_lo, 0);
+    if (p_lo + 16 < p_hi) load(p_lo + 16);
     __syncthreads();
     int buf = 0;
     for (int pb = p_lo; pb < p_hi; pb += 16, buf ^= 1) {
-        if (pb + 16 < p_hi) stage(pb + 16, buf ^ 1);
+        if (pb + 16 < p_hi) {
+            write(pb + 16, buf ^ 1);
+            if (pb + 32 < p_hi) load(pb + 32);
+        }
         Split8 a[TNB], b[TKB];
 #pragma unroll
         for (int i = 0; i < TNB; ++i) {
@@ -366,19 +392,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     }
 }
 
-// dW[n][k] = sum over the chunks of partial[chunk][n][k], in chunk order (deterministic), scattered into the
-// reference-shaped pieces (padded columns and rows dropped); the bias gradient likewise (k_cols = 1)
+// dW[n][k] = sum over the chunks of partial[chunk][n][k], in a fixed order (deterministic), scattered into the
+// reference-shaped pieces (padded columns and rows dropped); the bias gradient likewise (k_cols = 1).  A workgroup
+// owns 32 consecutive outputs; its 8 thread groups sum the chunks c = g, g + 8, ... (loads four chunks ahead) and
+// the 8 group sums are combined in group order through LDS.
 __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_rows, int k_cols,
                                                           const float* __restrict__ partial, MlpWeightRef dst) {
-    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    __shared__ float red[8][32];
     const long long n_el = (long long)n_rows * k_cols;
-    if (e >= n_el) return;
-    const int n = (int)(e / k_cols), k = (int)(e - (long long)n * k_cols);
-    float* d = mlp_elem(dst, n, mlp_col(dst.map, k));
-    if (!d) return;
+    const int grp = threadIdx.x >> 5, l = threadIdx.x & 31;
+    const long long e = (long long)blockIdx.x * 32 + l;
     float s = 0.f;
-    for (int c = 0; c < n_chunks; ++c) s += partial[(size_t)c * n_el + e];
-    *d = s;
+    if (e < n_el) {
+        int c = grp;
+        for (; c + 24 < n_chunks; c += 32) {
+            const float a = partial[(size_t)c * n_el + e], b = partial[(size_t)(c + 8) * n_el + e];
+            const float d = partial[(size_t)(c + 16) * n_el + e], f = partial[(size_t)(c + 24) * n_el + e];
+            s += a; s += b; s += d; s += f;
+        }
+        for (; c < n_chunks; c += 8) s += partial[(size_t)c * n_el + e];
+    }
+    red[grp][l] = s;
+    __syncthreads();
+    if (grp == 0 && e < n_el) {
+        float t = red[0][l];
+#pragma unroll
+        for (int g = 1; g < 8; ++g) t += red[g][l];
+        const int n = (int)(e / k_cols), k = (int)(e - (long long)n * k_cols);
+        float* d = mlp_elem(dst, n, mlp_col(dst.map, k));
+        if (d) *d = t;
+    }
 }
 
 void launch_mlp_pack(const MlpPackParams& p, hipStream_t s) {
@@ -421,14 +464,14 @@ void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const Ml
     GSD_WGRAD(8, 8, 4, 4) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 4, 3) else GSD_WGRAD(2, 8, 2, 4)
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
-    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
+    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 31) / 32)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
                        32 * p.k_rb, (const float*)p.partial, dst);
-    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 255) / 256), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1,
+    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 31) / 32), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1,
                        (const float*)p.bias_partial, dst_b);
 }
 
 void launch_mlp_rows_to_features(int P, int ldp, int n, const float* src, float* dst, int dst_rows, hipStream_t s) {
-    hipLaunchKernelGGL(k_mlp_rows_to_features, dim3(ldp / 256), dim3(256), 0, s, P, ldp, n, src, dst, dst_rows);
+    hipLaunchKernelGGL(k_mlp_rows_to_features, dim3(ldp / 64), dim3(256), 0, s, P, ldp, n, src, dst, dst_rows);
 }
 
 void launch_mlp_gather_bias(const MlpWeightRef& b, float* dst, int n_pad, hipStream_t s) {
