@@ -950,6 +950,7 @@ struct MlpWs {
     float *E, *ET, *H[9];   // H[1..8]: the hidden layers' outputs
     float *Gh, *ga, *gb, *dE;
     float *partial, *bias_partial;
+    unsigned short* bits[9];   // bits[1..8]: the ReLU masks of H[1..8] (16 row blocks x 2 halves x ldp words)
 };
 size_t carve_mlp(void* base, int64_t P, MlpWs* w) {
     char* p = base ? align_ptr(base) : nullptr;
@@ -976,6 +977,8 @@ size_t carve_mlp(void* base, int64_t P, MlpWs* w) {
     const int64_t chunks = (P + kMlpChunk - 1) / kMlpChunk;
     v.partial = reinterpret_cast<float*>(take(sizeof(float) * (size_t)chunks * 256 * 320));
     v.bias_partial = reinterpret_cast<float*>(take(sizeof(float) * (size_t)chunks * 256));
+    v.bits[0] = nullptr;
+    for (int l = 1; l <= 8; ++l) v.bits[l] = reinterpret_cast<unsigned short*>(take(2 * 16 * sizeof(short) * (size_t)v.ldp));
     if (w) *w = v;
     return off + kAlign;
 }
@@ -1045,6 +1048,7 @@ int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, cons
             if (l < 8) {
                 g.bias = B[l];
                 g.dst = ws.H[l + 1];
+                g.mask_out = ws.bits[l + 1];
                 gsd::launch_mlp_gemm(g, gsd::kMlpFwdRelu, s);
             } else {
                 g.bias = ws.bias_heads;
@@ -1078,10 +1082,12 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
         q.partial = ws.partial; q.bias_partial = ws.bias_partial;
         gsd::launch_mlp_wgrad(q, mlp_weight(l, d_weights), mlp_weight(l, d_biases, 1), s);
     };
-    auto dgemm = [&](int l, const float* G, int ks, const float* mask, float* dst, int n_a, int acc_a) {
+    auto dgemm = [&](int l, const float* G, int ks, int mask_layer, float* dst, int n_a, int acc_a) {
         gsd::MlpGemmParams g{};
         g.P = (int)P; g.ldp = ldp; g.src0 = G; g.ks0 = ks; g.frags = ws.bfrag[l]; g.rb = kMlpIn[l] / 32;
-        g.mask = mask; g.dst = dst; g.n_a = n_a; g.dst_a = ws.dE; g.accumulate_a = acc_a;
+        g.mask = mask_layer > 0 ? ws.H[mask_layer] : nullptr;
+        g.mask_in = mask_layer > 0 ? ws.bits[mask_layer] : nullptr;   // the forward's ReLU bits of that layer
+        g.dst = dst; g.n_a = n_a; g.dst_a = ws.dE; g.accumulate_a = acc_a;
         gsd::launch_mlp_gemm(g, gsd::kMlpBwdMask, s);
     };
     (void)chunks;
@@ -1089,16 +1095,16 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
         mlp_pack_all(W, ws, true, s);
         gsd::launch_mlp_rows_to_features((int)P, ldp, 58, grad_out, ws.Gh, 64, s);
         wgrad(8, ws.Gh, 2, ws.H[8], nullptr, 8, 8);
-        dgemm(8, ws.Gh, 4, ws.H[8], ws.ga, 0, 0);   // g of layer 7's pre-activation
+        dgemm(8, ws.Gh, 4, 8, ws.ga, 0, 0);   // g of layer 7's pre-activation
         float* g = ws.ga;
         float* other = ws.gb;
         for (int l = 7; l >= 0; --l) {
             if (l == 0) wgrad(0, g, 8, ws.E, ws.ET, 3, 2);
             else if (l == 5) wgrad(5, g, 8, ws.E, ws.H[5], 10, 2);
             else wgrad(l, g, 8, ws.H[l], nullptr, 8, 8);
-            if (l == 5) dgemm(5, g, 16, ws.H[5], other, 64, 0);   // rows 0-63: d enc(x); the rest masked by h5
-            else if (l > 0) dgemm(l, g, 16, ws.H[l], other, 0, 0);
-            else if (dx) dgemm(0, g, 16, nullptr, nullptr, 64, 1);   // d enc(x) += W0^T g (the t rows dropped)
+            if (l == 5) dgemm(5, g, 16, 5, other, 64, 0);   // rows 0-63: d enc(x); the rest masked by h5
+            else if (l > 0) dgemm(l, g, 16, l, other, 0, 0);
+            else if (dx) dgemm(0, g, 16, 0, nullptr, 64, 1);   // d enc(x) += W0^T g (the t rows dropped)
             float* tmp = g;
             g = other;
             other = tmp;

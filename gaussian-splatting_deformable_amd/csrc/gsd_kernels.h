@@ -333,6 +333,11 @@ struct MlpGemmParams {
     float* dst_a;
     int accumulate_a;
     const float* mask;              // backward: h of the rows >= n_a ([rows - n_a][ldp]); NULL: those rows dropped
+    // the ReLU masks as bits in the accumulator layout: word [(rb * 2 + h) * ldp + g] holds bit q of row
+    // 32 rb + 8 (q >> 2) + 4 h + (q & 3) of Gaussian g (h > 0).  Forward: written when mask_out != NULL; backward:
+    // read instead of mask when mask_in != NULL (row block rb >= n_a / 32 uses word rb - n_a / 32)
+    unsigned short* mask_out;
+    const unsigned short* mask_in;
 };
 struct MlpWgradParams {
     int P, ldp;

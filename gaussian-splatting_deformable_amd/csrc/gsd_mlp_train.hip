@@ -236,26 +236,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
         __syncthreads();
     }
     // accumulator register q of row block r: row n = 32 r + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g
+    unsigned bits_in[RB];
+    if (MODE == kMlpBwdMask && p.mask_in) {   // the forward's ReLU bits, one 16-bit word per row block
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const int rm = r - p.n_a / 32;
+            bits_in[r] = rm >= 0 ? p.mask_in[(size_t)(rm * 2 + h) * p.ldp + g] : 0xffffu;
+        }
+    }
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
+        unsigned bits_out = 0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int n = 32 * r + 8 * (q >> 2) + 4 * h + (q & 3);
             const float a = acc[r][q];
             if (MODE == kMlpFwdRelu) {
-                p.dst[(size_t)n * p.ldp + g] = fmaxf(a + p.bias[n], 0.f);
+                const float y = fmaxf(a + p.bias[n], 0.f);
+                p.dst[(size_t)n * p.ldp + g] = y;
+                bits_out |= (y > 0.f ? 1u : 0u) << q;
             } else if (MODE == kMlpFwdHeads) {
                 if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + p.bias[n];
             } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
                 if (n < p.n_a) {
                     float* d = p.dst_a + (size_t)n * p.ldp + g;
                     *d = p.accumulate_a ? *d + a : a;
+                } else if (p.mask_in) {
+                    p.dst[(size_t)(n - p.n_a) * p.ldp + g] = (bits_in[r] >> q) & 1u ? a : 0.f;   // threshold_backward
                 } else if (p.mask) {
                     const size_t o = (size_t)(n - p.n_a) * p.ldp + g;
                     p.dst[o] = p.mask[o] > 0.f ? a : 0.f;   // threshold_backward(g, h, 0)
                 }
             }
         }
+        if (MODE == kMlpFwdRelu && p.mask_out) p.mask_out[(size_t)(r * 2 + h) * p.ldp + g] = (unsigned short)bits_out;
     }
 }
 
