@@ -113,7 +113,7 @@ def roofline(kernel, ms, nbytes, workload):
         rate = v["instructions"] / (ms * 1e-3) / 1e9
         valu = {"achieved": round(rate, 2), "peak": VALU_PEAK_GINST, "unit": "G wave64-VALU-instr/s",
                 "frac": round(rate / VALU_PEAK_GINST, 4), "instructions_per_launch": int(v["instructions"]),
-                "pmc_issue_per_simd_cycle": v.get("issue_per_simd_cycle"), "pmc_valu_busy_frac": v.get("busy_frac"),
+                "pmc_issue_per_simd_cycle": v.get("issue_per_simd_cycle"),
                 "pmc_lds_issue_wait_frac": v.get("lds_issue_wait_frac")}
         if valu["frac"] > hbm["frac"]:
             roof.update(bound="valu", achieved=valu["achieved"], peak=valu["peak"], unit=valu["unit"],

@@ -41,9 +41,8 @@ def main(src, dst, workload):
             if cs.get("SQ_WAVE_CYCLES"):
                 e["valu"]["lds_issue_wait_frac"] = round(cs.get("SQ_WAIT_INST_LDS", 0.0) / cs["SQ_WAVE_CYCLES"], 4)
             if cs.get("SQ_ACTIVE_INST_VALU"):
-                # VALU pipe busy: SQ_ACTIVE_INST_VALU counts quad-cycles of VALU issue; the issue-rate figure above
-                # prices every instruction at 2 cycles, while transcendentals, DPP and selects take 4-8
-                e["valu"]["busy_frac"] = round(4.0 * cs["SQ_ACTIVE_INST_VALU"] / (1024.0 * cyc), 4)
+                # raw: SQ_ACTIVE_INST_VALU (summed over waves; ~1 per VALU instruction on the render kernels)
+                e["valu"]["active_inst_valu"] = int(cs["SQ_ACTIVE_INST_VALU"])
         out[short(k)] = e
     out["_workload"] = workload
     out["_note"] = (f"per-launch means over the profiled launches (scripts/prof_render.py, {workload}); FETCH_SIZE x2 "
