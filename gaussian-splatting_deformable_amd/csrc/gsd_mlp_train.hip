@@ -23,6 +23,8 @@
 //                bias gradient's row sums of g; k_mlp_wgrad_reduce sums the partials in a fixed order.
 //   k_mlp_encode / k_mlp_encode_bwd   enc(x), enc(t) feature-major; dL/dx from dL/d enc(x) through the stored
 //                sin / cos (d sin(2^i x) = 2^i cos(2^i x) dx: no trig in the backward).
+#include <cstdlib>
+
 #include "gsd_kernels.h"
 
 namespace gsd {
@@ -204,9 +206,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
 #pragma unroll
     for (int i = 0; i < PER; ++i)
         if (tid + 256 * i < NF) s_a[0][tid + 256 * i] = F[tid + 256 * i];
-    float x0[8], x1[8];
-    load_x8(p, 0, h, g, x0);
-    if (KS > 1) load_x8(p, 1, h, g, x1);
+    // X^T fragments kXDepth k-steps ahead (a ring of registers, rotated by copies the compiler renames away)
+    constexpr int kXDepth = 4;
+    float xq[kXDepth][8];
+#pragma unroll
+    for (int d = 0; d < kXDepth; ++d)
+        if (d < KS) load_x8(p, d, h, g, xq[d]);
     __syncthreads();
     for (int ks = 0; ks < KS; ++ks) {
         const int buf = ks & 1;
@@ -216,10 +221,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
             for (int i = 0; i < PER; ++i)
                 if (tid + 256 * i < NF) stage[i] = src[tid + 256 * i];
         }
-        const Split8 b = split8(x0);
+        const Split8 b = split8(xq[0]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x0[j] = x1[j];
-        if (ks + 2 < KS) load_x8(p, ks + 2, h, g, x1);
+        for (int d = 0; d + 1 < kXDepth; ++d)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xq[d][j] = xq[d + 1][j];
+        if (ks + kXDepth < KS) load_x8(p, ks + kXDepth, h, g, xq[kXDepth - 1]);
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             Split8 a;
@@ -247,16 +254,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         unsigned bits_out = 0;
+        float bias[16];
+        if (MODE != kMlpBwdMask) {   // rows 32 r + 8 j + 4 h .. + 3 are consecutive: one 16-B load per (r, j)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + 32 * r + 8 * j + 4 * h);
+                bias[4 * j] = b4.x; bias[4 * j + 1] = b4.y; bias[4 * j + 2] = b4.z; bias[4 * j + 3] = b4.w;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int n = 32 * r + 8 * (q >> 2) + 4 * h + (q & 3);
             const float a = acc[r][q];
             if (MODE == kMlpFwdRelu) {
-                const float y = fmaxf(a + p.bias[n], 0.f);
+                const float y = fmaxf(a + bias[q], 0.f);
                 p.dst[(size_t)n * p.ldp + g] = y;
                 bits_out |= (y > 0.f ? 1u : 0u) << q;
             } else if (MODE == kMlpFwdHeads) {
-                if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + p.bias[n];
+                if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + bias[q];
             } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
                 if (n < p.n_a) {
                     float* d = p.dst_a + (size_t)n * p.ldp + g;
@@ -275,7 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
 
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
 // One workgroup per Gaussian chunk computes the whole (32 NRB) x (32 KRB) output, one wave per tile of TNB x TKB
-// blocks of 32 x 32 (at most four waves: one per SIMD, 512 registers each).  Each 16-Gaussian step, every thread loads 64 B of one or two feature rows (of G or X), splits
+// blocks of 32 x 32 (four waves, one per SIMD with 512 registers; or eight, two per SIMD, on half-size tiles).  Each 16-Gaussian step, every thread loads 64 B of one or two feature rows (of G or X), splits
 // them into the three bf16 planes ONCE and writes them to LDS in the MFMA operand layout; the waves then read their
 // A (G) and B (X) fragments from there: [row][plane * 2 + h] slots of 16 B, 7 slots per row (112 B: the 16 lanes
 // of a b128 read hit 16 distinct bank quads).  Double-buffered: step s + 1 is staged while step s is multiplied.
@@ -284,7 +299,7 @@ constexpr int kWgSlots = 7;
 template <int NRB, int KRB, int TNB, int TKB>
 struct WgradShape {
     static constexpr int TN = NRB / TNB, TK = KRB / TKB, WAVES = TN * TK;
-    static_assert(TN * TNB == NRB && TK * TKB == KRB && WAVES <= 4, "wgrad tiling");
+    static_assert(TN * TNB == NRB && TK * TKB == KRB && WAVES <= 8, "wgrad tiling");
     static constexpr int ROWS = 32 * (NRB + KRB);                       // G rows then X rows
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int RPT = (ROWS + THREADS - 1) / THREADS;          // rows staged per thread
@@ -320,7 +335,8 @@ __device__ __forceinline__ void stage_row(const float (&raw)[16], int p0, int P,
 }
 
 template <int NRB, int KRB, int TNB, int TKB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_wgrad(MlpWgradParams p) {
+__global__ __launch_bounds__(64 * ((NRB / TNB) * (KRB / TKB)))
+__attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void k_mlp_wgrad(MlpWgradParams p) {
     typedef WgradShape<NRB, KRB, TNB, TKB> S;
     __shared__ bf16x8 s_op[2][S::ROWS][kWgSlots];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
@@ -475,7 +491,13 @@ void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const Ml
 #define GSD_WGRAD(N, K, TN, TK)                                                                            \
     if (p.n_rb == N && p.k_rb == K)                                                                        \
         hipLaunchKernelGGL((k_mlp_wgrad<N, K, TN, TK>), grid, dim3(64 * WgradShape<N, K, TN, TK>::WAVES), 0, s, p);
-    GSD_WGRAD(8, 8, 4, 4) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 4, 3) else GSD_WGRAD(2, 8, 2, 4)
+    static const bool w8 = [] {   // GSD_WGRAD_WAVES=8: the 8 x 8 shape as eight waves of 4 x 2 blocks (experiment)
+        const char* e = getenv("GSD_WGRAD_WAVES");
+        return e && atoi(e) == 8;
+    }();
+    if (w8 && p.n_rb == 8 && p.k_rb == 8)
+        hipLaunchKernelGGL((k_mlp_wgrad<8, 8, 4, 2>), grid, dim3(512), 0, s, p);
+    else GSD_WGRAD(8, 8, 4, 4) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 4, 3) else GSD_WGRAD(2, 8, 2, 4)
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
     hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 31) / 32)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
