@@ -325,7 +325,8 @@ struct MlpGemmParams {
     const float* src1;              // the rest: [16 ks1][ldp] (the concatenated inputs of layers 0 and 5)
     int ks1;
     const void* frags;              // k_mlp_pack output: [ks][rb][split][lane]
-    int rb;                         // output row blocks of 32
+    int rb;                         // output row blocks of 32 (of the packed A)
+    int rb_off;                     // launch-internal: first row block of this workgroup row (grid.y)
     const float* bias;              // forward: 32 rb floats
     float* dst;                     // forward hidden: [32 rb][ldp]; heads: (P, n_out) row-major; backward: g rows
     int n_out;                      // heads: outputs written (58)

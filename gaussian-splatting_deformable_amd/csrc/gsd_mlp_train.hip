@@ -191,21 +191,23 @@ __device__ __forceinline__ void load_x8(const MlpGemmParams& p, int ks, int h, i
 }
 
 template <int MODE, int RB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 : 2))) void k_mlp_gemm(MlpGemmParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_gemm(MlpGemmParams p) {
     constexpr int NF = RB * 3 * 64;               // 16-B fragments per k-step
     constexpr int PER = (NF + 255) / 256;         // per thread
     __shared__ bf16x8 s_a[2][NF];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
     const int g = blockIdx.x * 128 + wave * 32 + c;   // always < ldp
     const int KS = p.ks0 + p.ks1;
-    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags);
+    const int rb0 = blockIdx.y * RB;                  // this workgroup's RB row blocks of the p.rb packed ones
+    const size_t kstride = (size_t)p.rb * 3 * 64;     // fragments per k-step of the packed A
+    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags) + (size_t)rb0 * 3 * 64;
     f32x16 acc[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) acc[r] = f32x16{};
     bf16x8 stage[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-        if (tid + 256 * i < NF) s_a[0][tid + 256 * i] = F[tid + 256 * i];
+        if (tid + 256 * i < NF) s_a[0][tid + 256 * i] = F[tid + 256 * i];   // k-step 0's RB x 3 x 64 run
     // X^T fragments kXDepth k-steps ahead (a ring of registers, rotated by copies the compiler renames away)
     constexpr int kXDepth = 4;
     float xq[kXDepth][8];
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
     for (int ks = 0; ks < KS; ++ks) {
         const int buf = ks & 1;
         if (ks + 1 < KS) {   // the next k-step's fragments into registers (written to LDS after the MFMAs)
-            const bf16x8* src = F + (size_t)(ks + 1) * NF;
+            const bf16x8* src = F + (size_t)(ks + 1) * kstride;
 #pragma unroll
             for (int i = 0; i < PER; ++i)
                 if (tid + 256 * i < NF) stage[i] = src[tid + 256 * i];
@@ -242,12 +244,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
         }
         __syncthreads();
     }
-    // accumulator register q of row block r: row n = 32 r + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g
+    // accumulator register q of row block r: row n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g
     unsigned bits_in[RB];
     if (MODE == kMlpBwdMask && p.mask_in) {   // the forward's ReLU bits, one 16-bit word per row block
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-            const int rm = r - p.n_a / 32;
+            const int rm = rb0 + r - p.n_a / 32;
             bits_in[r] = rm >= 0 ? p.mask_in[(size_t)(rm * 2 + h) * p.ldp + g] : 0xffffu;
         }
     }
@@ -258,13 +260,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
         if (MODE != kMlpBwdMask) {   // rows 32 r + 8 j + 4 h .. + 3 are consecutive: one 16-B load per (r, j)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + 32 * r + 8 * j + 4 * h);
+                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + 32 * (rb0 + r) + 8 * j + 4 * h);
                 bias[4 * j] = b4.x; bias[4 * j + 1] = b4.y; bias[4 * j + 2] = b4.z; bias[4 * j + 3] = b4.w;
             }
         }
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const int n = 32 * r + 8 * (q >> 2) + 4 * h + (q & 3);
+            const int n = 32 * (rb0 + r) + 8 * (q >> 2) + 4 * h + (q & 3);
             const float a = acc[r][q];
             if (MODE == kMlpFwdRelu) {
                 const float y = fmaxf(a + bias[q], 0.f);
@@ -284,7 +286,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RB > 8 ? 1 
                 }
             }
         }
-        if (MODE == kMlpFwdRelu && p.mask_out) p.mask_out[(size_t)(r * 2 + h) * p.ldp + g] = (unsigned short)bits_out;
+        if (MODE == kMlpFwdRelu && p.mask_out)
+            p.mask_out[(size_t)((rb0 + r) * 2 + h) * p.ldp + g] = (unsigned short)bits_out;
     }
 }
 
@@ -467,14 +470,15 @@ void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, floa
     if (P > 0) hipLaunchKernelGGL(k_mlp_encode_bwd, dim3((P + 255) / 256), dim3(256), 0, s, P, ldp, E, dE, dx, accumulate);
 }
 
+// the 320-row backward of layer 5 as two workgroup rows of 5 row blocks (grid.y): 2 waves per SIMD instead of one
+// (1.72 ms with all 10 row blocks per workgroup)
 template <int MODE>
 static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
-    const dim3 grid(p.ldp / 128);
     switch (p.rb) {
-        case 2: hipLaunchKernelGGL((k_mlp_gemm<MODE, 2>), grid, dim3(256), 0, s, p); break;
-        case 3: hipLaunchKernelGGL((k_mlp_gemm<MODE, 3>), grid, dim3(256), 0, s, p); break;
-        case 8: hipLaunchKernelGGL((k_mlp_gemm<MODE, 8>), grid, dim3(256), 0, s, p); break;
-        case 10: hipLaunchKernelGGL((k_mlp_gemm<MODE, 10>), grid, dim3(256), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_mlp_gemm<MODE, 2>), dim3(p.ldp / 128), dim3(256), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_mlp_gemm<MODE, 3>), dim3(p.ldp / 128), dim3(256), 0, s, p); break;
+        case 8: hipLaunchKernelGGL((k_mlp_gemm<MODE, 8>), dim3(p.ldp / 128), dim3(256), 0, s, p); break;
+        case 10: hipLaunchKernelGGL((k_mlp_gemm<MODE, 5>), dim3(p.ldp / 128, 2), dim3(256), 0, s, p); break;
         default: break;
     }
 }
