@@ -224,7 +224,7 @@ __device__ __forceinline__ float pair16(float a, float b) {
 // Distance-4 step after sum8 (row_ror:4): lanes with bits 2-3 clear return the sum over lanes l, l ^ 4,
 // l ^ 8, l ^ 12 of the input to sum8.
 __device__ __forceinline__ float sum4(float v) {
-    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, true));
 }
 // Lane (l & ~3) + i's value in every lane of the quad (DPP quad_perm [i, i, i, i]).
 template <int I>
@@ -233,7 +233,7 @@ __device__ __forceinline__ float quad_bcast(float v) {
 }
 // Distance-8 step (row_ror:8 == lane ^ 8 inside a 16-lane row): every lane returns v(l) + v(l ^ 8).
 __device__ __forceinline__ float sum8(float v) {
-    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, true));
 }
 
 // Transposed butterfly: c[k] is this lane's value for column k (k = 0..7).

@@ -26,7 +26,6 @@
 // one record over 4 pixels each and a short transposed butterfly finishes it;
 // the sums go to LDS accumulators and, after each 256-record batch, to HBM as
 // one set of global atomics per (Gaussian, tile) instance.
-#include <cstdlib>
 #include <type_traits>
 
 #include "gsd_kernels.h"
@@ -40,7 +39,6 @@ namespace gsd {
 constexpr int kBatch = 4;
 // (forward culling is by the alpha box only: the backward's exact ellipse test costs the forward more than it
 // saves -- 0.306 vs 0.289 ms per 8x8 quadrant, 0.366 vs 0.261 per 4x4 lane group)
-constexpr int kBwdBatch = 4;  // backward: records whose alphas are evaluated together
 constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
 
 // Does the ellipse {d : Q(d) <= t} around (mx, my) meet the rectangle [x0, x1] x [y0, y1]?
@@ -163,12 +161,6 @@ __device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s
         }
     }
     wave_lds_handoff();
-}
-
-// List entries j0 .. j0 + 3 (j0 a multiple of 4) as one LDS word instead of four byte reads; entries at or past
-// `valid` are replaced by slot 0 (always staged in the current batch, so every value read through it is finite)
-__device__ __forceinline__ int list_slot(uint32_t w4, int u, int j0, int valid) {
-    return j0 + u < valid ? (int)((w4 >> (8 * u)) & 0xffu) : 0;
 }
 
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
@@ -354,6 +346,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     }
 }
 
+// DPP row_newbcast:U -- every lane of a 16-lane row takes lane U of that row (U a compile-time constant, so the
+// compiler folds the broadcast into the consuming VALU op as its DPP source)
+template <int U>
+__device__ __forceinline__ float row_bcast(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + U, 0xf, 0xf, true));
+}
+template <int U>
+__device__ __forceinline__ int row_bcast_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + U, 0xf, 0xf, true);
+}
+
 __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
     // staged records (stage_pc), all at a 16-B stride: one LDS address per record serves the three reads
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     float4* s_box = s_u.box;
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H);
     const int tid = threadIdx.x;
-    const int lane = tg.lane;
+    const int lane = tg.lane, u16 = lane & 15;
     __shared__ int s_tile_lc;
     const uint2 rg = p.ranges[tg.tile];
     const int pid = p.W * tg.py + tg.px;
@@ -445,108 +448,112 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         // the wave (a black background: the default of train.py), without its multiply-add
         auto walk = [&](auto with_bg) {
             constexpr bool kBg = decltype(with_bg)::value;
-            for (int j0 = 0; j0 < m; j0 += kBwdGroup) {
-                // Phase 1 (pixel-major): kBwdGroup records in sub-batches of kBwdBatch.  Each lane runs the
-                // back-to-front recurrence for its pixel and leaves two numbers per record in s_qa:
-                // v = o G dL/dalpha and w = alpha T.  Every one of the nine per-record sums is a dot product of these
-                // with per-pixel factors -- the pixel offsets (mean - pixel) and dL/dpixel -- so nothing else is
-                // needed from the lane.
-                unsigned long long any_m = 0;  // lanes that took any record of the group
-                uint32_t w4 = 0;  // the group's four list entries (kBwdGroup == kBwdBatch: one sub-batch)
-#pragma unroll
-                for (int sb = 0; sb < kBwdGroup / kBwdBatch; ++sb) {
-                    const int jb = j0 + sb * kBwdBatch;
-                    if (sb > 0 && jb >= m) {  // wave-uniform: the tail of the list
-#pragma unroll
-                        for (int u = 0; u < kBwdBatch; ++u) qa[sb * kBwdBatch + u][lane] = make_float2(0.f, 0.f);
-                        continue;
-                    }
-                    float OGs[kBwdBatch];
-                    bool keep[kBwdBatch];
-                    int slot[kBwdBatch];
-                    static_assert(kBwdBatch == 4, "one LDS word of list entries per batch");
-                    // the list is the wave's, so its entries are wave-uniform: read once into a scalar register, the
-                    // slot extraction and the bounds select run on the scalar unit, and each record costs one vector
-                    // move for its LDS address (shared by its three reads)
-                    w4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(list + jb));
-#pragma unroll
-                    for (int u = 0; u < kBwdBatch; ++u) {
-                        slot[u] = list_slot(w4, u, jb, m);
+            // The list is the wave's, so its records are wave-uniform.  Instead of every lane reading every record
+            // from LDS (36 B x 64 lanes per record: with four waves per CU doing so, the LDS array and not the VALU
+            // bounded this loop), lane u of each 16-lane row loads list entry j0 + u once per 16 entries, and
+            // record U reaches all lanes by DPP row_newbcast:U, folded into the consuming VALU op.
+            for (int j0 = 0; j0 < m; j0 += 16) {
+                const int nv = m - j0;  // entries left from j0 (wave-uniform)
+                const int rslot = u16 < nv ? (int)list[j0 + u16] : 0;  // slot 0 past the list: finite, never taken
+                const float4 rpc = s_pc[rslot];
+                const float2 rbo = *reinterpret_cast<const float2*>(&s_bo[rslot]);
+                const float4 rrgb = s_rgb[rslot];
+                auto hand_off = [&](auto kc) {
+                    constexpr int K = decltype(kc)::value;
+                    // Phase 1 (pixel-major): entries K .. K + 3.  Each lane runs the back-to-front recurrence for
+                    // its pixel and leaves two numbers per record in qa: v = o G dL/dalpha and w = alpha T.  Every
+                    // one of the nine per-record sums is a dot product of these with per-pixel factors -- the pixel
+                    // offsets (mean - pixel) and dL/dpixel -- so nothing else is needed from the lane.
+                    const int r = lane & 3, grp = lane >> 2;
+                    // phase 2's record (entry K + r) and its mean, read ahead of phase 1
+                    const int rs = K + r < nv ? (int)list[j0 + K + r] : 0;
+                    const float2 mrec = *reinterpret_cast<const float2*>(&s_pc[rs]);
+                    unsigned long long any_m = 0;  // lanes that took any record of the hand-off
+                    auto rec = [&](auto uc) {
+                        constexpr int U = K + decltype(uc)::value;
+                        const float4 pc = make_float4(row_bcast<U>(rpc.x), row_bcast<U>(rpc.y), row_bcast<U>(rpc.z),
+                                                      row_bcast<U>(rpc.w));
+                        const float2 bo = make_float2(row_bcast<U>(rbo.x), row_bcast<U>(rbo.y));
                         float G;
-                        const float2 bo = *reinterpret_cast<const float2*>(&s_bo[slot[u]]);
-                        record_alpha(s_pc[slot[u]], bo, pxf, pyf, G, keep[u]);
-                        OGs[u] = bo.y * G;  // o G: alpha before the 0.99 clamp (the same product)
-                    }
-#pragma unroll
-                    for (int u = 0; u < kBwdBatch; ++u) {
-#pragma clang fp contract(fast)
-                        // alpha = min(0.99, o G) >= 1/255 <=> !(o G < 1/255), NaN included (fminf(0.99, NaN) = 0.99)
-                        const unsigned long long valid_m = (jb + u < m ? ~0ull : 0ull) &
-                                                           wave_ballot(slot[u] > slot_min) & wave_ballot(keep[u]) &
-                                                           wave_ballot(!(OGs[u] < 1.0f / 255.0f));
+                        bool keep;
+                        record_alpha(pc, bo, pxf, pyf, G, keep);
+                        const float OG = bo.y * G;  // o G: alpha before the 0.99 clamp (the same product)
+                        // backward.cu:487-488 (list position below the pixel's last contributor); alpha =
+                        // min(0.99, o G) >= 1/255 <=> !(o G < 1/255), NaN included (fminf(0.99, NaN) = 0.99)
+                        const unsigned long long valid_m = (U < nv ? ~0ull : 0ull) &
+                                                           wave_ballot(row_bcast_i<U>(rslot) > slot_min) &
+                                                           wave_ballot(keep) & wave_ballot(!(OG < 1.0f / 255.0f));
                         any_m |= valid_m;
-                        const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
-                        // one select: o G zeroed where the lane skips the record gives alpha = 0 (T unchanged) and
-                        // a zero hand-off; the hand-off carries q = o G dL/dalpha (the flush no longer scales by o)
-                        const float og = valid ? OGs[u] : 0.f;
-                        const float alpha = fminf(0.99f, og);
-                        const float inv1ma = fast_recip(1.f - alpha);
-                        T = T * inv1ma;  // backward.cu:503 (T recovered by division)
-                        const float4 c = s_rgb[slot[u]];
-                        const float cd = fmaf(c.z, dpix2, fmaf(c.y, dpix1, c.x * dpix0));
-                        const float diff = cd - adot;
-                        // backward.cu:512-529 (kbg = 0: fmaf(diff, T, -0) is diff * T, bit for bit)
-                        const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
-                        qa[sb * kBwdBatch + u][lane] = make_float2(og * dL_dalpha, alpha * T);
-                        adot = fmaf(alpha, diff, adot);
-                    }
-                }
-                if (!any_m) continue;  // wave-uniform: no pixel took any of these records
-                wave_lds_handoff();
-                // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
-                // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i sits at (x0 + i, y0),
-                // x0 = qx0 + 4 (g & 1), y0 = qy0 + (g >> 1); relative to the record's mean ex = x0 - mx, ey = y0 - my.
-                // With S0 = sum v, X1 = sum v i, X2 = sum v i^2 (constant offsets i): sum v (x - mx) = ex S0 + X1,
-                // sum v (x - mx)^2 = ex (ex S0 + X1) + ex X1 + X2, the y sums from the lane's constant ey, and
-                // C = sum w dL/dpixel.  The reference's dx = mx - x (backward.cu:545-554) flips the first moments' sign
-                // (the flush).  19 VALU ops for the four pixels' sums instead of 27, and no per-pixel offsets.  (Raw
-                // tile-local moments centred only in the flush need no record read here, but the centring cancels:
-                // the float-atomic order noise of the sums grew to ~1e-4 relative.)
-                const int r = lane & 3, grp = lane >> 2;
-                static_assert(kBwdGroup == kBwdBatch, "phase 2 reads the group's slots from phase 1's list word");
-                const int rs = list_slot(w4, r, j0, m);
-                const float4 mrec = s_pc[rs];
-                const float2 q0 = qa[r][4 * grp], q1 = qa[r][4 * grp + 1], q2 = qa[r][4 * grp + 2],
-                             q3 = qa[r][4 * grp + 3];
-                float S0, Mx, Mxx, My, Mxy, Myy, C0, C1, C2;
-                {
+                        {
 #pragma clang fp contract(fast)
-                    const float ex = ph2_x0 - mrec.x, ey = ph2_y0 - mrec.y;
-                    S0 = (q0.x + q1.x) + (q2.x + q3.x);
-                    const float X1 = fmaf(3.f, q3.x, fmaf(2.f, q2.x, q1.x));  // sum v i
-                    const float X2 = fmaf(9.f, q3.x, fmaf(4.f, q2.x, q1.x));  // sum v i^2
-                    Mx = fmaf(ex, S0, X1);                                      // sum v (x - mx)
-                    Mxx = fmaf(ex, Mx + X1, X2);                                // sum v (x - mx)^2
-                    My = ey * S0;
-                    Myy = ey * My;
-                    Mxy = ey * Mx;
-                    C0 = fmaf(q3.y, dpq[3].x, fmaf(q2.y, dpq[2].x, fmaf(q1.y, dpq[1].x, q0.y * dpq[0].x)));
-                    C1 = fmaf(q3.y, dpq[3].y, fmaf(q2.y, dpq[2].y, fmaf(q1.y, dpq[1].y, q0.y * dpq[0].y)));
-                    C2 = fmaf(q3.y, dpq[3].z, fmaf(q2.y, dpq[2].z, fmaf(q1.y, dpq[1].z, q0.y * dpq[0].z)));
-                }
-                // the nine sums in s_acc order, summed over the 16 groups g (lane bits 5, 4 transposed; bits 3, 2
-                // by row rotations): afterwards lane 4 g + r with bits 2-3 clear holds record r's total of quantity
-                // (bit 5) + 2 (bit 4) [+ 4 for c1, 8 for c2]
-                const float c0 = sum4(sum8(pair16(pair32(Mx, My), pair32(Mxx, Mxy))));
-                const float c1 = sum4(sum8(pair16(pair32(Myy, S0), pair32(C0, C1))));
-                const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
-                wave_lds_handoff();  // phase-1 writes of the next group must stay behind these reads
-                if (!(lane & 12) && j0 + r < m) {
-                    const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
-                    atomicAdd(&s_acc[qk][rs], c0);
-                    atomicAdd(&s_acc[4 + qk][rs], c1);
-                    if (qk == 0) atomicAdd(&s_acc[8][rs], c2);
-                }
+                            const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
+                            // one select: o G zeroed where the lane skips the record gives alpha = 0 (T unchanged)
+                            // and a zero hand-off; the hand-off carries q = o G dL/dalpha
+                            const float og = valid ? OG : 0.f;
+                            const float alpha = fminf(0.99f, og);
+                            const float inv1ma = fast_recip(1.f - alpha);
+                            T = T * inv1ma;  // backward.cu:503 (T recovered by division)
+                            const float cd = fmaf(row_bcast<U>(rrgb.z), dpix2,
+                                                  fmaf(row_bcast<U>(rrgb.y), dpix1, row_bcast<U>(rrgb.x) * dpix0));
+                            const float diff = cd - adot;
+                            // backward.cu:512-529 (kbg = 0: fmaf(diff, T, -0) is diff * T, bit for bit)
+                            const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
+                            qa[U & 3][lane] = make_float2(og * dL_dalpha, alpha * T);
+                            adot = fmaf(alpha, diff, adot);
+                        }
+                    };
+                    rec(std::integral_constant<int, 0>{});
+                    rec(std::integral_constant<int, 1>{});
+                    rec(std::integral_constant<int, 2>{});
+                    rec(std::integral_constant<int, 3>{});
+                    if (!any_m) return;  // wave-uniform: no pixel took any of these records
+                    wave_lds_handoff();
+                    // Phase 2 (record-major): lane 4 g + r sums record r over pixels 4 g + i, i = 0..3 -- the lanes of
+                    // its own quad, whose dL/dpixel were broadcast into dpq once.  Pixel 4 g + i sits at (x0 + i,
+                    // y0), x0 = qx0 + 4 (g & 1), y0 = qy0 + (g >> 1); relative to the record's mean ex = x0 - mx,
+                    // ey = y0 - my.  With S0 = sum v, X1 = sum v i, X2 = sum v i^2 (constant offsets i):
+                    // sum v (x - mx) = ex S0 + X1, sum v (x - mx)^2 = ex (ex S0 + X1) + ex X1 + X2, the y sums from
+                    // the lane's constant ey, and C = sum w dL/dpixel.  The reference's dx = mx - x
+                    // (backward.cu:545-554) flips the first moments' sign (the flush).  19 VALU ops for the four
+                    // pixels' sums instead of 27, and no per-pixel offsets.  (Raw tile-local moments centred only
+                    // in the flush need no record read here, but the centring cancels: the float-atomic order noise
+                    // of the sums grew to ~1e-4 relative.)
+                    const float2 q0 = qa[r][4 * grp], q1 = qa[r][4 * grp + 1], q2 = qa[r][4 * grp + 2],
+                                 q3 = qa[r][4 * grp + 3];
+                    float S0, Mx, Mxx, My, Mxy, Myy, C0, C1, C2;
+                    {
+#pragma clang fp contract(fast)
+                        const float ex = ph2_x0 - mrec.x, ey = ph2_y0 - mrec.y;
+                        S0 = (q0.x + q1.x) + (q2.x + q3.x);
+                        const float X1 = fmaf(3.f, q3.x, fmaf(2.f, q2.x, q1.x));  // sum v i
+                        const float X2 = fmaf(9.f, q3.x, fmaf(4.f, q2.x, q1.x));  // sum v i^2
+                        Mx = fmaf(ex, S0, X1);                                      // sum v (x - mx)
+                        Mxx = fmaf(ex, Mx + X1, X2);                                // sum v (x - mx)^2
+                        My = ey * S0;
+                        Myy = ey * My;
+                        Mxy = ey * Mx;
+                        C0 = fmaf(q3.y, dpq[3].x, fmaf(q2.y, dpq[2].x, fmaf(q1.y, dpq[1].x, q0.y * dpq[0].x)));
+                        C1 = fmaf(q3.y, dpq[3].y, fmaf(q2.y, dpq[2].y, fmaf(q1.y, dpq[1].y, q0.y * dpq[0].y)));
+                        C2 = fmaf(q3.y, dpq[3].z, fmaf(q2.y, dpq[2].z, fmaf(q1.y, dpq[1].z, q0.y * dpq[0].z)));
+                    }
+                    // the nine sums in s_acc order, summed over the 16 groups g (lane bits 5, 4 transposed; bits 3,
+                    // 2 by row rotations): afterwards lane 4 g + r with bits 2-3 clear holds record r's total of
+                    // quantity (bit 5) + 2 (bit 4) [+ 4 for c1, 8 for c2]
+                    const float c0 = sum4(sum8(pair16(pair32(Mx, My), pair32(Mxx, Mxy))));
+                    const float c1 = sum4(sum8(pair16(pair32(Myy, S0), pair32(C0, C1))));
+                    const float c2 = sum4(sum8(pair16(pair32(C2, 0.f), 0.f)));
+                    wave_lds_handoff();  // phase-1 writes of the next hand-off must stay behind these reads
+                    if (!(lane & 12) && K + r < nv) {
+                        const int qk = ((lane >> 5) & 1) + ((lane >> 3) & 2);
+                        atomicAdd(&s_acc[qk][rs], c0);
+                        atomicAdd(&s_acc[4 + qk][rs], c1);
+                        if (qk == 0) atomicAdd(&s_acc[8][rs], c2);
+                    }
+                };
+                hand_off(std::integral_constant<int, 0>{});
+                if (nv > 4) hand_off(std::integral_constant<int, 4>{});
+                if (nv > 8) hand_off(std::integral_constant<int, 8>{});
+                if (nv > 12) hand_off(std::integral_constant<int, 12>{});
             }
         };
         if (any_bg)
@@ -580,297 +587,11 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     }
 }
 
-// ---- the backward with one record list per 4x4 pixel block (round 3) ----
-// The 8x8 quadrant of a wave is four 4x4 blocks, one per 16-lane DPP row (the forward's lane map).  Each block
-// walks its own compacted list of the batch's records (exact ellipse test against the quadrant, alpha box against
-// the block), all four side by side: a record whose box misses a block no longer occupies its lanes.  The lists'
-// records are not wave-uniform, so instead of per-lane LDS reads every record's fields are loaded ONCE into the
-// registers of one lane of its row -- lane u of row g holds record j0 + u of block g's list, 16 records per row
-// per step -- and broadcast to the row by DPP row_newbcast:u, which the compiler folds into the consuming VALU op
-// (v_sub_f32_dpp ... row_newbcast:u): the record reads cost nothing in the inner loop.  The hand-off to the
-// record-major sums works per row: lane (g, 4 r + i) sums record r of the hand-off over the four pixels of block
-// row i, the four block rows are combined by a transposed quad butterfly (quad_perm), and three LDS atomics per
-// lane add the nine sums into the workgroup's accumulators.
-template <int U>
-__device__ __forceinline__ float row_bcast(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + U, 0xf, 0xf, false));
-}
-template <int U>
-__device__ __forceinline__ int row_bcast_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x150 + U, 0xf, 0xf, false);
-}
-// transposed step over lane bit 0 (quad_perm [1,0,3,2]) / bit 1 (quad_perm [2,3,0,1]): lanes with the bit clear
-// return a summed over the lane pair, lanes with it set return b summed over the pair
-template <int CTRL>
-__device__ __forceinline__ float quad_pair(float a, float b, bool bit) {
-    const float keep = bit ? b : a, send = bit ? a : b;
-    return keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ float quad_add(float a) {
-    return a + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), CTRL, 0xf, 0xf, false));
-}
-
-__global__ __launch_bounds__(256) void k_render_bwd_grp(RenderBwdParams p) {
-    __shared__ uint32_t s_id[kTilePix];
-    __shared__ float4 s_pc[kTilePix];   // stage_pc: mx, my, -a/2, -c/2
-    __shared__ float4 s_bo[kTilePix];   // b, o, ellipse threshold, 1 / a
-    __shared__ float4 s_rgb[kTilePix];  // r, g, b, 1 / c
-    __shared__ float s_acc[9][kTilePix + 1];
-    __shared__ __attribute__((aligned(4))) uint8_t s_list[4][4][kTilePix];   // [wave][block]
-    __shared__ union {
-        float4 box[kTilePix];
-        float2 qa[4][4][4][16];   // [wave][block][record of the hand-off][pixel]
-    } s_u;
-    __shared__ int s_tile_lc;
-    float4* s_box = s_u.box;
-    const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);   // the forward's 4x4-block lane map
-    const int tid = threadIdx.x, lane = tg.lane, grp = lane >> 4, u_l = lane & 15;
-    const uint2 rg = p.ranges[tg.tile];
-    const int pid = p.W * tg.py + tg.px;
-    const int plane = p.H * p.W;
-    const bool inside = tg.inside;
-    const float T_final = inside ? p.final_T[pid] : 0.f;
-    float T = T_final;
-    const int last_contributor = inside ? (int)p.n_contrib[pid] : 0;
-    // largest last contributor of the row (block), of the wave, of the tile
-    int row_lc = last_contributor;
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) row_lc = max(row_lc, __shfl_xor(row_lc, off));
-    int wave_lc = max(row_lc, __shfl_xor(row_lc, 16));
-    wave_lc = max(wave_lc, __shfl_xor(wave_lc, 32));
-    const int blk_lc[4] = {__builtin_amdgcn_readlane(row_lc, 0), __builtin_amdgcn_readlane(row_lc, 16),
-                           __builtin_amdgcn_readlane(row_lc, 32), __builtin_amdgcn_readlane(row_lc, 48)};
-    if (tid == 0) s_tile_lc = 0;
-    lds_barrier();
-    if (lane == 0) atomicMax(&s_tile_lc, wave_lc);
-    lds_barrier();
-    const int total = min((int)(rg.y - rg.x), s_tile_lc);
-    const uint32_t end = rg.x + (uint32_t)total;
-    const int rounds = (total + kTilePix - 1) / kTilePix;
-    int toDo = total;
-    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
-    if (inside) {
-        dpix0 = p.dL_dpix[pid];
-        dpix1 = p.dL_dpix[plane + pid];
-        dpix2 = p.dL_dpix[2 * plane + pid];
-    }
-    // phase 2: lane (g, 4 r + i) sums block row i = u_l & 3 of its block: pixels (bx0 + j, by0 + i), j = 0..3 --
-    // the lanes 4 i + j of its row, whose dL/dpixel it holds from here on
-    const int p2_i = u_l & 3, p2_r = u_l >> 2;
-    const float bx0 = tg.qx0 + (float)((grp & 1) * 4), by0 = tg.qy0 + (float)((grp >> 1) * 4);
-    float3 dpq[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int x = (int)bx0 + j, y = (int)by0 + p2_i;
-        const bool in = x < p.W && y < p.H;
-        const int q = p.W * y + x;
-        dpq[j] = in ? make_float3(p.dL_dpix[q], p.dL_dpix[plane + q], p.dL_dpix[2 * plane + q])
-                    : make_float3(0.f, 0.f, 0.f);
-    }
-    float adot = 0.f;
-    const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
-    const float kbg = -T_final * bg_dot;
-    const bool any_bg = wave_ballot(kbg != 0.f) != 0;
-    const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
-    const float pxf = (float)tg.px, pyf = (float)tg.py;
-    uint8_t(*lists)[kTilePix] = s_list[tg.wave];
-    float2(*qa)[4][16] = s_u.qa[tg.wave];
-
-    for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
-        lds_barrier();
-        const int progress = i * kTilePix + tid;
-        if (progress < total) {  // loaded back to front (backward.cu:466-478)
-            const uint32_t g = p.point_list[end - progress - 1];
-            const RenderRec* r = p.rec + g;
-            const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
-            s_id[tid] = g;
-            s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
-            s_bo[tid] = make_float4(q0.w, q1.y, q2.y, q2.z);
-            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q2.w);
-            s_box[tid] = r->box;
-        }
-#pragma unroll
-        for (int q = 0; q < 9; ++q) s_acc[q][tid] = 0.f;
-        lds_barrier();
-        const int n = min(kTilePix, toDo);
-        const int front_base = total - 1 - i * kTilePix;
-        // compaction: the quadrant's exact ellipse test once per record, then each block's alpha box and its
-        // last-contributor cut (slot t is list position front_base - t: kept iff t > front_base - block lc)
-        int len[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < kTilePix / 64; ++k) {
-            const int t = k * 64 + lane;
-            bool hit = false;
-            float4 bx = make_float4(1e30f, -1e30f, 1e30f, -1e30f);
-            if (t < n && t > front_base - wave_lc) {
-                bx = s_box[t];
-                hit = bx.y >= tg.qx0 && bx.x <= tg.qx0 + 7.f && bx.w >= tg.qy0 && bx.z <= tg.qy0 + 7.f;
-                if (hit) {
-                    const float4 pc = s_pc[t];
-                    const float4 bo = s_bo[t];
-                    const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);
-                    const float det = co.x * co.z - co.y * co.y;
-                    if (co.x > 0.f && co.z > 0.f && det > 0.f)
-                        hit = ellipse_meets_rect(make_float2(pc.x, pc.y), co, bo.z, bo.w, s_rgb[t].w, tg.qx0,
-                                                 tg.qx0 + 7.f, tg.qy0, tg.qy0 + 7.f);
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float x0 = tg.qx0 + (float)((g & 1) * 4), y0 = tg.qy0 + (float)((g >> 1) * 4);
-                const bool h = hit && t > front_base - blk_lc[g] && bx.y >= x0 && bx.x <= x0 + 3.f && bx.w >= y0 &&
-                               bx.z <= y0 + 3.f;
-                const unsigned long long b = wave_ballot(h);
-                if (h)
-                    lists[g][len[g] + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))] = (uint8_t)t;
-                len[g] += __popcll(b);
-            }
-        }
-        wave_lds_handoff();
-        lds_barrier();  // every wave is done with s_box before s_u.qa is written
-        const int m_max = max(max(len[0], len[1]), max(len[2], len[3]));
-        const int my_len = grp == 0 ? len[0] : (grp == 1 ? len[1] : (grp == 2 ? len[2] : len[3]));
-        const int slot_min = front_base - last_contributor;  // slot t counts for this pixel iff t > slot_min
-        auto walk = [&](auto with_bg) {
-            constexpr bool kBg = decltype(with_bg)::value;
-            for (int j0 = 0; j0 < m_max; j0 += 16) {
-                // lane (g, u) loads record j0 + u of block g's list (slot 0 past the list: finite, never taken)
-                const int nv = my_len - j0;   // records of this block at j0 .. (row-uniform)
-                const int rslot = u_l < nv ? (int)lists[grp][j0 + u_l] : 0;
-                const float4 rpc = s_pc[rslot];
-                const float4 rbo = s_bo[rslot];
-                const float4 rrgb = s_rgb[rslot];
-#pragma unroll
-                for (int k = 0; k < 16; k += 4) {
-                    if (j0 + k >= m_max) break;   // wave-uniform
-                    unsigned long long any_m = 0;
-                    auto rec = [&](auto uc) {
-                        constexpr int U = decltype(uc)::value;
-                        constexpr int uu = U & 3;
-                        const float4 pc = make_float4(row_bcast<U>(rpc.x), row_bcast<U>(rpc.y), row_bcast<U>(rpc.z),
-                                                      row_bcast<U>(rpc.w));
-                        const float2 bo = make_float2(row_bcast<U>(rbo.x), row_bcast<U>(rbo.y));
-                        const int sl = row_bcast_i<U>(rslot);
-                        float G;
-                        bool keep;
-                        record_alpha(pc, bo, pxf, pyf, G, keep);
-                        const float OG = bo.y * G;
-                        const unsigned long long valid_m = wave_ballot(U < nv) & wave_ballot(sl > slot_min) &
-                                                           wave_ballot(keep) & wave_ballot(!(OG < 1.0f / 255.0f));
-                        any_m |= valid_m;
-                        {
-#pragma clang fp contract(fast)
-                            const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
-                            const float og = valid ? OG : 0.f;
-                            const float alpha = fminf(0.99f, og);
-                            const float inv1ma = fast_recip(1.f - alpha);
-                            T = T * inv1ma;  // backward.cu:503
-                            const float cd = fmaf(row_bcast<U>(rrgb.z), dpix2,
-                                                  fmaf(row_bcast<U>(rrgb.y), dpix1, row_bcast<U>(rrgb.x) * dpix0));
-                            const float diff = cd - adot;
-                            const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
-                            qa[grp][uu][u_l] = make_float2(og * dL_dalpha, alpha * T);
-                            adot = fmaf(alpha, diff, adot);
-                        }
-                    };
-                    // (U is a compile-time constant: the DPP control of each broadcast)
-                    if (k == 0) {
-                        rec(std::integral_constant<int, 0>{}); rec(std::integral_constant<int, 1>{});
-                        rec(std::integral_constant<int, 2>{}); rec(std::integral_constant<int, 3>{});
-                    } else if (k == 4) {
-                        rec(std::integral_constant<int, 4>{}); rec(std::integral_constant<int, 5>{});
-                        rec(std::integral_constant<int, 6>{}); rec(std::integral_constant<int, 7>{});
-                    } else if (k == 8) {
-                        rec(std::integral_constant<int, 8>{}); rec(std::integral_constant<int, 9>{});
-                        rec(std::integral_constant<int, 10>{}); rec(std::integral_constant<int, 11>{});
-                    } else {
-                        rec(std::integral_constant<int, 12>{}); rec(std::integral_constant<int, 13>{});
-                        rec(std::integral_constant<int, 14>{}); rec(std::integral_constant<int, 15>{});
-                    }
-                    if (!any_m) continue;   // wave-uniform: no pixel took any of these records
-                    wave_lds_handoff();
-                    // Phase 2: lane (g, 4 r + i) -- record r = p2_r of the hand-off, block row i = p2_i
-                    const bool rvalid = k + p2_r < nv;
-                    const int rs = rvalid ? (int)lists[grp][j0 + k + p2_r] : 0;
-                    const float4 mrec = s_pc[rs];
-                    const float4 qv01 = *reinterpret_cast<const float4*>(&qa[grp][p2_r][4 * p2_i]);
-                    const float4 qv23 = *reinterpret_cast<const float4*>(&qa[grp][p2_r][4 * p2_i + 2]);
-                    float Q[9];
-                    {
-#pragma clang fp contract(fast)
-                        const float ex = bx0 - mrec.x, ey = by0 + (float)p2_i - mrec.y;
-                        const float v0 = qv01.x, v1 = qv01.z, v2 = qv23.x, v3 = qv23.z;
-                        const float w0 = qv01.y, w1 = qv01.w, w2 = qv23.y, w3 = qv23.w;
-                        const float S0 = (v0 + v1) + (v2 + v3);
-                        const float X1 = fmaf(3.f, v3, fmaf(2.f, v2, v1));
-                        const float X2 = fmaf(9.f, v3, fmaf(4.f, v2, v1));
-                        const float Mx = fmaf(ex, S0, X1);
-                        Q[0] = Mx;
-                        Q[1] = ey * S0;
-                        Q[2] = fmaf(ex, Mx + X1, X2);
-                        Q[3] = ey * Mx;
-                        Q[4] = ey * Q[1];
-                        Q[5] = S0;
-                        Q[6] = fmaf(w3, dpq[3].x, fmaf(w2, dpq[2].x, fmaf(w1, dpq[1].x, w0 * dpq[0].x)));
-                        Q[7] = fmaf(w3, dpq[3].y, fmaf(w2, dpq[2].y, fmaf(w1, dpq[1].y, w0 * dpq[0].y)));
-                        Q[8] = fmaf(w3, dpq[3].z, fmaf(w2, dpq[2].z, fmaf(w1, dpq[1].z, w0 * dpq[0].z)));
-                    }
-                    wave_lds_handoff();  // phase-1 writes of the next hand-off stay behind these reads
-                    const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0;
-                    const float R0 = quad_pair<0xb1>(Q[0], Q[1], b0), R1 = quad_pair<0xb1>(Q[2], Q[3], b0);
-                    const float R2 = quad_pair<0xb1>(Q[4], Q[5], b0), R3 = quad_pair<0xb1>(Q[6], Q[7], b0);
-                    const float R4 = quad_add<0xb1>(Q[8]);
-                    const float S_0 = quad_pair<0x4e>(R0, R1, b1), S_1 = quad_pair<0x4e>(R2, R3, b1);
-                    const float S_2 = quad_add<0x4e>(R4);
-                    if (rvalid) {   // lane (b1, b0) holds quantities 2 b1 + b0 and 4 + 2 b1 + b0; every lane the 9th
-                        const int qk = (b1 ? 2 : 0) + (b0 ? 1 : 0);
-                        atomicAdd(&s_acc[qk][rs], S_0);
-                        atomicAdd(&s_acc[4 + qk][rs], S_1);
-                        if (qk == 0) atomicAdd(&s_acc[8][rs], S_2);
-                    }
-                }
-            }
-        };
-        if (any_bg)
-            walk(std::true_type{});
-        else
-            walk(std::false_type{});
-        lds_barrier();
-        if (tid < n) {  // finish record tid's sums in place (as k_render_bwd)
-            const float4 pc = s_pc[tid];
-            const float2 bo = *reinterpret_cast<const float2*>(&s_bo[tid]);
-            const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);
-            const float o = co.w;
-            const float m0 = -s_acc[0][tid], m1 = -s_acc[1][tid];
-            s_acc[0][tid] = (co.x * m0 + co.y * m1) * -ddelx_dx;
-            s_acc[1][tid] = (co.z * m1 + co.y * m0) * -ddely_dy;
-            s_acc[2][tid] *= -0.5f;
-            s_acc[3][tid] *= -0.5f;
-            s_acc[4][tid] *= -0.5f;
-            s_acc[5][tid] = o > 0.f ? s_acc[5][tid] / o : 0.f;
-        }
-        lds_barrier();
-        for (int e = tid; e < n * kRecUsed; e += kTilePix) {
-            const int r = e / kRecUsed, q = e - kRecUsed * r;
-            const float a = s_acc[q][r];
-            if (a != 0.f) atomicAdd(p.grad_rec + (size_t)s_id[r] * kGradRec + q, a);
-        }
-    }
-}
-
 void launch_render_fwd(const RenderParams& p, hipStream_t s) {
     if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_fwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 }
 void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
-    static const bool quadrant = [] {   // GSD_BWD_QUADRANT=1: the per-quadrant-list backward (k_render_bwd)
-        const char* e = getenv("GSD_BWD_QUADRANT");
-        return e && atoi(e) == 1;
-    }();
-    if (p.num_tiles <= 0) return;
-    if (quadrant) hipLaunchKernelGGL(k_render_bwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
-    else hipLaunchKernelGGL(k_render_bwd_grp, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+    if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 }
 
 }  // namespace gsd
