@@ -68,12 +68,15 @@ __device__ __forceinline__ bool ellipse_meets_rect(float2 xy, float4 co, float t
 // bench scene; the forward, cheaper per record and early-terminating, loses more to
 // the extra test than it saves).  Returns the count.
 // Slots below t_min are skipped too (the backward's last-contributor bound).
-template <bool kExact, int RW = 8, int RH = 8>
+// With kCount, *below returns per lane how many list entries have a slot <= t_cut (the lane's own bound): the
+// list is in slot order, so the entries with a larger slot are exactly those at list index >= *below.
+template <bool kExact, int RW = 8, int RH = 8, bool kCount = false>
 __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
                                             const float4* __restrict__ s_bo, const float4* __restrict__ s_rgb,
                                             uint8_t* __restrict__ s_list, int n, float qx0, float qy0, int lane,
-                                            int t_min = 0) {
+                                            int t_min = 0, int t_cut = 0, int* below_cut = nullptr) {
     int m = 0;
+    int cnt = 0;
 #pragma unroll
     for (int k = 0; k < kTilePix / 64; ++k) {
         const int t = k * 64 + lane;
@@ -98,8 +101,14 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
             const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
             s_list[m + below] = (uint8_t)t;
         }
+        if (kCount) {  // hits among slots k*64 .. t_cut: the mask's lowest clamp(t_cut - 64 k + 1, 0, 64) bits
+            const int nb = min(max(t_cut - k * 64 + 1, 0), 64);
+            const unsigned long long le = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
+            cnt += __popcll(mask & le);
+        }
         m += __popcll(mask);
     }
+    if (kCount) *below_cut = cnt;
     wave_lds_handoff();
     return m;
 }
@@ -439,11 +448,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         const int n = min(kTilePix, toDo);
         // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
         const int front_base = total - 1 - i * kTilePix;
-        const int m = wave_compact<true>(s_box, s_pc, s_bo, s_rgb, list, n, tg.qx0, tg.qy0, lane,
-                                         front_base - wave_lc + 1);
+        // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor, i.e.
+        // slot t counts for this pixel iff t > front_base - last_contributor: iff its list index >= first_valid
+        int first_valid;
+        const int m = wave_compact<true, 8, 8, true>(s_box, s_pc, s_bo, s_rgb, list, n, tg.qx0, tg.qy0, lane,
+                                                     front_base - wave_lc + 1, front_base - last_contributor,
+                                                     &first_valid);
         lds_barrier();  // every wave is done with s_box before s_u.qa is written
-        // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor
-        const int slot_min = front_base - last_contributor;  // slot t counts for this pixel iff t > slot_min
         // the group loop twice: with the background term of dL/dalpha and, where it is 0 for every pixel of
         // the wave (a black background: the default of train.py), without its multiply-add
         auto walk = [&](auto with_bg) {
@@ -481,7 +492,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                         // backward.cu:487-488 (list position below the pixel's last contributor); alpha =
                         // min(0.99, o G) >= 1/255 <=> !(o G < 1/255), NaN included (fminf(0.99, NaN) = 0.99)
                         const unsigned long long valid_m = (U < nv ? ~0ull : 0ull) &
-                                                           wave_ballot(row_bcast_i<U>(rslot) > slot_min) &
+                                                           wave_ballot(j0 + U >= first_valid) &
                                                            wave_ballot(keep) & wave_ballot(!(OG < 1.0f / 255.0f));
                         any_m |= valid_m;
                         {
