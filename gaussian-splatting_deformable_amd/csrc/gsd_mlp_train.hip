@@ -194,7 +194,8 @@ template <int MODE, int RB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_gemm(MlpGemmParams p) {
     constexpr int NF = RB * 3 * 64;               // 16-B fragments per k-step
     constexpr int PER = (NF + 255) / 256;         // per thread
-    __shared__ bf16x8 s_a[2][NF];
+    __shared__ bf16x8 s_a[2][PER * 256];   // padded to whole thread rows: the staging needs no per-thread guard
+    __shared__ __attribute__((aligned(16))) float s_t[4][32][36];   // epilogue: a wave's 32 x 32 block, transposed
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
     const int g = blockIdx.x * 128 + wave * 32 + c;   // always < ldp
     const int KS = p.ks0 + p.ks1;
@@ -204,90 +205,140 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     f32x16 acc[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) acc[r] = f32x16{};
-    bf16x8 stage[PER];
+    // backward: the forward's ReLU bits, one 16-bit word per row block, loaded now (their HBM latency behind the
+    // main loop rather than in front of the epilogue)
+    unsigned bits_in[RB];
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
-        if (tid + 256 * i < NF) s_a[0][tid + 256 * i] = F[tid + 256 * i];   // k-step 0's RB x 3 x 64 run
-    // X^T fragments kXDepth k-steps ahead (a ring of registers, rotated by copies the compiler renames away)
+    for (int r = 0; r < RB; ++r) {
+        bits_in[r] = 0xffffu;
+        if (MODE == kMlpBwdMask && p.mask_in) {
+            const int rm = rb0 + r - p.n_a / 32;
+            if (rm >= 0) bits_in[r] = p.mask_in[(size_t)(rm * 2 + h) * p.ldp + g];
+        }
+    }
+    bf16x8 stage[2][PER];   // A fragments two k-steps ahead: set u & 1 holds k-step ks + 2 (ks = ks0 + u)
+    // Every load below is unconditional, from a clamped index or k-step: divergent or data-dependent branches
+    // around the loads made the compiler's counter bookkeeping give up (vmcnt(0) before each use).
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s_a[0][tid + 256 * i] = F[min(tid + 256 * i, NF - 1)];   // k-step 0's fragments
+#pragma unroll
+    for (int i = 0; i < PER; ++i) stage[1][i] = F[(size_t)min(1, KS - 1) * kstride + min(tid + 256 * i, NF - 1)];
+    // X^T fragments kXDepth k-steps ahead in a ring of registers.  The k-loop is unrolled by the ring's depth so
+    // that slot u is always the same registers: a ring rotated by copies made every step wait for ALL of its
+    // outstanding loads (vmcnt(0): the copy reads the registers the newest loads target), which left the loads one
+    // step ahead instead of four and 58 % of the wave-cycles parked on s_waitcnt.
     constexpr int kXDepth = 4;
     float xq[kXDepth][8];
 #pragma unroll
-    for (int d = 0; d < kXDepth; ++d)
-        if (d < KS) load_x8(p, d, h, g, xq[d]);
+    for (int d = 0; d < kXDepth; ++d) load_x8(p, min(d, KS - 1), h, g, xq[d]);
     __syncthreads();
-    for (int ks = 0; ks < KS; ++ks) {
-        const int buf = ks & 1;
-        if (ks + 1 < KS) {   // the next k-step's fragments into registers (written to LDS after the MFMAs)
-            const bf16x8* src = F + (size_t)(ks + 1) * kstride;
+    for (int ks0 = 0; ks0 < KS; ks0 += kXDepth) {
 #pragma unroll
-            for (int i = 0; i < PER; ++i)
-                if (tid + 256 * i < NF) stage[i] = src[tid + 256 * i];
-        }
-        const Split8 b = split8(xq[0]);
+        for (int u = 0; u < kXDepth; ++u) {
+            const int ks = ks0 + u;
+            if (ks >= KS) break;   // wave-uniform: the tail of a depth not dividing KS
+            const int buf = ks & 1;
+            {   // k-step ks + 2's fragments into registers (ks + 1's, loaded a step ago, go to LDS after the
+                // MFMAs; past the end: re-reads, never used)
+                const bf16x8* src = F + (size_t)min(ks + 2, KS - 1) * kstride;
 #pragma unroll
-        for (int d = 0; d + 1 < kXDepth; ++d)
+                for (int i = 0; i < PER; ++i) stage[u & 1][i] = src[min(tid + 256 * i, NF - 1)];
+            }
+            const Split8 b = split8(xq[u]);
+            load_x8(p, min(ks + kXDepth, KS - 1), h, g, xq[u]);   // (past the end: a re-read, never used)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xq[d][j] = xq[d + 1][j];
-        if (ks + kXDepth < KS) load_x8(p, ks + kXDepth, h, g, xq[kXDepth - 1]);
+            for (int r = 0; r < RB; ++r) {
+                Split8 a;
+                a.hi = s_a[buf][(r * 3) * 64 + lane];
+                a.mid = s_a[buf][(r * 3 + 1) * 64 + lane];
+                a.lo = s_a[buf][(r * 3 + 2) * 64 + lane];
+                acc[r] = mfma_x6(a, b, acc[r]);
+            }
 #pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            Split8 a;
-            a.hi = s_a[buf][(r * 3) * 64 + lane];
-            a.mid = s_a[buf][(r * 3 + 1) * 64 + lane];
-            a.lo = s_a[buf][(r * 3 + 2) * 64 + lane];
-            acc[r] = mfma_x6(a, b, acc[r]);
-        }
-        if (ks + 1 < KS) {
-#pragma unroll
-            for (int i = 0; i < PER; ++i)
-                if (tid + 256 * i < NF) s_a[buf ^ 1][tid + 256 * i] = stage[i];
-        }
-        __syncthreads();
-    }
-    // accumulator register q of row block r: row n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g
-    unsigned bits_in[RB];
-    if (MODE == kMlpBwdMask && p.mask_in) {   // the forward's ReLU bits, one 16-bit word per row block
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            const int rm = rb0 + r - p.n_a / 32;
-            bits_in[r] = rm >= 0 ? p.mask_in[(size_t)(rm * 2 + h) * p.ldp + g] : 0xffffu;
+            for (int i = 0; i < PER; ++i) s_a[buf ^ 1][tid + 256 * i] = stage[(u + 1) & 1][i];
+            __syncthreads();
         }
     }
+    // accumulator register q of row block r: row n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g.
+    // The hidden-row epilogues (forward ReLU, backward mask) go out through LDS: the wave writes its 32 x 32 block
+    // transposed into s_t and stores each row's 32 Gaussians as 16-B pieces -- four 1-KB store instructions per
+    // block instead of sixteen 256-B ones (the one-dword stores were store-issue bound: 30 % of the forward GEMM's
+    // time, 44 % of the backward's).
+    const int g0 = blockIdx.x * 128 + wave * 32;    // the wave's first Gaussian
+    const int srow = lane >> 3, scol = 4 * (lane & 7);   // the transposed read: rows srow + 8 i, columns scol..+3
+    float(*st)[36] = s_t[wave];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-        unsigned bits_out = 0;
-        float bias[16];
-        if (MODE != kMlpBwdMask) {   // rows 32 r + 8 j + 4 h .. + 3 are consecutive: one 16-B load per (r, j)
+        const int nb = 32 * (rb0 + r);   // the block's first row
+        if (MODE == kMlpFwdHeads) {      // (P, n_out) row-major per Gaussian: 58 floats, written as is
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + 32 * (rb0 + r) + 8 * j + 4 * h);
-                bias[4 * j] = b4.x; bias[4 * j + 1] = b4.y; bias[4 * j + 2] = b4.z; bias[4 * j + 3] = b4.w;
-            }
-        }
+                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + nb + 8 * j + 4 * h);
+                const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int n = 32 * (rb0 + r) + 8 * (q >> 2) + 4 * h + (q & 3);
-            const float a = acc[r][q];
-            if (MODE == kMlpFwdRelu) {
-                const float y = fmaxf(a + bias[q], 0.f);
-                p.dst[(size_t)n * p.ldp + g] = y;
-                bits_out |= (y > 0.f ? 1u : 0u) << q;
-            } else if (MODE == kMlpFwdHeads) {
-                if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = a + bias[q];
-            } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
-                if (n < p.n_a) {
-                    float* d = p.dst_a + (size_t)n * p.ldp + g;
-                    *d = p.accumulate_a ? *d + a : a;
-                } else if (p.mask_in) {
-                    p.dst[(size_t)(n - p.n_a) * p.ldp + g] = (bits_in[r] >> q) & 1u ? a : 0.f;   // threshold_backward
-                } else if (p.mask) {
-                    const size_t o = (size_t)(n - p.n_a) * p.ldp + g;
-                    p.dst[o] = p.mask[o] > 0.f ? a : 0.f;   // threshold_backward(g, h, 0)
+                for (int i = 0; i < 4; ++i) {
+                    const int n = nb + 8 * j + 4 * h + i;
+                    if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = acc[r][4 * j + i] + bq[i];
                 }
             }
+            continue;
         }
-        if (MODE == kMlpFwdRelu && p.mask_out)
-            p.mask_out[(size_t)((rb0 + r) * 2 + h) * p.ldp + g] = (unsigned short)bits_out;
+        float v[16];
+        if (MODE == kMlpFwdRelu) {
+            unsigned bits_out = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + nb + 8 * j + 4 * h);
+                const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float y = fmaxf(acc[r][4 * j + i] + bq[i], 0.f);
+                    v[4 * j + i] = y;
+                    bits_out |= (y > 0.f ? 1u : 0u) << (4 * j + i);
+                }
+            }
+            if (p.mask_out) p.mask_out[(size_t)((rb0 + r) * 2 + h) * p.ldp + g] = (unsigned short)bits_out;
+        } else {   // backward: rows < n_a -> the encoding's gradient (no ReLU), the rest masked by h
+            const bool enc_rows = nb < p.n_a;   // n_a is a multiple of 32: per block
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float a = acc[r][q];
+                if (enc_rows) {
+                    v[q] = a;
+                } else if (p.mask_in) {
+                    v[q] = (bits_in[r] >> q) & 1u ? a : 0.f;   // threshold_backward
+                } else if (p.mask) {
+                    const int n = nb + 8 * (q >> 2) + 4 * h + (q & 3);
+                    v[q] = p.mask[(size_t)(n - p.n_a) * p.ldp + g] > 0.f ? a : 0.f;   // threshold_backward(g, h, 0)
+                } else {
+                    v[q] = 0.f;
+                }
+            }
+            if (!enc_rows && !p.mask_in && !p.mask) continue;   // no mask: those rows are dropped
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) st[8 * (q >> 2) + 4 * h + (q & 3)][c] = v[q];
+        wave_lds_handoff();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = srow + 8 * i, n = nb + row;
+            const float4 y = *reinterpret_cast<const float4*>(&st[row][scol]);
+            float* d;
+            bool acc_old = false;
+            if (MODE == kMlpBwdMask && nb < p.n_a) {
+                d = p.dst_a + (size_t)n * p.ldp + g0 + scol;
+                acc_old = p.accumulate_a != 0;
+            } else {
+                d = p.dst + (size_t)(MODE == kMlpBwdMask ? n - p.n_a : n) * p.ldp + g0 + scol;
+            }
+            float4 o = y;
+            if (acc_old) {
+                const float4 old = *reinterpret_cast<const float4*>(d);
+                o = make_float4(old.x + y.x, old.y + y.y, old.z + y.z, old.w + y.w);
+            }
+            *reinterpret_cast<float4*>(d) = o;
+        }
+        wave_lds_handoff();   // the next block's writes stay behind these reads
     }
 }
 
