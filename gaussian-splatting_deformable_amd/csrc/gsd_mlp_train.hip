@@ -12,12 +12,11 @@
 // Layout.  Activations live FEATURE-MAJOR in HBM, [feature][ldp] (ldp = P rounded up to 256): the forward writes
 // every layer's post-ReLU output h_l (the backward's ReLU masks and weight-gradient operands), the backward writes
 // the pre-activation gradients g_l.  The MFMA operand maps then need no transposes:
-//   k_mlp_gemm   Y^T = A . X^T for a tile of 256 Gaussians (4 waves x 2 column blocks of 32): A = the layer's
-//                weights W (forward) or W^T (backward), pre-split and packed fragment-major by k_mlp_pack; X^T loaded
-//                straight from the feature-major activations (lane (h, c): features 16 ks + 8 h + j of Gaussian c,
-//                each load a coalesced 128-B row segment per half-wave) and split in registers.  Epilogues: bias +
-//                ReLU -> h_l (forward), bias -> the heads' (P, 58) outputs, or the ReLU mask of h_l -> g_l and the
-//                encoding's gradient rows (backward).
+//   k_mlp_gemm_dma   Y^T = A . X^T for a tile of 256 Gaussians (8 waves x 32): A = the layer's weights W (forward)
+//                or W^T (backward), pre-split and packed fragment-major by k_mlp_pack; both A and the activation rows
+//                copied global -> LDS by LDS-DMA three k-steps ahead; lane (h, c) reads features 16 ks + 8 h + j of
+//                Gaussian c and splits them in registers.  Epilogues: bias + ReLU -> h_l (forward), bias -> the
+//                heads' (P, 58) outputs, or the ReLU mask of h_l -> g_l and the encoding's gradient rows (backward).
 //   k_mlp_wgrad  dW = g . X^T over the Gaussians: both operands feature-major, so lane (h, c) reads 8 consecutive
 //                Gaussians of one feature row (32 B); split-K over Gaussian chunks into per-wave partials, plus the
 //                bias gradient's row sums of g; k_mlp_wgrad_reduce sums the partials in a fixed order.
@@ -178,95 +177,17 @@ __global__ __launch_bounds__(256) void k_mlp_encode_bwd(int P, int ldp, const fl
     }
 }
 
-// ---- Y^T = A X^T for a tile of 128 Gaussians and ALL of the layer's output rows ----
-// One wave per 32 Gaussians (the B operand's columns), the workgroup's four waves sharing each k-step's A
-// fragments (RB row blocks x 3 splits x 1 KB) through an LDS double buffer: the fragments of k-step ks + 1 are
-// fetched into registers while ks's MFMAs run and written to the other buffer behind them, one barrier per k-step.
-// Each activation is read from HBM once per layer (all rows in one workgroup) and its loads run two k-steps ahead.
-__device__ __forceinline__ void load_x8(const MlpGemmParams& p, int ks, int h, int g, float (&v)[8]) {
-    const float* src = ks < p.ks0 ? p.src0 + (size_t)(16 * ks + 8 * h) * p.ldp
-                                  : p.src1 + (size_t)(16 * (ks - p.ks0) + 8 * h) * p.ldp;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = src[(size_t)j * p.ldp + g];
-}
-
+// The GEMM epilogue: accumulator register q of row block r holds row
+// n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3) of Gaussian g = g0 + c.  The hidden-row epilogues (forward ReLU,
+// backward mask) go out through LDS: the wave writes its 32 x 32 block transposed into st and stores each row's 32
+// Gaussians as 16-B pieces -- four 1-KB store instructions per block instead of sixteen 256-B ones (the one-dword
+// stores were store-issue bound: 30 % of the forward GEMM's time, 44 % of the backward's).
 template <int MODE, int RB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_gemm(MlpGemmParams p) {
-    constexpr int NF = RB * 3 * 64;               // 16-B fragments per k-step
-    constexpr int PER = (NF + 255) / 256;         // per thread
-    __shared__ bf16x8 s_a[2][PER * 256];   // padded to whole thread rows: the staging needs no per-thread guard
-    __shared__ __attribute__((aligned(16))) float s_t[4][32][36];   // epilogue: a wave's 32 x 32 block, transposed
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
-    const int g = blockIdx.x * 128 + wave * 32 + c;   // always < ldp
-    const int KS = p.ks0 + p.ks1;
-    const int rb0 = blockIdx.y * RB;                  // this workgroup's RB row blocks of the p.rb packed ones
-    const size_t kstride = (size_t)p.rb * 3 * 64;     // fragments per k-step of the packed A
-    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags) + (size_t)rb0 * 3 * 64;
-    f32x16 acc[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) acc[r] = f32x16{};
-    // backward: the forward's ReLU bits, one 16-bit word per row block, loaded now (their HBM latency behind the
-    // main loop rather than in front of the epilogue)
-    unsigned bits_in[RB];
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-        bits_in[r] = 0xffffu;
-        if (MODE == kMlpBwdMask && p.mask_in) {
-            const int rm = rb0 + r - p.n_a / 32;
-            if (rm >= 0) bits_in[r] = p.mask_in[(size_t)(rm * 2 + h) * p.ldp + g];
-        }
-    }
-    bf16x8 stage[2][PER];   // A fragments two k-steps ahead: set u & 1 holds k-step ks + 2 (ks = ks0 + u)
-    // Every load below is unconditional, from a clamped index or k-step: divergent or data-dependent branches
-    // around the loads made the compiler's counter bookkeeping give up (vmcnt(0) before each use).
-#pragma unroll
-    for (int i = 0; i < PER; ++i) s_a[0][tid + 256 * i] = F[min(tid + 256 * i, NF - 1)];   // k-step 0's fragments
-#pragma unroll
-    for (int i = 0; i < PER; ++i) stage[1][i] = F[(size_t)min(1, KS - 1) * kstride + min(tid + 256 * i, NF - 1)];
-    // X^T fragments kXDepth k-steps ahead in a ring of registers.  The k-loop is unrolled by the ring's depth so
-    // that slot u is always the same registers: a ring rotated by copies made every step wait for ALL of its
-    // outstanding loads (vmcnt(0): the copy reads the registers the newest loads target), which left the loads one
-    // step ahead instead of four and 58 % of the wave-cycles parked on s_waitcnt.
-    constexpr int kXDepth = 4;
-    float xq[kXDepth][8];
-#pragma unroll
-    for (int d = 0; d < kXDepth; ++d) load_x8(p, min(d, KS - 1), h, g, xq[d]);
-    __syncthreads();
-    for (int ks0 = 0; ks0 < KS; ks0 += kXDepth) {
-#pragma unroll
-        for (int u = 0; u < kXDepth; ++u) {
-            const int ks = ks0 + u;
-            if (ks >= KS) break;   // wave-uniform: the tail of a depth not dividing KS
-            const int buf = ks & 1;
-            {   // k-step ks + 2's fragments into registers (ks + 1's, loaded a step ago, go to LDS after the
-                // MFMAs; past the end: re-reads, never used)
-                const bf16x8* src = F + (size_t)min(ks + 2, KS - 1) * kstride;
-#pragma unroll
-                for (int i = 0; i < PER; ++i) stage[u & 1][i] = src[min(tid + 256 * i, NF - 1)];
-            }
-            const Split8 b = split8(xq[u]);
-            load_x8(p, min(ks + kXDepth, KS - 1), h, g, xq[u]);   // (past the end: a re-read, never used)
-#pragma unroll
-            for (int r = 0; r < RB; ++r) {
-                Split8 a;
-                a.hi = s_a[buf][(r * 3) * 64 + lane];
-                a.mid = s_a[buf][(r * 3 + 1) * 64 + lane];
-                a.lo = s_a[buf][(r * 3 + 2) * 64 + lane];
-                acc[r] = mfma_x6(a, b, acc[r]);
-            }
-#pragma unroll
-            for (int i = 0; i < PER; ++i) s_a[buf ^ 1][tid + 256 * i] = stage[(u + 1) & 1][i];
-            __syncthreads();
-        }
-    }
-    // accumulator register q of row block r: row n = 32 (rb0 + r) + 8 (q >> 2) + 4 h + (q & 3), column = Gaussian g.
-    // The hidden-row epilogues (forward ReLU, backward mask) go out through LDS: the wave writes its 32 x 32 block
-    // transposed into s_t and stores each row's 32 Gaussians as 16-B pieces -- four 1-KB store instructions per
-    // block instead of sixteen 256-B ones (the one-dword stores were store-issue bound: 30 % of the forward GEMM's
-    // time, 44 % of the backward's).
-    const int g0 = blockIdx.x * 128 + wave * 32;    // the wave's first Gaussian
+__device__ __forceinline__ void gemm_epilogue(const MlpGemmParams& p, const f32x16 (&acc)[RB],
+                                              const unsigned (&bits_in)[RB], float (*st)[36], int rb0, int g0,
+                                              int lane) {
+    const int h = lane >> 5, c = lane & 31, g = g0 + c;
     const int srow = lane >> 3, scol = 4 * (lane & 7);   // the transposed read: rows srow + 8 i, columns scol..+3
-    float(*st)[36] = s_t[wave];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         const int nb = 32 * (rb0 + r);   // the block's first row
@@ -341,6 +262,126 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         wave_lds_handoff();   // the next block's writes stay behind these reads
     }
 }
+
+// ---- Y^T = A X^T for a tile of 256 Gaussians and all of the launch's output rows ----
+// A = the layer's W (forward) or W^T (backward), pre-split into three bf16 planes by k_mlp_pack (fragment-major);
+// X^T = the feature-major activations, split in registers; 6 MFMAs (32x32x16 bf16) per row block and k-step.
+// Eight waves (two per SIMD) own 256 Gaussians and all of the launch's row blocks.  Every k-step, the workgroup
+// copies the operands of k-step ks + 3 global -> LDS with global_load_lds_dwordx4 (no VGPR round trip): the
+// A fragments (RB x 3 chunks of 1 KB, fragment-major as k_mlp_pack wrote them) and the 16 activation rows of its
+// 256 Gaussians (1 KB each).  Each wave issues the same number of copies per stage (chunks past RB x 3 re-copy chunk
+// 0 into padding), so one counted `s_waitcnt vmcnt(per-stage copies)` before the k-step's raw s_barrier retires the
+// stage the next k-step reads while the two newest stay in flight: the copies cross the barrier instead of draining at
+// every k-step.  All LDS is one array (a
+// second __shared__ object made hipcc wait for every copy before each LDS read, cdna_hip_programming.md §5).
+template <int RB>
+struct GemmDmaLds {
+    static constexpr int kChunks = RB * 3;             // 1-KB fragment chunks of A per k-step
+    static constexpr int kAPer = (kChunks + 7) / 8;    // copies per wave per k-step for A
+    static constexpr int kASlot = kAPer * 8 * 1024;
+    static constexpr int kXSlot = 16 * 1024;           // 16 feature rows x 256 Gaussians x 4 B
+    static constexpr int kSlots = 4;                   // k-step ks reads slot ks % 4 while ks + 1 .. ks + 3 are staged
+    static constexpr int kX0 = kSlots * kASlot;
+    static constexpr int kBytes = kX0 + kSlots * kXSlot;   // <= 160 KB (>= 36 KB: the epilogue's scratch aliases it)
+    static constexpr int kPerStage = kAPer + 2;        // copies per wave per k-step (A, then two activation rows)
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {   // s_waitcnt vmcnt(N): two stages of copies stay in flight
+    static_assert(N == 6 || N == 8 || N == 10, "copies per two stages");
+    if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// one 16-B-per-lane global -> LDS copy (1 KB per wave-instruction at lds + 16 lane).  A non-template function: with
+// the builtin written inside the kernel template, the host pass silently dropped the kernel's launch stubs.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ void dma16(const void* src, unsigned char* lds) {
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds, 16, 0, 0);
+}
+
+// Stage k-step KS_IN (clamped: past the end a harmless re-copy, so every stage issues the same count) into ring
+// slot SLOT.  (A macro: as a lambda or a helper template inside the kernel template, the host pass silently failed to
+// instantiate the kernel's launch stub.)
+#define GSD_GEMM_DMA_ISSUE(KS_IN, SLOT)                                                                         \
+    do {                                                                                                        \
+        const int ks_ = min((KS_IN), KS - 1), slot_ = (SLOT);                                                   \
+        _Pragma("unroll") for (int i_ = 0; i_ < L::kAPer; ++i_) {                                               \
+            const int ch_ = wave + 8 * i_;                                                                      \
+            dma16(F + (size_t)ks_ * kstride + (size_t)(ch_ < L::kChunks ? ch_ : 0) * 64 + lane,                 \
+                  s_mem + slot_ * L::kASlot + ch_ * 1024);                                                       \
+        }                                                                                                       \
+        const float* xs_ = ks_ < p.ks0 ? p.src0 + (size_t)(16 * ks_) * p.ldp                                    \
+                                       : p.src1 + (size_t)(16 * (ks_ - p.ks0)) * p.ldp;                         \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                                      \
+            const int r_ = 2 * wave + i_;                                                                       \
+            dma16(xs_ + (size_t)r_ * p.ldp + blockIdx.x * 256 + 4 * lane,                                      \
+                  s_mem + L::kX0 + slot_ * L::kXSlot + r_ * 1024);                                               \
+        }                                                                                                       \
+    } while (0)
+
+template <int MODE, int RB>
+__global__ __launch_bounds__(512) void k_mlp_gemm_dma(MlpGemmParams p) {
+    using L = GemmDmaLds<RB>;
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[L::kBytes];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
+    const int gw = blockIdx.x * 256 + wave * 32;      // the wave's first Gaussian (< ldp)
+    const int KS = p.ks0 + p.ks1;
+    const int rb0 = blockIdx.y * RB;
+    const size_t kstride = (size_t)p.rb * 3 * 64;     // 16-B fragments per k-step of the packed A
+    const bf16x8* F = reinterpret_cast<const bf16x8*>(p.frags) + (size_t)rb0 * 3 * 64;
+    f32x16 acc[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[r] = f32x16{};
+    unsigned bits_in[RB];   // backward: the forward's ReLU words, loaded ahead (used after the loop)
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        bits_in[r] = 0xffffu;
+        if (MODE == kMlpBwdMask && p.mask_in) {
+            const int rm = rb0 + r - p.n_a / 32;
+            if (rm >= 0) bits_in[r] = p.mask_in[(size_t)(rm * 2 + h) * p.ldp + gw + c];
+        }
+    }
+    GSD_GEMM_DMA_ISSUE(0, 0);
+    GSD_GEMM_DMA_ISSUE(1, 1);
+    GSD_GEMM_DMA_ISSUE(2, 2);
+    wait_vm<2 * L::kPerStage>();   // k-step 0 landed (this wave's copies) ...
+    raw_barrier();                 // ... and every wave's
+    for (int ks = 0; ks < KS; ++ks) {
+        const int slot = ks & 3;
+        // k-step ks + 3 into the slot k-step ks - 1 read (every wave is past it)
+        GSD_GEMM_DMA_ISSUE(ks + 3, (ks + 3) & 3);
+        const float* xrow = reinterpret_cast<const float*>(s_mem + L::kX0 + slot * L::kXSlot) + wave * 32 + c;
+        float xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = xrow[(8 * h + j) * 256];
+        const Split8 b = split8(xv);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + slot * L::kASlot);
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            Split8 a;
+            a.hi = sa[(r * 3) * 64 + lane];
+            a.mid = sa[(r * 3 + 1) * 64 + lane];
+            a.lo = sa[(r * 3 + 2) * 64 + lane];
+            acc[r] = mfma_x6(a, b, acc[r]);
+        }
+        wait_vm<2 * L::kPerStage>();   // k-step ks + 1 landed; ks + 2 and ks + 3 stay in flight across the barrier
+        raw_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's re-copies, before the scratch reuses the rings
+    raw_barrier();
+    float(*st)[36] = reinterpret_cast<float(*)[36]>(s_mem) + wave * 32;
+    gemm_epilogue<MODE, RB>(p, acc, bits_in, st, rb0, gw, lane);
+}
+
+#undef GSD_GEMM_DMA_ISSUE
 
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
 // One workgroup per Gaussian chunk computes the whole (32 NRB) x (32 KRB) output, one wave per tile of TNB x TKB
@@ -525,11 +566,11 @@ void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, floa
 // (1.72 ms with all 10 row blocks per workgroup)
 template <int MODE>
 static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
-    switch (p.rb) {
-        case 2: hipLaunchKernelGGL((k_mlp_gemm<MODE, 2>), dim3(p.ldp / 128), dim3(256), 0, s, p); break;
-        case 3: hipLaunchKernelGGL((k_mlp_gemm<MODE, 3>), dim3(p.ldp / 128), dim3(256), 0, s, p); break;
-        case 8: hipLaunchKernelGGL((k_mlp_gemm<MODE, 8>), dim3(p.ldp / 128), dim3(256), 0, s, p); break;
-        case 10: hipLaunchKernelGGL((k_mlp_gemm<MODE, 5>), dim3(p.ldp / 128, 2), dim3(256), 0, s, p); break;
+    switch (p.rb) {   // 320 rows (layer 5's W^T): two workgroup rows of 5 blocks
+        case 2: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 2>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 3>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;
+        case 8: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 8>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;
+        case 10: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 5>), dim3(p.ldp / 256, 2), dim3(512), 0, s, p); break;
         default: break;
     }
 }
