@@ -42,6 +42,7 @@ if rank >= 0:
     dist.init_process_group("gloo", rank=rank, world_size=world)
     step(pc, 4.0 * rank)
     flat.allreduce()
+    dist.barrier()   # no rank tears the group down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 else:                      # the single-process reference: both views into one slab
     for r in range(world):
@@ -107,6 +108,7 @@ for it in range(2):
             step(pc, 4.0 * r + it)
         opt.step(zero_grad=True)
 if rank >= 0:
+    dist.barrier()   # no rank tears the group down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 torch.save({"p": opt.param_slab.cpu(), "m": opt.exp_avg.cpu(), "v": opt.exp_avg_sq.cpu()}, out)
 '''
@@ -169,6 +171,7 @@ for it in range(3):
         (out["render"] * w).sum().backward()
 torch.cuda.synchronize()
 if dist.is_initialized():
+    dist.barrier()   # no rank tears the group down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 torch.save({"p": opt.param_slab.cpu(), "m": opt.exp_avg.cpu(), "v": opt.exp_avg_sq.cpu()}, sys.argv[1])
 '''

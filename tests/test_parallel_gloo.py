@@ -47,6 +47,7 @@ def _worker(rank, world, port, out_dir):
         p.grad.copy_(torch.from_numpy(g))
     fg.allreduce()
     np.save(os.path.join(out_dir, f"rank{r}.npy"), fg.slab.numpy())
+    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 
 
@@ -96,6 +97,7 @@ def _worker_sh_views(rank, world, port, out_dir):
     fg.allreduce()
     assert not fg.reduced
     np.save(os.path.join(out_dir, f"rank{r}.npy"), fg.slab.numpy())
+    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 
 
@@ -148,6 +150,7 @@ def _worker_buckets(rank, world, port, out_dir, early=False):
             work.wait()
     assert covered == fg.slab.numel()
     np.save(os.path.join(out_dir, f"{'e' if early else 'b'}rank{r}.npy"), fg.slab.numpy())
+    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 
 
@@ -229,6 +232,7 @@ def _worker_densify(rank, world, port, out_dir):
     torch.manual_seed(1000 + r)   # different generators per rank: the split samples must come from rank 0
     dens.densify_and_prune(2e-4, 0.005, 2.0, 30)
     np.savez(os.path.join(out_dir, f"dens{r}.npz"), *[p.detach().numpy() for p in ps])
+    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 
 
@@ -286,6 +290,7 @@ def _worker_addend(rank, world, port, out_dir):
             (a, b, t), = fg.addend_ranges()
             assert (a, b) == (0, params[0].numel()) and fg.addends == {}
             np.save(os.path.join(out_dir, f"brank{r}.npy"), fg.slab.numpy())
+    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 
 
@@ -379,6 +384,7 @@ def _worker_divergent(rank, world, port, out_dir):
             msgs.append(f"{case}: raised {'differ' in str(e)}")
     with open(os.path.join(out_dir, f"rank{r}.txt"), "w") as fh:
         fh.write("\n".join(msgs))
+    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
     dist.destroy_process_group()
 
 
