@@ -1001,9 +1001,12 @@ gsd::MlpWeightRef mlp_weight(int l, float* const* w, int ldw_override = -1) {
     return r;
 }
 
-void mlp_pack_all(float* const* weights, const MlpWs& ws, bool backward, hipStream_t s) {
+// fused: the forward's weights for k_mlp_fwd_fused, whose B operands past the encoding are the layer before's
+// accumulators (the accumulator-order k permutation: layer 0 none, layer 5 from k-step 4, the rest from 0)
+void mlp_pack_all(float* const* weights, const MlpWs& ws, bool backward, bool fused, hipStream_t s) {
     for (int l = 0; l < 9; ++l) {
         gsd::MlpPackParams pp{};
+        pp.perm_from = !fused || l == 0 ? 1 << 30 : (l == 5 ? 4 : 0);
         pp.w = mlp_weight(l, weights);
         pp.transpose = backward ? 1 : 0;
         pp.M = backward ? kMlpIn[l] : kMlpOut[l];
@@ -1028,10 +1031,32 @@ int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, cons
     hipStream_t s = as_stream(stream);
     float* const* W = const_cast<float* const*>(weights);
     float* const* B = const_cast<float* const*>(biases);
+    // GSD_MLP_FWD=gemm: the layer-by-layer GEMMs (k_mlp_gemm_dma) instead of the layer-fused kernel, for comparison
+    static const bool fused = [] {
+        const char* e = getenv("GSD_MLP_FWD");
+        return !(e && strcmp(e, "gemm") == 0);
+    }();
     timed(kMlpTrainFwd, s, [&] {
-        mlp_pack_all(W, ws, false, s);
+        mlp_pack_all(W, ws, false, fused, s);
         gsd::launch_mlp_gather_bias(mlp_weight(8, B, 1), ws.bias_heads, 64, s);
         gsd::launch_mlp_encode((int)P, (int)ws.ldp, x, t, ws.E, ws.ET, s);
+        if (fused) {
+            gsd::MlpFusedParams f{};
+            f.P = (int)P;
+            f.ldp = (int)ws.ldp;
+            f.E = ws.E;
+            f.ET = ws.ET;
+            for (int l = 0; l < 9; ++l) f.frags[l] = ws.ffrag[l];
+            for (int l = 0; l < 8; ++l) {
+                f.bias[l] = B[l];
+                f.H[l] = ws.H[l + 1];
+                f.bits[l] = ws.bits[l + 1];
+            }
+            f.bias_heads = ws.bias_heads;
+            f.out = out;
+            gsd::launch_mlp_fwd_fused(f, s);
+            return;
+        }
         for (int l = 0; l < 9; ++l) {
             gsd::MlpGemmParams g{};
             g.P = (int)P;
@@ -1092,7 +1117,7 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
     };
     (void)chunks;
     timed(kMlpTrainBwd, s, [&] {
-        mlp_pack_all(W, ws, true, s);
+        mlp_pack_all(W, ws, true, false, s);
         gsd::launch_mlp_rows_to_features((int)P, ldp, 58, grad_out, ws.Gh, 64, s);
         wgrad(8, ws.Gh, 2, ws.H[8], nullptr, 8, 8);
         dgemm(8, ws.Gh, 4, 8, ws.ga, 0, 0);   // g of layer 7's pre-activation

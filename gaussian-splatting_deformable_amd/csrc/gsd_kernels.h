@@ -316,6 +316,24 @@ struct MlpPackParams {
     int M, K;              // packed A is M x K (multiples of 32 / 16); forward A = W, backward A = W^T
     int transpose;
     void* out;             // (K / 16) x (M / 32) x 3 x 64 fragments of 16 B
+    // k-steps >= perm_from take their 16 columns in the accumulator order of the layer before (element j of lane
+    // half h is column 8 (j >> 2) + 4 h + (j & 3) of the step), for a B operand read straight from the previous
+    // layer's accumulators (k_mlp_fwd_fused); natural order below it
+    int perm_from;
+};
+// The layer-fused training forward (k_mlp_fwd_fused): the encoding in, every hidden layer's output, its ReLU words
+// and the heads out; the weights packed with the accumulator-order k permutation (perm_from 0; layer 5: 4; layer 0:
+// natural).
+struct MlpFusedParams {
+    int P, ldp;
+    const float* E;          // [64][ldp]: enc(x), row 63 zero
+    const float* ET;         // [32][ldp]: enc(t), rows 21.. zero
+    const void* frags[9];    // packed W of the eight hidden layers and the heads
+    const float* bias[8];    // the hidden layers' biases (256)
+    const float* bias_heads; // 64 (58 used)
+    float* H[8];             // layer l's output: [256][ldp]
+    unsigned short* bits[8]; // its ReLU words: [(rb * 2 + h) * ldp + g]
+    float* out;              // (P, 58) row-major
 };
 enum { kMlpFwdRelu = 0, kMlpFwdHeads = 1, kMlpBwdMask = 2 };
 struct MlpGemmParams {
@@ -356,6 +374,7 @@ void launch_mlp_pack(const MlpPackParams& p, hipStream_t s);
 void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E, float* ET, hipStream_t s);
 void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, float* dx, int accumulate, hipStream_t s);
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s);
+void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s);
 // dW scattered into the reference-shaped weight pieces (dst.W; map/rows as the forward weight), db into dst_b
 void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s);
 void launch_mlp_rows_to_features(int P, int ldp, int n, const float* src, float* dst, int dst_rows, hipStream_t s);

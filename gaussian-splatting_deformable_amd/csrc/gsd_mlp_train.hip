@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void k_mlp_pack(MlpPackParams p) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int k = 16 * ks + 8 * (lane >> 5) + j;
+        const int h = lane >> 5;
+        const int k = 16 * ks + (ks >= p.perm_from ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j);
         // forward: A = W, rows m = output features, columns k = (padded) input features; backward: A = W^T
         const float* e = p.transpose ? mlp_elem(p.w, k, mlp_col(p.w.map, m)) : mlp_elem(p.w, m, mlp_col(p.w.map, k));
         v[j] = e ? *e : 0.f;
@@ -383,6 +384,295 @@ __global__ __launch_bounds__(512) void k_mlp_gemm_dma(MlpGemmParams p) {
 
 #undef GSD_GEMM_DMA_ISSUE
 
+// ---- the training forward fused across the layers ----
+// One workgroup of four waves (one per SIMD, ~400 registers each) takes 128 Gaussians through all nine layers.  A
+// wave keeps its 32 Gaussians' activations in registers: layer l's accumulators (32 rows x 32 Gaussians per row
+// block, column on the lane) become, after bias and ReLU, layer l + 1's B operand with no lane movement -- k-step
+// 2 rb + s is accumulator registers 8 s .. 8 s + 7 of row block rb, which is why the weights of the layers fed this
+// way are packed with the accumulator-order k permutation (MlpPackParams::perm_from).  Only the weights move: the
+// split fragments of one k-step (24 KB) are copied global -> LDS by LDS-DMA into a four-slot ring three k-steps
+// ahead and shared by the four waves (a wave reading them from L2 itself, as the bf16 k_mlp_fwd does, would need
+// ~4x the L2 bandwidth); the ring runs straight through the eight hidden layers (122 k-steps), the heads get their
+// own.  Every hidden output still goes to HBM (the backward's operands and ReLU words), but no layer re-reads its
+// input: 1 GB per layer at P = 1M instead of 2.
+constexpr int kFusedStep = 8 * 3 * 64;   // bf16x8 per hidden k-step: 8 row blocks x 3 splits x 64 lanes (24 KB)
+
+// s_waitcnt vmcnt(N) with a compile-time N: the copies and stores younger than the stage being retired
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+    static_assert(N >= 0 && N < 64, "vmcnt is six bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// dma16 as inline asm (M0 written and restored in the same statement): the compiler does not see this copy, so it
+// neither drains it before unrelated LDS reads nor counts it -- every wait on it is the caller's s_waitcnt vmcnt.
+// lds: the wave-uniform LDS byte address.
+__device__ __forceinline__ void dma16_asm(const void* src, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)(lds_ptr_t)(const_cast<void*>(p));
+}
+
+// the same with N known only after unrolling (a loop counter): constant-folds to one case
+__device__ __forceinline__ void wait_vm_u(int n) {
+    switch (n) {
+#define GSD_VM_CASE(N) \
+    case N: wait_vm_c<N>(); break;
+        GSD_VM_CASE(4) GSD_VM_CASE(12) GSD_VM_CASE(13) GSD_VM_CASE(21) GSD_VM_CASE(22) GSD_VM_CASE(28)
+        GSD_VM_CASE(29) GSD_VM_CASE(30) GSD_VM_CASE(31) GSD_VM_CASE(32) GSD_VM_CASE(33) GSD_VM_CASE(37)
+        GSD_VM_CASE(38) GSD_VM_CASE(39) GSD_VM_CASE(20) GSD_VM_CASE(36) GSD_VM_CASE(14) GSD_VM_CASE(24)
+        GSD_VM_CASE(26) GSD_VM_CASE(27) GSD_VM_CASE(35)
+#undef GSD_VM_CASE
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (unreachable: every count used is listed)
+    }
+}
+
+// global stores a k-step of a fused layer issues (the layer before's output rows and ReLU words, see below)
+__device__ __forceinline__ constexpr int fused_stores(int kse, int ks, int prev) {
+    return ks < 0 ? prev : (ks < kse ? 0 : 8 + (ks - kse < 8 ? 1 : 0));
+}
+
+// One hidden layer's k-steps -- KSE from the encoding registers (xe: enc(x) k-steps 0-3, then xt: enc(t) k-steps
+// 4-5), then KSA from the activation registers -- fully unrolled so that every register-array index is a constant.
+// s: the global k-step of the layer's first (its ring slot is s & 3).  Each k-step:
+//  1. copies k-step s + ks + 3 (of this layer, or of the next one's first three) into the slot k-step s + ks - 1
+//     read: 24 chunks of 1 KB, six per wave, shared by the four waves;
+//  2. per row block: the next block's three fragments read from LDS, then this block's six MFMAs; beside them one
+//     of the eight rows of the PREVIOUS layer's output this k-step consumes (act[ks - KSE]) goes to HBM (and on the
+//     first eight of them, that row block's ReLU word): the output stores ride under the MFMAs instead of stalling
+//     an epilogue, and act is live anyway;
+//  3. s_waitcnt vmcnt(stores and copies issued after k-step s + ks + 1's copies) and a raw barrier.
+// PREV: the stores of each of the layer before's last two k-steps (0 after layer 0).
+template <int KSE, int KSA, int PREV>
+__device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsigned char* s_mem, int s, int l,
+                                                   int wave, int lane, unsigned voff_h, unsigned voff_b,
+                                                   const float (&xe)[4][8], const float (&xt)[2][8],
+                                                   const float (&act)[16][8], const unsigned (&bits)[8],
+                                                   f32x16 (&acc)[8]) {
+    constexpr int KS = KSE + KSA;
+    const bf16x8* fc = reinterpret_cast<const bf16x8*>(p.frags[l]) + lane;
+    // past the last hidden layer: its own last k-step again (a harmless re-copy keeps the per-step count uniform)
+    const bf16x8* fn = l < 7 ? reinterpret_cast<const bf16x8*>(p.frags[l + 1]) + lane : fc + (KS - 1) * kFusedStep;
+    const int ldp = p.ldp;
+    float* Hp = KSA ? p.H[l - 1] : nullptr;
+    unsigned short* Bp = KSA ? p.bits[l - 1] : nullptr;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        {
+            const int kk = ks + 3;
+            const bf16x8* f = kk < KS ? fc + kk * kFusedStep : (l < 7 ? fn + (kk - KS) * kFusedStep : fn);
+            const unsigned dst = lds_addr(s_mem) + ((s + kk) & 3) * (24 * 1024);
+#ifndef GSD_FX_NODMA
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int ch = wave + 4 * i;
+                dma16_asm(f + ch * 64, __builtin_amdgcn_readfirstlane(dst + ch * 1024));
+            }
+#else
+            (void)f; (void)dst;
+#endif
+        }
+        Split8 b;
+        if (ks < KSE) b = ks < 4 ? split8(xe[ks < 4 ? ks : 0]) : split8(xt[ks >= 4 && ks < 6 ? ks - 4 : 0]);
+        else b = split8(act[ks >= KSE ? ks - KSE : 0]);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + ((s + ks) & 3) * (24 * 1024));
+        Split8 a;
+        a.hi = sa[lane];
+        a.mid = sa[64 + lane];
+        a.lo = sa[128 + lane];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            Split8 an = a;
+            if (r + 1 < 8) {
+                an.hi = sa[((r + 1) * 3) * 64 + lane];
+                an.mid = sa[((r + 1) * 3 + 1) * 64 + lane];
+                an.lo = sa[((r + 1) * 3 + 2) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // the next block's reads issue ahead of this block's MFMAs
+#ifndef GSD_FX_NOSTORE
+            if (ks >= KSE) {
+#else
+            if (ks >= KSE && ks < 0) {
+#endif
+                const int k2 = ks >= KSE ? ks - KSE : 0;   // act[k2][r]: row 16 k2 + 8 (r >> 2) + 4 h + (r & 3)
+#ifdef GSD_FX_NT
+                __builtin_nontemporal_store(act[k2][r], Hp + (size_t)(16 * k2 + 8 * (r >> 2) + (r & 3)) * ldp + voff_h);
+                if (r == 0 && k2 < 8)
+                    __builtin_nontemporal_store((unsigned short)bits[k2 < 8 ? k2 : 0], Bp + (size_t)(2 * k2) * ldp + voff_b);
+#else
+                Hp[(size_t)(16 * k2 + 8 * (r >> 2) + (r & 3)) * ldp + voff_h] = act[k2][r];
+                if (r == 0 && k2 < 8) Bp[(size_t)(2 * k2) * ldp + voff_b] = (unsigned short)bits[k2 < 8 ? k2 : 0];
+#endif
+            }
+            acc[r] = mfma_x6(a, b, acc[r]);
+            a = an;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        wait_vm_u(fused_stores(KSE, ks - 2, PREV) + fused_stores(KSE, ks - 1, PREV) + fused_stores(KSE, ks, PREV) +
+                  12);
+#ifndef GSD_FX_NOBAR
+        raw_barrier();
+#endif
+    }
+}
+
+// bias (from LDS) + ReLU into the next layer's B operand (k-step 2 rb + s8 = registers 8 s8 .. 8 s8 + 7) and the
+// ReLU words; no global access (their stores ride in the next layer's k-steps)
+__device__ __forceinline__ void fused_hidden_epilogue(const float* s_bias, int h, const f32x16 (&acc)[8],
+                                                      float (&act)[16][8], unsigned (&bits)[8]) {
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+        unsigned w = 0;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 b4 = *reinterpret_cast<const float4*>(s_bias + 32 * rb + 8 * q4 + 4 * h);
+            const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int q = 4 * q4 + i;
+                const float y = fmaxf(acc[rb][q] + bq[i], 0.f);
+                act[2 * rb + (q >> 3)][q & 7] = y;
+                w |= (y > 0.f ? 1u : 0u) << q;
+            }
+        }
+        bits[rb] = w;
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_fwd_fused(MlpFusedParams p) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[4 * 24 * 1024];
+    // the biases in an LDS object of their own: the compiler then knows the ring's copies cannot write them and
+    // reads them without draining the copies in flight (one LDS array: an s_waitcnt vmcnt(0) per epilogue)
+    __shared__ __attribute__((aligned(16))) float s_bias[8 * 256 + 64];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
+    const int g = blockIdx.x * 128 + wave * 32 + c;   // < ldp (the grid covers ldp / 128 workgroups)
+    const unsigned voff_h = (unsigned)(4 * h) * (unsigned)p.ldp + (unsigned)g;   // row 4 h of a layer's output
+    const unsigned voff_b = (unsigned)h * (unsigned)p.ldp + (unsigned)g;         // ReLU word of half h
+#pragma unroll
+    for (int l = 0; l < 8; ++l) s_bias[256 * l + tid] = p.bias[l][tid];
+    if (tid < 64) s_bias[2048 + tid] = p.bias_heads[tid];
+    // the encoding in the B operand's natural order: lane half h holds rows 16 ks + 8 h + j
+    float xe[4][8], xt[2][8];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xe[ks][j] = p.E[(size_t)(16 * ks + 8 * h + j) * p.ldp + g];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xt[ks][j] = p.ET[(size_t)(16 * ks + 8 * h + j) * p.ldp + g];
+    // before the first copy: plain loads never wait behind one.  The builtin (0xf70: vmcnt 0, the other counters
+    // free), not asm, so that the compiler knows these loads are done and sets no waits of its own on them later
+    __builtin_amdgcn_s_waitcnt(0xf70);
+    __syncthreads();   // the biases in LDS
+    float act[16][8];
+    unsigned bits[8];
+    f32x16 acc[8];
+    {
+        const bf16x8* f0 = reinterpret_cast<const bf16x8*>(p.frags[0]) + lane;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int ch = wave + 4 * i;
+                dma16_asm(f0 + k * kFusedStep + ch * 64,
+                          __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + k * (24 * 1024) + ch * 1024));
+            }
+    }
+    wait_vm_c<12>();
+    raw_barrier();
+    fused_hidden_layer<6, 0, 0>(p, s_mem, 0, 0, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+    fused_hidden_epilogue(s_bias, h, acc, act, bits);
+    fused_hidden_layer<0, 16, 0>(p, s_mem, 6, 1, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+    fused_hidden_epilogue(s_bias + 256, h, acc, act, bits);
+#pragma unroll 1
+    for (int l = 2; l <= 4; ++l) {
+        fused_hidden_layer<0, 16, 8>(p, s_mem, 6 + 16 * (l - 1), l, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+        fused_hidden_epilogue(s_bias + 256 * l, h, acc, act, bits);
+    }
+    fused_hidden_layer<4, 16, 8>(p, s_mem, 70, 5, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+    fused_hidden_epilogue(s_bias + 256 * 5, h, acc, act, bits);
+#pragma unroll 1
+    for (int l = 6; l <= 7; ++l) {
+        fused_hidden_layer<0, 16, 8>(p, s_mem, 90 + 16 * (l - 6), l, wave, lane, voff_h, voff_b, xe, xt, act, bits,
+                                     acc);
+        fused_hidden_epilogue(s_bias + 256 * l, h, acc, act, bits);
+    }
+    // the heads (58 outputs, two row blocks): their own ring over the same LDS, 6 chunks per k-step (two copies per
+    // wave, the last two re-copy chunk 0); the last hidden layer's output rides under their MFMAs as above
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    const bf16x8* fh = reinterpret_cast<const bf16x8*>(p.frags[8]) + lane;
+#define GSD_HEADS_ISSUE(KS)                                                                                    \
+    do {                                                                                                       \
+        const int k_ = min((KS), 15);                                                                          \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                                     \
+            const int ch_ = wave + 4 * i_;                                                                     \
+            dma16_asm(fh + k_ * (2 * 3 * 64) + (ch_ < 6 ? ch_ : 0) * 64,                                       \
+                      __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (8 * 1024) + ch_ * 1024));   \
+        }                                                                                                      \
+    } while (0)
+    f32x16 ho[2] = {f32x16{}, f32x16{}};
+    GSD_HEADS_ISSUE(0);
+    GSD_HEADS_ISSUE(1);
+    GSD_HEADS_ISSUE(2);
+    wait_vm_c<4>();
+    raw_barrier();
+    float* H7 = p.H[7];
+    unsigned short* B7 = p.bits[7];
+    const int ldp = p.ldp;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+        GSD_HEADS_ISSUE(ks + 3);
+        const Split8 b = split8(act[ks]);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (8 * 1024));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#ifdef GSD_FX_NT
+            __builtin_nontemporal_store(act[ks][j], H7 + (size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_h);
+#else
+            H7[(size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_h] = act[ks][j];
+#endif
+        }
+        if (ks < 8) B7[(size_t)(2 * ks) * ldp + voff_b] = (unsigned short)bits[ks < 8 ? ks : 0];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            Split8 a;
+            a.hi = sa[(r * 3) * 64 + lane];
+            a.mid = sa[(r * 3 + 1) * 64 + lane];
+            a.lo = sa[(r * 3 + 2) * 64 + lane];
+            ho[r] = mfma_x6(a, b, ho[r]);
+        }
+        wait_vm_u(4 + (ks >= 2 ? fused_stores(0, ks - 2, 0) : 0) + (ks >= 1 ? fused_stores(0, ks - 1, 0) : 0) +
+                  fused_stores(0, ks, 0));
+        raw_barrier();
+    }
+#undef GSD_HEADS_ISSUE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's re-copies: nothing left in flight at exit
+    if (g < p.P) {
+        const float* bh = s_bias + 2048;
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const float4 b4 = *reinterpret_cast<const float4*>(bh + 32 * r + 8 * q4 + 4 * h);
+                const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int n = 32 * r + 8 * q4 + 4 * h + i;
+                    if (n < 58) p.out[(size_t)g * 58 + n] = ho[r][4 * q4 + i] + bq[i];
+                }
+            }
+    }
+}
+
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
 // One workgroup per Gaussian chunk computes the whole (32 NRB) x (32 KRB) output, one wave per tile of TNB x TKB
 // blocks of 32 x 32 (four waves, one per SIMD with 512 registers; or eight, two per SIMD, on half-size tiles).  Each 16-Gaussian step, every thread loads 64 B of one or two feature rows (of G or X), splits
@@ -573,6 +863,10 @@ static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
         case 10: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 5>), dim3(p.ldp / 256, 2), dim3(512), 0, s, p); break;
         default: break;
     }
+}
+
+void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s) {
+    if (p.P > 0) hipLaunchKernelGGL(k_mlp_fwd_fused, dim3(p.ldp / 128), dim3(256), 0, s, p);
 }
 
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s) {
