@@ -423,19 +423,21 @@ __device__ __forceinline__ void wait_vm_u(int n) {
     switch (n) {
 #define GSD_VM_CASE(N) \
     case N: wait_vm_c<N>(); break;
-        GSD_VM_CASE(4) GSD_VM_CASE(12) GSD_VM_CASE(13) GSD_VM_CASE(21) GSD_VM_CASE(22) GSD_VM_CASE(28)
-        GSD_VM_CASE(29) GSD_VM_CASE(30) GSD_VM_CASE(31) GSD_VM_CASE(32) GSD_VM_CASE(33) GSD_VM_CASE(37)
-        GSD_VM_CASE(38) GSD_VM_CASE(39) GSD_VM_CASE(20) GSD_VM_CASE(36) GSD_VM_CASE(14) GSD_VM_CASE(24)
-        GSD_VM_CASE(26) GSD_VM_CASE(27) GSD_VM_CASE(35)
+#define GSD_VM_CASE8(N) GSD_VM_CASE(N) GSD_VM_CASE(N + 1) GSD_VM_CASE(N + 2) GSD_VM_CASE(N + 3) GSD_VM_CASE(N + 4) \
+    GSD_VM_CASE(N + 5) GSD_VM_CASE(N + 6) GSD_VM_CASE(N + 7)
+        GSD_VM_CASE8(0) GSD_VM_CASE8(8) GSD_VM_CASE8(16) GSD_VM_CASE8(24) GSD_VM_CASE8(32) GSD_VM_CASE8(40)
+#undef GSD_VM_CASE8
 #undef GSD_VM_CASE
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (unreachable: every count used is listed)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (unreachable: every count used is < 48)
     }
 }
 
 // global stores a k-step of a fused layer issues (the layer before's output rows and ReLU words, see below)
+constexpr int kActStores = 8;   // 4-B row stores per activation k-step (a 16-B form via a quad transpose was 1.5 % slower)
 __device__ __forceinline__ constexpr int fused_stores(int kse, int ks, int prev) {
-    return ks < 0 ? prev : (ks < kse ? 0 : 8 + (ks - kse < 8 ? 1 : 0));
+    return ks < 0 ? prev : (ks < kse ? 0 : kActStores + (ks - kse < 8 ? 1 : 0));
 }
+
 
 // One hidden layer's k-steps -- KSE from the encoding registers (xe: enc(x) k-steps 0-3, then xt: enc(t) k-steps
 // 4-5), then KSA from the activation registers -- fully unrolled so that every register-array index is a constant.
@@ -469,15 +471,11 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
             const int kk = ks + 3;
             const bf16x8* f = kk < KS ? fc + kk * kFusedStep : (l < 7 ? fn + (kk - KS) * kFusedStep : fn);
             const unsigned dst = lds_addr(s_mem) + ((s + kk) & 3) * (24 * 1024);
-#ifndef GSD_FX_NODMA
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const int ch = wave + 4 * i;
                 dma16_asm(f + ch * 64, __builtin_amdgcn_readfirstlane(dst + ch * 1024));
             }
-#else
-            (void)f; (void)dst;
-#endif
         }
         Split8 b;
         if (ks < KSE) b = ks < 4 ? split8(xe[ks < 4 ? ks : 0]) : split8(xt[ks >= 4 && ks < 6 ? ks - 4 : 0]);
@@ -496,20 +494,13 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
                 an.lo = sa[((r + 1) * 3 + 2) * 64 + lane];
             }
             __builtin_amdgcn_sched_barrier(0);   // the next block's reads issue ahead of this block's MFMAs
-#ifndef GSD_FX_NOSTORE
             if (ks >= KSE) {
-#else
-            if (ks >= KSE && ks < 0) {
-#endif
                 const int k2 = ks >= KSE ? ks - KSE : 0;   // act[k2][r]: row 16 k2 + 8 (r >> 2) + 4 h + (r & 3)
-#ifdef GSD_FX_NT
+                // nontemporal: the 8 GB of hidden outputs stream past L2 instead of evicting the weights every
+                // workgroup re-reads from it (2 % faster than plain stores)
                 __builtin_nontemporal_store(act[k2][r], Hp + (size_t)(16 * k2 + 8 * (r >> 2) + (r & 3)) * ldp + voff_h);
                 if (r == 0 && k2 < 8)
                     __builtin_nontemporal_store((unsigned short)bits[k2 < 8 ? k2 : 0], Bp + (size_t)(2 * k2) * ldp + voff_b);
-#else
-                Hp[(size_t)(16 * k2 + 8 * (r >> 2) + (r & 3)) * ldp + voff_h] = act[k2][r];
-                if (r == 0 && k2 < 8) Bp[(size_t)(2 * k2) * ldp + voff_b] = (unsigned short)bits[k2 < 8 ? k2 : 0];
-#endif
             }
             acc[r] = mfma_x6(a, b, acc[r]);
             a = an;
@@ -517,9 +508,7 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
         }
         wait_vm_u(fused_stores(KSE, ks - 2, PREV) + fused_stores(KSE, ks - 1, PREV) + fused_stores(KSE, ks, PREV) +
                   12);
-#ifndef GSD_FX_NOBAR
         raw_barrier();
-#endif
     }
 }
 
@@ -634,14 +623,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
         const Split8 b = split8(act[ks]);
         const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (8 * 1024));
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-#ifdef GSD_FX_NT
+        for (int j = 0; j < 8; ++j)
             __builtin_nontemporal_store(act[ks][j], H7 + (size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_h);
-#else
-            H7[(size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_h] = act[ks][j];
-#endif
-        }
-        if (ks < 8) B7[(size_t)(2 * ks) * ldp + voff_b] = (unsigned short)bits[ks < 8 ? ks : 0];
+        if (ks < 8) __builtin_nontemporal_store((unsigned short)bits[ks < 8 ? ks : 0], B7 + (size_t)(2 * ks) * ldp + voff_b);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             Split8 a;

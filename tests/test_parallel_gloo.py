@@ -31,6 +31,24 @@ def view_grads(yaw):
     return [b["dL_dmeans3D"], b["dL_dsh"], b["dL_dopacity"], b["dL_dscales"], b["dL_drotations"]]
 
 
+def _teardown(rank, world, out_dir):
+    """Tear gloo down without a peer losing its connection mid-teardown: a barrier, then every rank but 0
+    destroys its groups and says so through a file, and rank 0 (which hosts the TCP store) goes last.  A
+    plain barrier + destroy on every rank at once let rank 0's store close under a peer still tearing down
+    (that peer then aborted in a gloo thread: "terminate called without an active exception")."""
+    import time
+    dist.barrier()
+    if rank != 0:
+        dist.destroy_process_group()
+        open(os.path.join(out_dir, ".down%d" % rank), "w").close()
+        return
+    deadline = time.time() + 60
+    while time.time() < deadline and not all(os.path.exists(os.path.join(out_dir, ".down%d" % r))
+                                             for r in range(1, world)):
+        time.sleep(0.01)
+    dist.destroy_process_group()
+
+
 def _worker(rank, world, port, out_dir):
     import sys
     for p in (PKG, ROOT):
@@ -47,8 +65,7 @@ def _worker(rank, world, port, out_dir):
         p.grad.copy_(torch.from_numpy(g))
     fg.allreduce()
     np.save(os.path.join(out_dir, f"rank{r}.npy"), fg.slab.numpy())
-    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
-    dist.destroy_process_group()
+    _teardown(rank, world, out_dir)
 
 
 def _free_port():
@@ -97,8 +114,7 @@ def _worker_sh_views(rank, world, port, out_dir):
     fg.allreduce()
     assert not fg.reduced
     np.save(os.path.join(out_dir, f"rank{r}.npy"), fg.slab.numpy())
-    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
-    dist.destroy_process_group()
+    _teardown(rank, world, out_dir)
 
 
 def test_two_rank_sh_views_protocol(tmp_path):
@@ -150,8 +166,7 @@ def _worker_buckets(rank, world, port, out_dir, early=False):
             work.wait()
     assert covered == fg.slab.numel()
     np.save(os.path.join(out_dir, f"{'e' if early else 'b'}rank{r}.npy"), fg.slab.numpy())
-    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
-    dist.destroy_process_group()
+    _teardown(rank, world, out_dir)
 
 
 def test_four_rank_bucketed_allreduce_equals_sum_of_views(tmp_path):
@@ -232,8 +247,7 @@ def _worker_densify(rank, world, port, out_dir):
     torch.manual_seed(1000 + r)   # different generators per rank: the split samples must come from rank 0
     dens.densify_and_prune(2e-4, 0.005, 2.0, 30)
     np.savez(os.path.join(out_dir, f"dens{r}.npz"), *[p.detach().numpy() for p in ps])
-    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
-    dist.destroy_process_group()
+    _teardown(rank, world, out_dir)
 
 
 def test_two_rank_densify_keeps_replicas_identical(tmp_path):
@@ -290,8 +304,7 @@ def _worker_addend(rank, world, port, out_dir):
             (a, b, t), = fg.addend_ranges()
             assert (a, b) == (0, params[0].numel()) and fg.addends == {}
             np.save(os.path.join(out_dir, f"brank{r}.npy"), fg.slab.numpy())
-    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
-    dist.destroy_process_group()
+    _teardown(rank, world, out_dir)
 
 
 def test_two_rank_addend_joins_after_the_sum(tmp_path):
@@ -384,8 +397,7 @@ def _worker_divergent(rank, world, port, out_dir):
             msgs.append(f"{case}: raised {'differ' in str(e)}")
     with open(os.path.join(out_dir, f"rank{r}.txt"), "w") as fh:
         fh.write("\n".join(msgs))
-    dist.barrier()   # no rank tears gloo down while a peer's last exchange is still in flight
-    dist.destroy_process_group()
+    _teardown(rank, world, out_dir)
 
 
 def test_rank_divergent_layouts_raise_on_every_rank(tmp_path):
