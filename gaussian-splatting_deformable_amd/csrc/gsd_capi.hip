@@ -1100,9 +1100,11 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
     float* const* W = const_cast<float* const*>(weights);
     const int ldp = (int)ws.ldp;
     const int chunks = (int)((P + kMlpChunk - 1) / kMlpChunk);
-    auto wgrad = [&](int l, const float* G, int n_rb, const float* X0, const float* X1, int k_rb, int k_rb0) {
+    auto wgrad = [&](int l, const float* G, int n_rb, const float* X0, const float* X1, int k_rb, int k_rb0,
+                     int k_off = 0) {
         gsd::MlpWgradParams q{};
         q.P = (int)P; q.ldp = ldp; q.G = G; q.n_rb = n_rb; q.X0 = X0; q.X1 = X1; q.k_rb = k_rb; q.k_rb0 = k_rb0;
+        q.k_off = k_off;
         q.tiles_n = (n_rb + 3) / 4; q.tiles_k = (k_rb + 3) / 4; q.chunk = kMlpChunk;
         q.partial = ws.partial; q.bias_partial = ws.bias_partial;
         gsd::launch_mlp_wgrad(q, mlp_weight(l, d_weights), mlp_weight(l, d_biases, 1), s);
@@ -1125,7 +1127,10 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
         float* other = ws.gb;
         for (int l = 7; l >= 0; --l) {
             if (l == 0) wgrad(0, g, 8, ws.E, ws.ET, 3, 2);
-            else if (l == 5) wgrad(5, g, 8, ws.E, ws.H[5], 10, 2);
+            else if (l == 5) {   // columns 0-63 (enc(x)) and 64-319 (h5) as two calls (both bias gradients equal)
+                wgrad(5, g, 8, ws.E, nullptr, 2, 2, 0);
+                wgrad(5, g, 8, ws.H[5], nullptr, 8, 8, 64);
+            }
             else wgrad(l, g, 8, ws.H[l], nullptr, 8, 8);
             if (l == 5) dgemm(5, g, 16, 5, other, 64, 0);   // rows 0-63: d enc(x); the rest masked by h5
             else if (l > 0) dgemm(l, g, 16, l, other, 0, 0);

@@ -365,6 +365,7 @@ struct MlpWgradParams {
     const float* X0;                // [32 k_rb0][ldp], then X1: [32 (k_rb - k_rb0)][ldp]
     const float* X1;
     int k_rb, k_rb0;
+    int k_off;                      // padded input column of this call's first k (a layer's k range in pieces)
     int tiles_n, tiles_k;           // 128 x 128 output tiles
     int chunk;                      // Gaussians per wave (multiple of 16)
     float* partial;                 // [chunks][32 n_rb][32 k_rb]

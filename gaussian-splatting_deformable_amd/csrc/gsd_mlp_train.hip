@@ -674,14 +674,6 @@ struct WgradShape {
     static constexpr int RPT = (ROWS + THREADS - 1) / THREADS;          // rows staged per thread
 };
 
-__device__ __forceinline__ void load_row16(const float* __restrict__ row, int p0, float (&v)[16]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float4 f = *reinterpret_cast<const float4*>(row + p0 + 4 * q);
-        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
-    }
-}
-
 __device__ __forceinline__ void stage_row(const float (&raw)[16], int p0, int P, bf16x8* __restrict__ slot,
                                           float* bsum) {
     float v[16];
@@ -724,18 +716,35 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
             src[i] = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
         }
     }
-    // rows of step s + 2 in registers while step s multiplies; split and written to LDS one step ahead
-    float raw[S::RPT][16];
+    // Each row's 32 Gaussians of two steps are loaded together (eight 16-B loads: whole 128-B lines; one 64-B
+    // segment per row and step ran the staging at ~2.8 TB/s), and split + written to LDS one step ahead: step s + 1
+    // is staged while step s multiplies, the next pair loaded right after its predecessor's second half is staged.
+    // (One row per thread only: with more, e.g. layer 5's 576 rows on 256 threads, the pair of steps in registers
+    // spills, so those shapes keep one 16-Gaussian segment per row and step, loaded two steps ahead.)
+    constexpr bool kWide = S::RPT == 1;
+    constexpr int kWid = kWide ? 32 : 16;
+    float raw[S::RPT][kWid];
     auto load = [&](int p0) {
 #pragma unroll
         for (int i = 0; i < S::RPT; ++i)
-            if (tid + S::THREADS * i < S::ROWS) load_row16(src[i], p0, raw[i]);
+            if (tid + S::THREADS * i < S::ROWS) {
+#pragma unroll
+                for (int q = 0; q < kWid / 4; ++q) {
+                    const float4 f = *reinterpret_cast<const float4*>(src[i] + p0 + 4 * q);
+                    raw[i][4 * q] = f.x; raw[i][4 * q + 1] = f.y; raw[i][4 * q + 2] = f.z; raw[i][4 * q + 3] = f.w;
+                }
+            }
     };
-    auto write = [&](int p0, int buf) {
+    auto write = [&](int p0, int buf, int half) {   // half: compile-time after unrolling
 #pragma unroll
         for (int i = 0; i < S::RPT; ++i) {
             const int r = tid + S::THREADS * i;
-            if (r < S::ROWS) stage_row(raw[i], p0, p_hi, s_op[buf][r], r < 32 * NRB ? &bsum[i] : nullptr);
+            if (r < S::ROWS) {
+                float v[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = raw[i][16 * half + j];
+                stage_row(v, p0, p_hi, s_op[buf][r], r < 32 * NRB ? &bsum[i] : nullptr);
+            }
         }
     };
     f32x16 acc[TNB][TKB];
@@ -743,33 +752,57 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
     for (int i = 0; i < TNB; ++i)
 #pragma unroll
         for (int j = 0; j < TKB; ++j) acc[i][j] = f32x16{};
-    load(p_lo);
-    write(p_lo, 0);
-    if (p_lo + 16 < p_hi) load(p_lo + 16);
+    load(p_lo);   // the chunk starts on a 32-Gaussian boundary; reads up to ldp stay inside the padded rows
+    write(p_lo, 0, 0);
+    if (!kWide && p_lo + 16 < p_hi) load(p_lo + 16);
     __syncthreads();
+    // one step's multiply: the fragments from LDS buffer bf, six MFMAs per block pair
+#define GSD_WGRAD_MMA(bf)                                                                                       \
+    do {                                                                                                        \
+        Split8 a_[TNB], b_[TKB];                                                                                \
+        _Pragma("unroll") for (int i = 0; i < TNB; ++i) {                                                       \
+            const bf16x8* sl = s_op[bf][32 * (TNB * tn + i) + c];                                               \
+            a_[i].hi = sl[0 + h]; a_[i].mid = sl[2 + h]; a_[i].lo = sl[4 + h];                                  \
+        }                                                                                                       \
+        _Pragma("unroll") for (int j = 0; j < TKB; ++j) {                                                       \
+            const bf16x8* sl = s_op[bf][32 * NRB + 32 * (TKB * tk + j) + c];                                    \
+            b_[j].hi = sl[0 + h]; b_[j].mid = sl[2 + h]; b_[j].lo = sl[4 + h];                                  \
+        }                                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < TNB; ++i)                                                         \
+            _Pragma("unroll") for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6(a_[i], b_[j], acc[i][j]);       \
+    } while (0)
     int buf = 0;
-    for (int pb = p_lo; pb < p_hi; pb += 16, buf ^= 1) {
-        if (pb + 16 < p_hi) {
-            write(pb + 16, buf ^ 1);
-            if (pb + 32 < p_hi) load(pb + 32);
+    if constexpr (kWide) {
+        // the two waves of a SIMD (w and w + 4) take the step's two phases in opposite orders, so that one's
+        // staging VALU runs beside the other's MFMAs instead of both staging, then both multiplying
+        const bool mma_first = S::WAVES == 8 && (wave & 4);
+        for (int pb2 = p_lo; pb2 < p_hi; pb2 += 32) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int pb = pb2 + 16 * hh;
+                if (pb < p_hi) {   // workgroup-uniform
+                    if (mma_first) GSD_WGRAD_MMA(buf);
+                    if (pb + 16 < p_hi) {
+                        write(pb + 16, buf ^ 1, hh ^ 1);
+                        if (hh == 0 && pb2 + 32 < p_hi) load(pb2 + 32);
+                    }
+                    if (!mma_first) GSD_WGRAD_MMA(buf);
+                    __syncthreads();
+                    buf ^= 1;
+                }
+            }
         }
-        Split8 a[TNB], b[TKB];
-#pragma unroll
-        for (int i = 0; i < TNB; ++i) {
-            const bf16x8* sl = s_op[buf][32 * (TNB * tn + i) + c];
-            a[i].hi = sl[0 + h]; a[i].mid = sl[2 + h]; a[i].lo = sl[4 + h];
+    } else {
+        for (int pb = p_lo; pb < p_hi; pb += 16, buf ^= 1) {
+            if (pb + 16 < p_hi) {
+                write(pb + 16, buf ^ 1, 0);
+                if (pb + 32 < p_hi) load(pb + 32);
+            }
+            GSD_WGRAD_MMA(buf);
+            __syncthreads();
         }
-#pragma unroll
-        for (int j = 0; j < TKB; ++j) {
-            const bf16x8* sl = s_op[buf][32 * NRB + 32 * (TKB * tk + j) + c];
-            b[j].hi = sl[0 + h]; b[j].mid = sl[2 + h]; b[j].lo = sl[4 + h];
-        }
-#pragma unroll
-        for (int i = 0; i < TNB; ++i)
-#pragma unroll
-            for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6(a[i], b[j], acc[i][j]);
-        __syncthreads();
     }
+#undef GSD_WGRAD_MMA
     // partial[chunk][n][k], n = 32 (TNB tn + i) + 8 (q >> 2) + 4 h + (q & 3), k = 32 (TKB tk + j) + c
     float* out = p.partial + (size_t)blockIdx.x * (32 * NRB) * (32 * KRB);
 #pragma unroll
@@ -795,7 +828,7 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
 // reference-shaped pieces (padded columns and rows dropped); the bias gradient likewise (k_cols = 1).  A workgroup
 // owns 32 consecutive outputs; its 8 thread groups sum the chunks c = g, g + 8, ... (loads four chunks ahead) and
 // the 8 group sums are combined in group order through LDS.
-__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_rows, int k_cols,
+__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_rows, int k_cols, int k_off,
                                                           const float* __restrict__ partial, MlpWeightRef dst) {
     __shared__ float red[8][32];
     const long long n_el = (long long)n_rows * k_cols;
@@ -818,7 +851,7 @@ __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_ro
 #pragma unroll
         for (int g = 1; g < 8; ++g) t += red[g][l];
         const int n = (int)(e / k_cols), k = (int)(e - (long long)n * k_cols);
-        float* d = mlp_elem(dst, n, mlp_col(dst.map, k));
+        float* d = mlp_elem(dst, n, mlp_col(dst.map, k_off + k));
         if (d) *d = t;
     }
 }
@@ -867,12 +900,14 @@ void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const Ml
         hipLaunchKernelGGL((k_mlp_wgrad<N, K, TN, TK>), grid, dim3(64 * WgradShape<N, K, TN, TK>::WAVES), 0, s, p);
     // eight waves of half-size tiles, two per SIMD (8 x 8 at P = 1M: 0.92 ms per layer against 1.18 for four waves of
     // 4 x 4 blocks, one per SIMD: the second wave per SIMD hides the staging waits)
-    GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 3) else GSD_WGRAD(2, 8, 1, 2)
+    // (layer 5's 320 columns run as two calls, 64 + 256, both on the wide-load 8-wave shapes: 1.47 ms as one call)
+    GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 2, 2, 1) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 3)
+    else GSD_WGRAD(2, 8, 1, 2)
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
     hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 31) / 32)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
-                       32 * p.k_rb, (const float*)p.partial, dst);
-    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 31) / 32), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1,
+                       32 * p.k_rb, p.k_off, (const float*)p.partial, dst);
+    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 31) / 32), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1, 0,
                        (const float*)p.bias_partial, dst_b);
 }
 
