@@ -469,6 +469,10 @@ static int enqueue_render(const gsd_raster_args* a, void* geom_buffer, void* ima
     rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
     rp.out_color = out_color;
     rp.k_guard = k_guard; rp.k_cap = cap;
+    if (a->grad_scratch) {  // the backward's gradient records (gsd_rasterize_backward's scratch layout)
+        rp.zero_rec = reinterpret_cast<float4*>(align_ptr(a->grad_scratch));
+        rp.zero_n16 = (long long)gsd::kGradRec * a->P / 4;
+    }
     timed(kRenderFwd, s, [&] { gsd::launch_render_fwd(rp, s); });
     GSD_CHECK(a->debug, s);
     return GSD_OK;
@@ -550,10 +554,12 @@ int gsd_rasterize_backward(const gsd_raster_args* a, const int32_t* radii, const
     rp.ranges = im.ranges; rp.point_list = b.point_list; rp.rec = g.rec;
     rp.bg = a->background; rp.final_T = im.final_T; rp.n_contrib = im.n_contrib;
     rp.dL_dpix = dL_dout_color;
-    // the per-Gaussian gradient records (scratch) start at zero; render_bwd adds into them
+    // the per-Gaussian gradient records (scratch) start at zero; render_bwd adds into them.  A scratch the forward
+    // was given as args.grad_scratch was zeroed by its compositing kernel (ABI 14)
     float* rec = reinterpret_cast<float*>(align_ptr(scratch));
     rp.grad_rec = rec;
-    GSD_HIP(hipMemsetAsync(rec, 0, sizeof(float) * gsd::kGradRec * (size_t)a->P, s));
+    if (a->grad_scratch != scratch)
+        GSD_HIP(hipMemsetAsync(rec, 0, sizeof(float) * gsd::kGradRec * (size_t)a->P, s));
     if (K > 0) {
         timed(kRenderBwd, s, [&] { gsd::launch_render_bwd(rp, s); });
         GSD_CHECK(a->debug, s);

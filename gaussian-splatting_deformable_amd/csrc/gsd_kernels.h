@@ -184,6 +184,8 @@ struct RenderParams {
     float* out_color;
     const uint32_t* k_guard;  // optional: skip the launch when *k_guard (num_rendered) > k_cap
     uint32_t k_cap;
+    float4* zero_rec;         // optional: the backward's gradient records, zeroed by this launch (n16 float4s)
+    long long zero_n16;
 };
 
 struct RenderBwdParams {

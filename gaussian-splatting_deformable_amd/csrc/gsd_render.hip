@@ -245,9 +245,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     __shared__ float4 s_rgb[kTilePix];
     __shared__ float4 s_box[kTilePix];
     __shared__ __attribute__((aligned(4))) uint8_t s_list[4][kFwdGroups][kTilePix];
+    const int tid = threadIdx.x;
+    // the backward's gradient records cleared here, ahead of the capacity check (a relaunch after a short binning
+    // buffer clears them again): ~2 16-B stores per lane, issued before the VALU-bound compositing and never
+    // waited on, instead of a separate 64-B-per-Gaussian memset launch in the backward
+    if (p.zero_rec) {
+        const long long stride = (long long)gridDim.x * kTilePix;
+        for (long long e = (long long)blockIdx.x * kTilePix + tid; e < p.zero_n16; e += stride)
+            p.zero_rec[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     if (over_capacity(p.k_guard, p.k_cap)) return;
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);
-    const int tid = threadIdx.x;
     // `done` (the pixel has saturated, or lies outside the image) as the wave's lane mask: the per-record
     // decisions below are lane masks combined on the scalar unit and used as select masks
     // (__builtin_amdgcn_inverse_ballot_w64), so no bool is materialised in a vector register

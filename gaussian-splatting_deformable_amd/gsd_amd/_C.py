@@ -160,12 +160,19 @@ class _Args:
 _K_GUESS = {}   # device -> last num_rendered
 
 
+def backward_scratch_bytes(P):
+    """gsd_backward_scratch_bytes: the backward's gradient-record scratch (ABI 14: zeroed by a forward given it)."""
+    return int(_native.load().gsd_backward_scratch_bytes(int(P)))
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, debug, sh_split=None, activation=None):
+                        prefiltered, debug, sh_split=None, activation=None, grad_scratch=None):
     """RasterizeGaussiansCUDA (rasterize_points.cu:35-115):
     -> (num_rendered, color (3,H,W), radii (P,) int32, geomBuffer, binningBuffer, imgBuffer).
-    ``sh_split`` (a ShSplit, with ``sh`` empty) is this library's extension for the fused render path."""
+    ``sh_split`` (a ShSplit, with ``sh`` empty) is this library's extension for the fused render path.
+    ``grad_scratch`` (ABI 14): a uint8 device tensor of backward_scratch_bytes(P) that the forward zeroes for one
+    rasterize_gaussians_backward(..., scratch=grad_scratch) of this view (no memset in that backward)."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     lib = _native.load()
@@ -173,6 +180,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
               projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, debug,
               sh_split, activation)
     dev, P, H, W = a.dev, a.P, a.H, a.W
+    if grad_scratch is not None:
+        if (grad_scratch.device != dev or grad_scratch.dtype != torch.uint8
+                or grad_scratch.numel() < backward_scratch_bytes(P)):
+            raise RuntimeError("grad_scratch must be a uint8 device tensor of backward_scratch_bytes(P) bytes")
+        a.c.grad_scratch = grad_scratch.data_ptr()
     radii = torch.empty(P, dtype=torch.int32, device=dev)   # preprocess writes every entry (forward.cu:174)
     byte = dict(dtype=torch.uint8, device=dev)
     if P == 0:
@@ -205,7 +217,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
                                  campos, geomBuffer, R, binningBuffer, imageBuffer, debug, sh_split=None,
-                                 activation=None, raw_opacity=None, adam=None):
+                                 activation=None, raw_opacity=None, adam=None, scratch=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:117-196):
     -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
     With ``sh_split`` the SH gradients go to its sinks and dL_dsh is None; so is dL_dcov3D when no
@@ -213,7 +225,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     ``activation`` (a _native.Activation; scales / rotations and ``raw_opacity`` are then the raw parameters)
     the parameter gradients go to its sinks and only dL_dmeans2D (and dL_dcov3D, dL_dsh) are returned.
     ``adam`` (a _native.AdamEpilogue) fuses the Adam step of the SH pieces / raw parameters it names into this
-    backward: those are updated in place and their sinks are not written."""
+    backward: those are updated in place and their sinks are not written.  ``scratch``: the ``grad_scratch`` the
+    forward of this view zeroed (used once), or None (allocated and zeroed here)."""
     lib = _native.load()
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))  # rasterize_points.cu:142-143
     a = _Args(background, means3D, colors, raw_opacity if activation is not None else None, scales, rotations,
@@ -235,7 +248,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         views.append(slab[off:off + P * w].view(P, w) if w else None)
         off += P * w
     drot, dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales = views
-    scratch = torch.empty(lib.gsd_backward_scratch_bytes(P), dtype=torch.uint8, device=dev)
+    if scratch is not None and scratch.numel() >= lib.gsd_backward_scratch_bytes(P) and scratch.device == dev:
+        a.c.grad_scratch = scratch.data_ptr()   # zeroed by the forward: the backward skips its memset
+    else:
+        scratch = torch.empty(lib.gsd_backward_scratch_bytes(P), dtype=torch.uint8, device=dev)
     if dsh is not None:
         dsh = dsh.view(P, M, 3)
     if P != 0:

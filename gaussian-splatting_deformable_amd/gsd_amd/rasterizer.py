@@ -9,6 +9,7 @@ HIP kernels through ``gsd_amd._C``.
 """
 from __future__ import annotations
 
+import os
 from typing import NamedTuple
 
 import torch
@@ -108,7 +109,7 @@ class _RasterizeSplitSH(torch.autograd.Function):
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(
             rs.bg, means3D, None, opacities, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
             rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, None, rs.sh_degree, rs.campos, rs.prefiltered,
-            rs.debug, sh_split=split)
+            rs.debug, sh_split=split, grad_scratch=_grad_scratch(ctx, means3D))
         _save(ctx, rs, num_rendered, radii, means3D, scales, rotations, f_dc, f_rest, sh_offset, geomBuffer,
               binningBuffer, imgBuffer)
         return color, radii
@@ -140,7 +141,7 @@ class _RasterizeRaw(torch.autograd.Function):
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(
             rs.bg, xyz, None, opacity, scaling, rotation, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
             rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, None, rs.sh_degree, rs.campos, rs.prefiltered,
-            rs.debug, sh_split=split, activation=_native.Activation())
+            rs.debug, sh_split=split, activation=_native.Activation(), grad_scratch=_grad_scratch(ctx, xyz))
         _save(ctx, rs, num_rendered, radii, xyz, scaling, rotation, f_dc, f_rest, None, geomBuffer, binningBuffer,
               imgBuffer, opacity=opacity)
         return color, radii
@@ -169,6 +170,27 @@ class _RasterizeRaw(torch.autograd.Function):
         g_m2d, d_dc, d_rest, _, _ = _split_sh_backward(ctx, grad_out_color, activation=act, raw_opacity=opacity,
                                                        epi=epi, raw=raw)
         return ret[0], g_m2d, d_dc, d_rest, ret[1], ret[2], ret[3], None, None
+
+
+FWD_ZERO_SCRATCH = os.environ.get("GSD_FWD_ZERO_SCRATCH", "1") != "0"   # 0: the backward zeroes its own scratch
+
+
+def _grad_scratch(ctx, means3D):
+    """The backward's gradient-record scratch, allocated by the forward when a gradient will be asked for: the
+    forward's compositing kernel zeroes it (ABI 14 grad_scratch), so the backward needs no memset launch."""
+    ctx.grad_scratch = None
+    if FWD_ZERO_SCRATCH and any(ctx.needs_input_grad) and means3D.is_cuda and means3D.size(0) > 0:
+        ctx.grad_scratch = torch.empty(_C.backward_scratch_bytes(means3D.size(0)), dtype=torch.uint8,
+                                       device=means3D.device)
+    return ctx.grad_scratch
+
+
+def _take_scratch(ctx):
+    """The zeroed scratch for the first backward of this forward; None afterwards (a second backward through the
+    same graph zeroes a fresh one itself)."""
+    s = getattr(ctx, "grad_scratch", None)
+    ctx.grad_scratch = None
+    return s
 
 
 def _save(ctx, rs, num_rendered, radii, means3D, scales, rotations, f_dc, f_rest, sh_offset, geomBuffer,
@@ -217,7 +239,7 @@ def _split_sh_backward(ctx, grad_out_color, activation=None, raw_opacity=None, e
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
         binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity,
-        adam=epi)
+        adam=epi, scratch=_take_scratch(ctx))
     if epi is not None:   # parameters the kernel updated in place: autograd's saved-tensor checks must see it
         for p in (*raw, f_dc, f_rest):
             if id(p) in p._gsd_flat.fused:
@@ -282,7 +304,8 @@ def _backward_sh_views(ctx, rs, grad_out_color, means3D, scales, rotations, radi
     g_m2d, _, g_op, g_m3d, _, _, g_sc, g_rot = _C.rasterize_gaussians_backward(
         rs.bg, means3D, radii, None, scales, rotations, rs.scale_modifier, None, rs.viewmatrix, rs.projmatrix,
         rs.tanfovx, rs.tanfovy, grad_out_color, None, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered,
-        binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity)
+        binningBuffer, imgBuffer, rs.debug, sh_split=split, activation=activation, raw_opacity=raw_opacity,
+        scratch=_take_scratch(ctx))
     f_flat = getattr(f_dc, "_gsd_flat", None)
     if f_flat is not None:
         f_flat.verify_layout()   # every rank's P and settings agree before the P-sized all-gather

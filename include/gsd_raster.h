@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 13
+#define GSD_ABI_VERSION 14
 
 enum {
     GSD_OK = 0,
@@ -147,6 +147,12 @@ typedef struct gsd_raster_args {
     const gsd_sh_split* sh_split; /* NULL, or the split SH operand above (then shs == NULL) */
     const gsd_activation* activation; /* NULL, or: scales / rotations / opacities are raw parameters */
     const gsd_adam_epilogue* adam;    /* backward only: NULL, or the fused Adam step above (ABI 8) */
+    void* grad_scratch;         /* ABI 14.  Forward: NULL, or a buffer of gsd_backward_scratch_bytes(P) bytes that
+                                   the compositing kernel zeroes (under its VALU-bound work, instead of a separate
+                                   64-B-per-Gaussian memset in the backward).  Backward: when it equals the
+                                   backward's `scratch` argument, that scratch is taken as zeroed by the forward
+                                   that was given it and is not cleared again (pass it to ONE backward only);
+                                   NULL or any other value: the backward zeroes its scratch itself. */
 } gsd_raster_args;
 
 int gsd_abi_version(void);

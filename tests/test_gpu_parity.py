@@ -157,6 +157,38 @@ def test_backward_matches_oracle(oracle_mod, P, W, H, deg, seed):
         assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
 
 
+@pytest.mark.parametrize("short_binning", [False, True])
+def test_backward_with_forward_zeroed_scratch(oracle_mod, short_binning):
+    """ABI 14 grad_scratch: the forward's compositing kernel zeroes the backward's gradient records (here a
+    NaN-filled buffer) and the backward given that scratch skips its memset -- gradients still match the oracle.
+    short_binning: the first phase-2 launch is cut short by a small binning buffer, the relaunch zeroes again."""
+    from gsd_amd import _C
+    P, W, H, deg, seed = 6_000, 640, 360, 3, 4
+    d = scene_inputs(P, W, H, deg, seed=seed, device=DEV)
+    g = torch.Generator().manual_seed(seed)
+    dpix = torch.randn(3, H, W, generator=g).mul_(1e-3).to(DEV)
+    o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    scratch = torch.full((_C.backward_scratch_bytes(P),), 0xFF, dtype=torch.uint8, device=DEV)   # NaN floats
+    if short_binning:
+        _C._K_GUESS[torch.device(DEV)] = 8
+    empty = torch.empty(0)
+    fwd = _C.rasterize_gaussians(d["bg"], d["means3D"], empty, d["opacities"], d["scales"], d["rotations"], 1.0,
+                                 empty, d["viewmatrix"], d["projmatrix"], d["tanfovx"], d["tanfovy"], d["H"], d["W"],
+                                 d["shs"], d["sh_degree"], d["campos"], False, False, grad_scratch=scratch)
+    check_forward_against(o, d, fwd)
+    K, color, radii, geom, binning, img = fwd
+    grads = _C.rasterize_gaussians_backward(d["bg"], d["means3D"], radii, empty, d["scales"], d["rotations"], 1.0,
+                                            empty, d["viewmatrix"], d["projmatrix"], d["tanfovx"], d["tanfovy"], dpix,
+                                            d["shs"], d["sh_degree"], d["campos"], geom, K, binning, img, False,
+                                            scratch=scratch)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for name, gt in zip(names, grads):
+        got = gt.cpu().numpy().reshape(ob[name].shape)
+        assert np.isfinite(got).all(), name
+        assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
+
+
 def test_backward_low_opacity(oracle_mod):
     """Opacity logits down to -9 (o ~ 1.2e-4, far below the 1/255 alpha floor) and up to +4: every gradient,
     dL/dopacity included, within rel L2 1e-4 of the oracle's sum of G * dL/dalpha (backward.cu:552), and
