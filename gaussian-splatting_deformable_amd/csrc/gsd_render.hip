@@ -187,6 +187,22 @@ __device__ __forceinline__ float gauss_exp(float power) {
     return __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
 #endif
 }
+// The threshold decision alpha >= 1/255 (forward.cu:345, backward.cu:501) taken on the fast exp is final only
+// outside a narrow band around the threshold: the fast G is within ~4.5e-7 (relative) of exp(power), so where o G
+// lies within 2^-18 (3.8e-6) of 1/255 both passes recompute G with the libm-accurate expf (<= 1 ulp) and decide on
+// that.  The band is rare (a few pairs per million) and its lanes are wave-divergent, so it costs one compare per
+// pair and a scalar branch; the decisions then differ from the reference's only where its own alpha lies within
+// the two expf implementations' ulp of 1/255.
+constexpr float kAlphaThr = 1.0f / 255.0f;
+constexpr float kAlphaLo = kAlphaThr * (1.0f - 3.814697265625e-06f);
+constexpr float kAlphaHi = kAlphaThr * (1.0f + 3.814697265625e-06f);
+// o G with the accurate exp (the band's recomputation); pc / bo staged as below
+__device__ __forceinline__ float record_og_precise(float4 pc, float2 bo, float pxf, float pyf) {
+    const float dx = pc.x - pxf;
+    const float dy = pc.y - pyf;
+    const float power = (pc.z * dx * dx + pc.w * dy * dy) - bo.x * dx * dy;
+    return bo.y * expf(power);
+}
 // The render kernels stage a record as pc = (mx, my, -a/2, -c/2) and bo = (b, o): with the halves folded into
 // the staged conic, (-a/2 dx) dx + (-c/2 dy) dy is exactly -0.5f * (a dx dx + c dy dy) (scaling by a power of
 // two commutes with rounding), so power below has the reference's bits with one multiply fewer per pair.
@@ -328,8 +344,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 if (j0 + u >= m) break;
-                unsigned long long take_m = ~done_m & in_m[u] & wave_ballot(keep[u]) &
-                                            wave_ballot(a[u] >= 1.0f / 255.0f);
+                unsigned long long take_m = ~done_m & in_m[u] & wave_ballot(keep[u]) & wave_ballot(a[u] >= kAlphaLo);
+                const unsigned long long near_m = take_m & wave_ballot(a[u] < kAlphaHi);
+                if (near_m) {  // rare: o G within the fast exp's error band of 1/255 -- decide on the accurate exp
+                    const bool near = __builtin_amdgcn_inverse_ballot_w64(near_m);
+                    if (near) a[u] = fminf(0.99f, record_og_precise(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf));
+                    take_m &= ~(near_m & wave_ballot(!(a[u] >= kAlphaThr)));
+                }
                 if (!take_m) continue;
                 const float alpha = a[u];
                 const float test_T = T * (1 - alpha);
@@ -496,12 +517,17 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                         float G;
                         bool keep;
                         record_alpha(pc, bo, pxf, pyf, G, keep);
-                        const float OG = bo.y * G;  // o G: alpha before the 0.99 clamp (the same product)
+                        float OG = bo.y * G;  // o G: alpha before the 0.99 clamp (the same product)
                         // backward.cu:487-488 (list position below the pixel's last contributor); alpha =
                         // min(0.99, o G) >= 1/255 <=> !(o G < 1/255), NaN included (fminf(0.99, NaN) = 0.99)
-                        const unsigned long long valid_m = (U < nv ? ~0ull : 0ull) &
-                                                           wave_ballot(j0 + U >= first_valid) &
-                                                           wave_ballot(keep) & wave_ballot(!(OG < 1.0f / 255.0f));
+                        unsigned long long valid_m = (U < nv ? ~0ull : 0ull) & wave_ballot(j0 + U >= first_valid) &
+                                                     wave_ballot(keep) & wave_ballot(!(OG < kAlphaLo));
+                        const unsigned long long near_m = valid_m & wave_ballot(OG < kAlphaHi);
+                        if (near_m) {  // rare: the forward's band recomputation, so both passes decide alike
+                            if (__builtin_amdgcn_inverse_ballot_w64(near_m))
+                                OG = record_og_precise(pc, bo, pxf, pyf);
+                            valid_m &= ~(near_m & wave_ballot(OG < kAlphaThr));
+                        }
                         any_m |= valid_m;
                         {
 #pragma clang fp contract(fast)

@@ -59,7 +59,7 @@ def lib():
                                   _vp, _vp, _vp]
         L.orc_render_fwd.restype = None
         L.orc_render_fwd.argtypes = [ctypes.c_int, ctypes.c_int, _u32p, _u32p, _f32p, _f32p, _f32p, _f32p, _f32p,
-                                     _f32p, _u32p]
+                                     _f32p, _u32p, _vp]
         L.orc_render_bwd.restype = None
         L.orc_render_bwd.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u32p, _u32p, _f32p, _f32p, _f32p,
                                      _f32p, _f32p, _u32p, _f32p, _f32p, _f32p, _f32p, _f32p]
@@ -177,12 +177,13 @@ def forward(means3D, opacities, *, shs=None, colors_precomp=None, scales=None, r
     color = np.zeros((3, H, W), np.float32)
     final_T = np.zeros(H * W, np.float32)
     n_contrib = np.zeros(H * W, np.uint32)
+    margin = np.zeros((H * W, 2), np.float32)
     L.orc_render_fwd(W, H, ranges, np.ascontiguousarray(vals), means2D, np.ascontiguousarray(feats), conic, bg,
-                     color, final_T, n_contrib)
+                     color, final_T, n_contrib, margin.ctypes.data_as(_vp))
     return dict(num_rendered=K, color=color, radii=radii, means2D=means2D, depths=depths, cov3D=cov3D, rgb=rgb,
                 conic_opacity=conic, tiles_touched=touched, clamped=clamped, point_offsets=offsets, keys=keys,
                 point_list=vals, ranges=ranges, final_T=final_T.reshape(H, W), n_contrib=n_contrib.reshape(H, W),
-                M=M, P=P)
+                margin_alpha=margin[:, 0].reshape(H, W), margin_T=margin[:, 1].reshape(H, W), M=M, P=P)
 
 
 def backward(fwd, dL_dpix, means3D, *, shs=None, colors_precomp=None, scales=None, rotations=None,

@@ -28,6 +28,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -354,7 +355,7 @@ int64_t orc_binning(int P, int W, int H, const float* means2D, const float* dept
 /* forward.cu:261-374 renderCUDA (per pixel; the 256-wide batching does not change results) */
 void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_list, const float* means2D,
                     const float* features, const float* conic_opacity, const float* bg,
-                    float* out_color, float* final_T, uint32_t* n_contrib) {
+                    float* out_color, float* final_T, uint32_t* n_contrib, float* margin) {
     const int gx = (W + TILE_X - 1) / TILE_X, gy = (H + TILE_Y - 1) / TILE_Y;
 #pragma omp parallel for collapse(2) schedule(dynamic, 1) num_threads(NT)
     for (int ty = 0; ty < gy; ++ty)
@@ -364,6 +365,10 @@ void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_
                 for (int px = tx * TILE_X; px < tx * TILE_X + TILE_X && px < W; ++px) {
                     float T = 1.0f, C[3] = {0, 0, 0};
                     uint32_t contributor = 0, last = 0;
+                    /* decision margins (test infrastructure, not the reference): the smallest relative distance of
+                     * an evaluated alpha from 1/255 and of a tested T (1 - alpha) from 1e-4 -- where either is within
+                     * the exp's rounding, an implementation with another expf may decide the other way */
+                    float m_alpha = INFINITY, m_T = INFINITY;
                     const float fx = (float)px, fy = (float)py;
                     for (uint32_t k = r0; k < r1; ++k) {
                         contributor++;
@@ -373,8 +378,10 @@ void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_
                         float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                         if (power > 0.0f) continue;
                         float alpha = fminf_(0.99f, co[3] * expf(power));
+                        if (margin) m_alpha = fminf(m_alpha, fabsf((float)((double)alpha * 255.0 - 1.0)));
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1 - alpha);
+                        if (margin) m_T = fminf(m_T, fabsf((float)((double)test_T * 1e4 - 1.0)));
                         if (test_T < 0.0001f) break;
                         for (int ch = 0; ch < 3; ++ch) C[ch] += features[3 * g + ch] * alpha * T;
                         T = test_T;
@@ -383,6 +390,7 @@ void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_
                     const int pid = W * py + px;
                     final_T[pid] = T;
                     n_contrib[pid] = last;
+                    if (margin) { margin[2 * pid] = m_alpha; margin[2 * pid + 1] = m_T; }
                     for (int ch = 0; ch < 3; ++ch) out_color[ch * H * W + pid] = C[ch] + T * bg[ch];
                 }
         }
@@ -398,9 +406,23 @@ void orc_render_bwd(int P, int W, int H, const uint32_t* ranges, const uint32_t*
                     const uint32_t* n_contrib, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
                     float* dL_dopacity, float* dL_dcolors) {
     const int gx = (W + TILE_X - 1) / TILE_X, gy = (H + TILE_Y - 1) / TILE_Y;
-    const int nt = NT;
-    /* one double accumulator set per thread: m2x m2y cx cy cw op r g b */
-    double* accs = (double*)calloc(((size_t)P * 9 + 1) * nt, sizeof(double));
+    /* one double accumulator set per thread: m2x m2y cx cy cw op r g b.  The thread count is capped so the sets
+     * stay within 2 GiB (72 B per Gaussian each: many-core hosts would otherwise ask for tens of GB), and an
+     * allocation failure halves it down to one thread before failing loudly. */
+    const size_t per_thread = ((size_t)P * 9 + 1) * sizeof(double);
+    int nt = NT;
+    const size_t budget = (size_t)2 << 30;
+    if ((size_t)nt * per_thread > budget) nt = (int)(budget / per_thread) > 1 ? (int)(budget / per_thread) : 1;
+    double* accs = NULL;
+    for (;;) {
+        accs = (double*)calloc((size_t)nt * per_thread / sizeof(double), sizeof(double));
+        if (accs || nt == 1) break;
+        nt /= 2;
+    }
+    if (!accs) {
+        fprintf(stderr, "orc_render_bwd: cannot allocate %zu bytes of accumulators\n", per_thread);
+        abort();
+    }
     const float ddelx_dx = (float)(0.5 * W), ddely_dy = (float)(0.5 * H);
 #pragma omp parallel num_threads(nt)
     {

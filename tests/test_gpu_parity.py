@@ -3,10 +3,11 @@
 Bars (DESIGN.md "Parity"):
   bit-exact   radii, depths, means2D, conic/opacity, rgb, clamp flags, num_rendered,
               ranges, point_list (== the reference's stable sort of |tile|depth| keys)
-  tolerance   image and final_T |diff| <= 1e-5 except at compositing-decision flips (alpha within ulps
-              of 1/255, T near 1e-4: v_exp_f32 vs expf) -- at most 3e-5 of the pixels, each <= 1e-2,
-              mean |diff| <= 1e-7 (image_bar); n_contrib mismatches <= 0.1% of pixels; gradients: per-tensor relative L2 <= 1e-4 (float atomics
-              reorder sums), SE(3) deform vs float64 autograd: rel L2 <= 1e-5.
+  tolerance   image and final_T |diff| <= 1e-5 and n_contrib exact at every pixel whose compositing decisions are
+              not borderline in the oracle; at a borderline pixel (some alpha within 1e-6 of 1/255, or some
+              T (1 - alpha) within 3e-5 of 1e-4, relative) a decision may flip -- the flips are counted and
+              reported, and there |diff| <= 1e-2 (image_bar).  Mean |diff| <= 1e-7.  Gradients: per-tensor
+              relative L2 <= 1e-4 (float atomics reorder sums), SE(3) deform vs float64 autograd: rel L2 <= 1e-5.
 """
 from __future__ import annotations
 
@@ -105,26 +106,43 @@ def check_forward_against(o, d, fwd, colors=None):
     np.testing.assert_array_equal(st["point_list"].astype(np.uint32), o["point_list"])
     # the reference's sort keys, rebuilt from (tile of the range, depth bits of the id): identical
     c = color.cpu().numpy()
-    image_bar(c, o["color"], st["final_T"], o["final_T"])
-    nc_mismatch = np.mean(st["n_contrib"].astype(np.uint32) != o["n_contrib"])
-    assert nc_mismatch <= 1e-3, nc_mismatch
+    image_bar(c, st["final_T"], st["n_contrib"], o, tag=f"P={d['means3D'].shape[0]} {d['W']}x{d['H']}")
     return K
 
 
-def image_bar(c, c_ref, T, T_ref):
-    """Image and final_T bars: |diff| <= 1e-5 at every pixel but those where a compositing decision
-    flips between the hardware exp (v_exp_f32, a few ulp) and the oracle's expf -- an alpha within ulps of 1/255
-    or T (1 - alpha) within ulps of 1e-4.  There one record's contribution (alpha T c < 1/255 + 1e-4) and the
-    small change it makes to the T behind it differ: such pixels may differ by up to 1e-2, and there may be at
-    most 3e-5 of all pixels (~60 at 1080p, ~250 at 4K; a handful were seen at 4K).  Mean |diff| <= 1e-7."""
+# Borderline decisions (the oracle's per-pixel margins, oracle.forward): alpha within ALPHA_MARGIN (relative) of
+# 1/255 -- the HIP kernels decide such alphas on the accurate expf (a band of 3.8e-6 around the threshold, where
+# the hardware exp's few-ulp error could matter), so only the two expf implementations' ulp can still separate
+# them; T (1 - alpha) within T_MARGIN of 1e-4 -- T carries the hardware exp's few-ulp alpha differences of every
+# record before it (up to ~3e-6 relative at T = 1e-4).
+ALPHA_MARGIN = 1e-6
+T_MARGIN = 3e-5
+
+
+def image_bar(c, T, nc, o, tag=""):
+    """Image / final_T / n_contrib bars against the oracle forward `o`.  Outside the borderline
+    pixels: |diff| <= 1e-5 and n_contrib exact.  A pixel whose result differs beyond that must be borderline (a
+    flip); flips are counted and reported (GSD_PARITY_REPORT: a JSONL file to append the counts to), and bounded
+    by 1e-2 (one record's contribution, alpha T c < 1/255 + 1e-4, and the T behind it).  Mean |diff| <= 1e-7."""
+    import json
+    import os
+    c_ref, T_ref, nc_ref = o["color"], o["final_T"], o["n_contrib"]
+    border = (o["margin_alpha"] < ALPHA_MARGIN) | (o["margin_T"] < T_MARGIN)
     dc = np.abs(c - c_ref).max(axis=0)          # per pixel, over the channels
     dT = np.abs(T - T_ref)
-    flips = (dc > 1e-5) | (dT > 1e-5)
-    npix = dc.size
-    assert flips.sum() <= max(2, 3e-5 * npix), (int(flips.sum()), float(dc.max()), float(dT.max()))
-    assert dc.max() <= 1e-2 and dT.max() <= 1e-2, (float(dc.max()), float(dT.max()))
+    nc_bad = nc.astype(np.uint32) != nc_ref
+    flips = (dc > 1e-5) | (dT > 1e-5) | nc_bad
+    stats = dict(tag=tag, pixels=int(dc.size), borderline=int(border.sum()), flips=int(flips.sum()),
+                 n_contrib_mismatch=int(nc_bad.sum()),
+                 alpha_borderline=int((o["margin_alpha"] < ALPHA_MARGIN).sum()),
+                 max_abs_outside=float(dc[~border].max(initial=0.0)), max_abs_flips=float(dc[flips].max(initial=0.0)))
+    if os.environ.get("GSD_PARITY_REPORT"):
+        with open(os.environ["GSD_PARITY_REPORT"], "a") as f:
+            f.write(json.dumps(stats) + "\n")
+    assert not (flips & ~border).any(), ("a decision flipped at a non-borderline pixel", stats)
+    assert dc.max() <= 1e-2 and dT.max() <= 1e-2, stats
     assert np.abs(c - c_ref).mean() <= 1e-7 and dT.mean() <= 1e-7, (np.abs(c - c_ref).mean(), dT.mean())
-    return int(flips.sum())
+    return stats
 
 
 CASES = [  # (P, W, H, deg, seed): config-1 shape, odd sizes, every SH degree
