@@ -21,7 +21,15 @@ of the same workload (VALU issue for the render kernels, HBM otherwise; traffic
 null when no PMC pass of that workload exists); and the CPU baseline -- the
 OpenMP C oracle on the host's cores, full views of the same workload for ~10 s.
 
-  python bench.py [--gpus N --steps K --warmup W --config 4 --cpu-baseline auto|off]
+Every step also updates the densification statistics (max_radii2D and add_densification_stats, train.py:610-618,
+which the reference runs every iteration below densify_until_iter); configuration 5 also runs densify_and_prune.
+
+``--with-mlp``: the whole reference training step -- the deformation network DirectTemporalNeRF
+(gaussian_model.py:242-316) live in render() at iteration 5000 (offsets on means, scales, rotations and SH), the
+offset-norm term of the loss (train.py:329-332) and the network's Adam group (training_setup :843, the offset
+schedule's rate at that iteration).  A separate line (config.workload says "MLP live"); the headline is without.
+
+  python bench.py [--gpus N --steps K --warmup W --config 4 --cpu-baseline auto|off --with-mlp]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 ``--gpus N`` means N ranks: without a launcher (no WORLD_SIZE in the environment) and N > 1, this process
@@ -76,6 +84,21 @@ def algorithmic_bytes(P, V, K, W, H, C):
     }
 
 
+# the deformation network (DirectTemporalNeRF): multiply-adds per Gaussian of one forward -- 84 -> 256, six
+# 256 -> 256, the skip layer 319 -> 256, the four heads 256 -> 58
+MLP_MACS_PER_GAUSSIAN = 84 * 256 + 6 * 256 * 256 + 319 * 256 + 256 * 58
+# f32 training GEMMs on the bf16 matrix cores at f32 accuracy (BF16x6: six bf16 MFMAs per f32 product): the f32-
+# equivalent roof is the dense bf16 peak (MI355X_MICROARCH.md, 2.5166 PFLOP/s) / 6
+BF16X6_PEAK_TFLOPS = 2516.6 / 6.0
+
+
+def mfma_flops(P):
+    """Algorithmic FLOPs per call of the deformation network's training kernels: the forward's GEMMs, and the
+    backward's dX GEMMs (dL/dx included, as the reference's autograd computes it) plus its weight gradients."""
+    f = 2.0 * MLP_MACS_PER_GAUSSIAN * P
+    return {"deform_mlp_train_fwd": f, "deform_mlp_train_bwd": 2.0 * f}
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes (and the VALU issue figures) per launch of ``kernel`` from the newest committed PMC summary of
     the same workload (profiles/**/pmc_traffic.json whose "_workload" is ``workload``, e.g. "cfg4"; written by
@@ -125,17 +148,30 @@ def roofline(kernel, ms, nbytes, workload):
     return roof
 
 
+def mfma_roofline(kernel, ms, flops, workload):
+    """A matrix-core kernel against the BF16x6 f32-equivalent roof: algorithmic FLOPs / live launch time."""
+    ach = flops / (ms * 1e-3) / 1e12
+    return {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2), "peak": round(BF16X6_PEAK_TFLOPS, 1),
+            "unit": "TFLOP/s", "frac": round(ach / BF16X6_PEAK_TFLOPS, 4), "traffic": None,
+            "algorithmic_flops": flops, "avg_launch_ms": round(ms, 4), "workload": workload}
+
+
 FUSED_STEP = os.environ.get("GSD_FUSED_STEP", "1") != "0"
+MLP_ITERATION = 5000   # >= 3000: the network's offsets are live (gaussian_model.py:308-313)
 
 
-def make_optimizer(pc):
+def make_optimizer(pc, net=None):
     """training_setup (scene/gaussian_model.py:834-864) param groups, spatial_lr_scale = 1, eps 1e-15, as one
     fused HIP Adam over flat slabs (gsd_amd.optim.FusedAdam; torch.optim.Adam semantics).  In the SE(3) mode the
     per-Gaussian twist (the deformation network's output in the dormant reference path,
     scene/gaussian_model.py:99-173) is a trained parameter of its own group, so d_se3 reaches the optimizer."""
     from gsd_amd.optim import FusedAdam
-    groups = [
-        {"params": [pc._xyz], "lr": 0.00016, "name": "xyz"},
+    groups = [{"params": [pc._xyz], "lr": 0.00016, "name": "xyz"}]
+    if net is not None:   # training_setup :843, at the offset schedule's rate of the bench's iteration
+        from gsd_amd.schedule import offset_schedule
+        groups.append({"params": list(net.parameters()), "lr": float(offset_schedule()(MLP_ITERATION)),
+                       "name": "offset_model"})
+    groups += [
         {"params": [pc._features_dc], "lr": 0.0025, "name": "f_dc"},
         {"params": [pc._features_rest], "lr": 0.0025 / 20.0, "name": "f_rest"},
         {"params": [pc._opacity], "lr": 0.05, "name": "opacity"},
@@ -242,6 +278,8 @@ def main():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--densify-interval", type=int, default=None,
                     help="densify_and_prune every N steps (train.py:610-648); default 100 for config 5, else off")
+    ap.add_argument("--with-mlp", action="store_true",
+                    help="DirectTemporalNeRF live in the step (iteration 5000): offsets, offset-norm loss, its Adam")
     args = ap.parse_args()
     err = check_ranks(args.gpus)
     if err:
@@ -270,7 +308,16 @@ def main():
     # configuration 5: "densification/prune step active" -- densify_and_prune every 100 views, so P changes
     densify_every = args.densify_interval if args.densify_interval is not None else (100 if args.config == 5 else 0)
     params = make_gaussians(P, W, H, seed=args.config, se3=cfg.get("se3")).to(dev)   # replicated on every rank
-    pc = DeformableGaussians(params, sh_degree=D, deform="se3" if se3 else "additive")
+    net = None
+    if args.with_mlp:
+        if se3:
+            print("bench.py: --with-mlp runs the reference's additive deform (configurations 2, 4, 5)", file=sys.stderr)
+            sys.exit(2)
+        from gsd_amd.deform_mlp import DirectTemporalNeRF
+        torch.manual_seed(1234)   # the same initial network on every rank
+        net = DirectTemporalNeRF().to(dev)
+    iteration = MLP_ITERATION if net is not None else 0
+    pc = DeformableGaussians(params, sh_degree=D, deform="se3" if se3 else "additive", offset_model=net)
     cam = synthetic_camera(W, H, yaw_deg=2.0 * rank).to(dev)     # one view per GPU, yaw offsets k*2 deg
     bg = torch.zeros(3, device=dev)
     pipe = default_pipe()
@@ -278,15 +325,13 @@ def main():
     # so the optimisation stays near the configured workload (a random target drives opacities and scales
     # away from it within tens of steps, shrinking num_rendered while the bench runs)
     with torch.no_grad():
-        target = render(cam, pc, pipe, bg)["render"]
+        target = render(cam, pc, pipe, bg, iteration)["render"]
         noise = torch.randn(3, H, W, generator=torch.Generator().manual_seed(100 + rank)).to(dev)
         target = (target + 0.02 * noise).clamp_(0.0, 1.0)
-    opt = make_optimizer(pc)
+    opt = make_optimizer(pc, net)
     # every .grad is a view of one slab (opt.flat): the one buffer the all-reduce sums
-    dens = None
-    if densify_every:
-        from gsd_amd.densify import GaussianDensifier
-        dens = GaussianDensifier(pc, opt)
+    from gsd_amd.densify import GaussianDensifier
+    dens = GaussianDensifier(pc, opt)   # the statistics run every step; densify_and_prune every densify_every
     nstep = [0]
 
     # autograd's seed gradient d loss / d loss = 1, allocated once (a bare loss.backward() launches a fill each
@@ -294,7 +339,7 @@ def main():
     seed = torch.ones((), device=dev)
 
     def step():
-        out = render(cam, pc, pipe, bg)
+        out = render(cam, pc, pipe, bg, iteration)
         # train.py:323-332 + :529, lambda_dssim = 0.2: the offset-norm term is 0 (and skipped) when nothing moves
         # the means (configurations 2, 4, 5); in the SE(3) mode (1, 3) it is the moved distance's mean norm
         loss = training_loss(out["render"], target, out["means3D_offset"], 0.2)
@@ -310,37 +355,37 @@ def main():
             # over each bucket as its sum arrives; a no-op collective at N = 1.  The gradient slab is marked
             # stale for the next step instead of cleared.
             opt.allreduce_step(zero_grad=True)
-        if dens is not None:
-            # train.py:610-648 with the reference's thresholds (densify_grad_threshold 0.0002, min opacity 0.005);
-            # the synthetic scene's extent is its depth range (z in [2, 10])
-            dens.add_densification_stats(out["viewspace_points"], out["radii"])
-            nstep[0] += 1
-            if nstep[0] % densify_every == 0:
-                dens.densify_and_prune(0.0002, 0.005, 10.0, None)   # new slabs (FusedAdam.rebuild): opt.flat
+        # train.py:610-618, every iteration below densify_until_iter: max_radii2D + add_densification_stats (one
+        # fused pass); train.py:640-644 with the reference's thresholds (densify_grad_threshold 0.0002, min opacity
+        # 0.005) every densify_every steps; the synthetic scene's extent is its depth range (z in [2, 10])
+        dens.add_densification_stats(out["viewspace_points"], out["radii"])
+        nstep[0] += 1
+        if densify_every and nstep[0] % densify_every == 0:
+            dens.densify_and_prune(0.0002, 0.005, 10.0, None)   # new slabs (FusedAdam.rebuild): opt.flat
         return out
 
     # Adam moves every parameter by ~lr per step whatever the gradient, so the scene drifts from the configured
     # workload as steps accumulate; each measurement below starts from the initial parameters and optimizer
     # state (restored outside the timed regions; with densification the initial scene is rebuilt, P included)
-    snapshot = [p.detach().clone() for p in pc.parameters()]
+    trained = list(pc.parameters()) + (list(net.parameters()) if net is not None else [])
+    snapshot = [p.detach().clone() for p in trained]
 
     def restore():
         with torch.no_grad():
-            if dens is not None and pc._xyz.shape[0] != snapshot[0].shape[0]:   # densified: the initial P back
+            if pc._xyz.shape[0] != snapshot[0].shape[0]:   # densified: the initial P back
                 init = dict(zip(dens._names(), snapshot))
                 dens._apply(lambda n, d, m, v: (init[n].clone(), torch.zeros_like(init[n]), torch.zeros_like(init[n])))
-            for p, s0 in zip(pc.parameters(), snapshot):
+            for p, s0 in zip(trained, snapshot):
                 p.copy_(s0)
             opt.reset_state()
-            if dens is not None:
-                dens._reset_stats()
+            dens._reset_stats()
         nstep[0] = 0
         opt.flat.invalidate()   # as a fresh optimizer: no gradients yet
 
     gc.collect()   # before the warmup, so the device is busy again when the timed steps start
     for _ in range(args.warmup):
         step()
-    if dens is not None:
+    if densify_every:
         # one densification in the warmup as well: PyTorch loads each elementwise kernel's code object on its
         # first launch (~0.1 s over densify_and_prune's ops on a fresh process), a one-time cost, not a step's
         dens.densify_and_prune(0.0002, 0.005, 10.0, None)
@@ -411,7 +456,7 @@ def main():
             if queued:
                 torch.cuda._sleep(2_000_000)
             e0.record()
-            o = render(cam, pc, pipe, bg)
+            o = render(cam, pc, pipe, bg, iteration)
             training_loss(o["render"], target, o["means3D_offset"], 0.2).backward(seed)
             e1.record()
             torch.cuda.synchronize()
@@ -475,7 +520,10 @@ def main():
         per_kernel = {k: tot / max(n, 1) for k, (tot, n) in kt.items()}
         dom = max(kt, key=lambda k: kt[k][0]) if kt else None
         roof = None
-        if dom:
+        if dom in mfma_flops(1):   # the deformation network's training call (--with-mlp): the matrix cores
+            roof = mfma_roofline(dom, per_kernel[dom], mfma_flops(int(pc._xyz.shape[0]))[dom],
+                                 f"cfg{args.config}+mlp")
+        elif dom:
             # the kernel-timing pass's scene: V and K of its last view, P of that view (no densification in it)
             nbytes = algorithmic_bytes(int(pc._xyz.shape[0]), V, K, W, H, (min(D, 3) + 1) ** 2).get(dom)
             if nbytes:
@@ -498,14 +546,19 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"cfg{args.config}: {P} Gaussians, SH deg {D}, {W}x{H}, 1 view/GPU; "
                                    + ("per-Gaussian SE(3) deform (fused exp-map) + " if se3 else "")
-                                   + "render fwd + 0.8 L1 + 0.2 (1 - SSIM) + bwd"
+                                   + ("MLP live: DirectTemporalNeRF offsets (iteration 5000) + " if net is not None
+                                      else "")
+                                   + "render fwd + 0.8 L1 + 0.2 (1 - SSIM)"
+                                   + (" + 0.1 mean |offset|" if net is not None else "") + " + bwd"
                                    + (" + d_se3" if se3 else "")
-                                   + " + RCCL all-reduce of per-Gaussian grads + Adam"
+                                   + (" + MLP bwd" if net is not None else "")
+                                   + " + densification statistics + RCCL all-reduce of per-Gaussian grads + Adam"
+                                   + (" (incl. the MLP's group)" if net is not None else "")
                                    + (f"; densify_and_prune every {densify_every} steps" if densify_every else ""),
                        "P": P, "width": W, "height": H, "sh_degree": D, "views_per_step": world,
                        "parallelism": f"dp{world}", "visible": V, "num_rendered": K,
                        "num_rendered_timed_first": K_start, "num_rendered_timed_last": K_end,
-                       "densify_interval": densify_every or None,
+                       "densify_interval": densify_every or None, "deform_mlp": net is not None,
                        "P_timed_last": P_end},
             "fwd_bwd_ms_per_view": round(fwd_bwd_ms, 4),
             "fwd_bwd_ms_per_view_host_synced": round(fwd_bwd_synced_ms, 4),

@@ -23,6 +23,10 @@ constexpr float kSH3_0 = -0.5900435899266435f, kSH3_1 = 2.890611442640554f, kSH3
                 kSH3_3 = 0.3731763325901154f, kSH3_4 = -0.4570457994644658f, kSH3_5 = 1.445305721320277f,
                 kSH3_6 = -0.5900435899266435f;
 
+// F.relu as torch computes it (clamp_min): NaN propagates -- fmaxf(NaN, 0) would return 0 and hide a diverging
+// network behind finite outputs and zero gradients
+__device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.f); }
+
 // The 4x4 camera matrices, read once per block into SGPR-resident registers.
 struct Mat4 {
     float m[16];

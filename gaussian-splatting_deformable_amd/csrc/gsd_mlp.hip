@@ -133,7 +133,7 @@ __device__ __forceinline__ void mlp_hidden_epilogue(const f32x16 (&acc)[NC][8], 
             for (int s = 0; s < 2; ++s)
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    act[c][2 * rb + s][j] = (__bf16)fmaxf(acc[c][rb][8 * s + j] + bv[8 * s + j], 0.f);
+                    act[c][2 * rb + s][j] = (__bf16)relu_nan(acc[c][rb][8 * s + j] + bv[8 * s + j]);
     }
 }
 

@@ -214,9 +214,9 @@ __device__ __forceinline__ void gemm_epilogue(const MlpGemmParams& p, const f32x
                 const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float y = fmaxf(acc[r][4 * j + i] + bq[i], 0.f);
+                    const float y = relu_nan(acc[r][4 * j + i] + bq[i]);
                     v[4 * j + i] = y;
-                    bits_out |= (y > 0.f ? 1u : 0u) << (4 * j + i);
+                    bits_out |= (!(y <= 0.f) ? 1u : 0u) << (4 * j + i);
                 }
             }
             if (p.mask_out) p.mask_out[(size_t)((rb0 + r) * 2 + h) * p.ldp + g] = (unsigned short)bits_out;
@@ -526,9 +526,9 @@ __device__ __forceinline__ void fused_hidden_epilogue(const float* s_bias, int h
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int q = 4 * q4 + i;
-                const float y = fmaxf(acc[rb][q] + bq[i], 0.f);
+                const float y = relu_nan(acc[rb][q] + bq[i]);
                 act[2 * rb + (q >> 3)][q & 7] = y;
-                w |= (y > 0.f ? 1u : 0u) << q;
+                w |= (!(y <= 0.f) ? 1u : 0u) << q;
             }
         }
         bits[rb] = w;

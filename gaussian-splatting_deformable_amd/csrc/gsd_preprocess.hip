@@ -202,10 +202,11 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     RenderRec* rr = p.rec + idx;  // what the render kernels gather per instance (RenderRec)
     rr->q0 = make_float4(pix.x, pix.y, co.x, co.y);
     rr->q1 = make_float4(co.z, co.w, col.x, col.y);
-    // the backward's exact ellipse culling: alpha >= 1/255 <=> Q <= 2 ln(255 o), with 0.1 % + 0.05 of slack for
-    // the v_exp / v_log rounding, and the hardware reciprocals of a and c
-    rr->q2 = make_float4(col.z, 2.0f * 0.69314718f * __builtin_amdgcn_logf(255.0f * co.w) * 1.001f + 0.05f,
-                         __builtin_amdgcn_rcpf(co.x), __builtin_amdgcn_rcpf(co.z));
+    // t_o = -ln(255 o), rounded once from double: the render kernels' alpha threshold (alpha >= 1/255 <=> power >=
+    // t_o, gsd_render.hip record_og) and, with slack, the backward's ellipse culling (Q <= -2 t_o); the hardware
+    // reciprocals of a and c
+    rr->q2 = make_float4(col.z, (float)(-log(255.0 * (double)co.w)), __builtin_amdgcn_rcpf(co.x),
+                         __builtin_amdgcn_rcpf(co.z));
     rr->box = alpha_box(pix, co);
     // per-tile instance counts by global atomics -- only on the fallback path for very
     // large tile grids; normally k_tile_hist builds them from LDS histograms instead

@@ -86,14 +86,14 @@ __device__ __forceinline__ int wave_compact(const float4* __restrict__ s_box, co
             hit = bx.y >= qx0 && bx.x <= qx0 + (float)(RW - 1) && bx.w >= qy0 && bx.z <= qy0 + (float)(RH - 1);
             if (kExact && hit) {
                 const float4 pc = s_pc[t];
-                const float4 bo = s_bo[t];  // (b, o, alpha threshold with slack, 1 / a)
-                const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
+                const float4 bo = s_bo[t];  // (b, t_o, o, 1 / a)
+                const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.z);  // exact: (a, b, c, o)
                 const float det = co.x * co.z - co.y * co.y;
-                // alpha >= 1/255  <=>  Q <= 2 ln(255 o); the threshold carries 0.1 % + 0.05 of slack (v_exp /
-                // v_log rounding) and comes precomputed with the reciprocals (RenderRec.q2)
+                // alpha >= 1/255  <=>  Q <= 2 ln(255 o) = -2 t_o, with 0.1 % + 0.05 of slack (the exact decision
+                // is power >= t_o, record_alpha); the reciprocals come precomputed (RenderRec.q2)
                 if (co.x > 0.f && co.z > 0.f && det > 0.f)
-                    hit = ellipse_meets_rect(make_float2(pc.x, pc.y), co, bo.z, bo.w, s_rgb[t].w, qx0,
-                                             qx0 + (float)(RW - 1), qy0, qy0 + (float)(RH - 1));
+                    hit = ellipse_meets_rect(make_float2(pc.x, pc.y), co, fmaf(-2.002f, bo.y, 0.05f), bo.w,
+                                             s_rgb[t].w, qx0, qx0 + (float)(RW - 1), qy0, qy0 + (float)(RH - 1));
             }
         }
         const unsigned long long mask = wave_ballot(hit);
@@ -172,52 +172,38 @@ __device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s
     wave_lds_handoff();
 }
 
-// forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel (0 => skipped).
-// Shared by both passes so their skip decisions are identical.  power is evaluated exactly as the
-// reference writes it (no contraction), so alpha differs from the reference only through exp:
-// the hardware 2^x (v_exp_f32, 1 ulp) on power * log2(e), <= ~5 ulp over the range that matters
-// (power in [-12, 0]), against ~10 VALU ops for the libm-accurate expf.  Results stay inside the image /
-// n_contrib tolerances of DESIGN.md 4; GSD_PRECISE_EXP restores expf.  (Carrying log2(e) in the staged
-// conic and contracting power to FMAs saves 4 ops but moves alpha across the 1/255 threshold for some
-// pixels: image errors of 2e-3 at 400x400.)
-__device__ __forceinline__ float gauss_exp(float power) {
-#ifdef GSD_PRECISE_EXP
-    return expf(power);
-#else
-    return __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
-#endif
-}
-// The threshold decision alpha >= 1/255 (forward.cu:345, backward.cu:501) taken on the fast exp is final only
-// outside a narrow band around the threshold: the fast G is within ~4.5e-7 (relative) of exp(power), so where o G
-// lies within 2^-18 (3.8e-6) of 1/255 both passes recompute G with the libm-accurate expf (<= 1 ulp) and decide on
-// that.  The band is rare (a few pairs per million) and its lanes are wave-divergent, so it costs one compare per
-// pair and a scalar branch; the decisions then differ from the reference's only where its own alpha lies within
-// the two expf implementations' ulp of 1/255.
-constexpr float kAlphaThr = 1.0f / 255.0f;
-constexpr float kAlphaLo = kAlphaThr * (1.0f - 3.814697265625e-06f);
-constexpr float kAlphaHi = kAlphaThr * (1.0f + 3.814697265625e-06f);
-// o G with the accurate exp (the band's recomputation); pc / bo staged as below
-__device__ __forceinline__ float record_og_precise(float4 pc, float2 bo, float pxf, float pyf) {
-    const float dx = pc.x - pxf;
-    const float dy = pc.y - pyf;
-    const float power = (pc.z * dx * dx + pc.w * dy * dy) - bo.x * dx * dy;
-    return bo.y * expf(power);
-}
-// The render kernels stage a record as pc = (mx, my, -a/2, -c/2) and bo = (b, o): with the halves folded into
+// forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel, shared by both passes so their
+// decisions are identical.  power is evaluated exactly as the reference writes it (no contraction), so it has the
+// reference's bits.  The threshold decision alpha = min(0.99, o exp(power)) >= 1/255 is taken as power >= t_o, with
+// t_o = -ln(255 o) rounded once from double by the preprocess (RenderRec.q2.y): the exact boundary, up to t_o's
+// half ulp (~2 ulp of alpha) -- where the reference's own rounded o * expf(power) decides the same way except
+// within its ulps of 1/255 (the borderline pixels of the parity tests).  A hardware exp (v_exp_f32, a few ulp)
+// deciding on o G itself had flipped decisions outside that band.  With ln o = -t_o - ln 255 the unclamped alpha
+// o G = exp(power - t_o) / 255 is one v_exp_f32 of an FMA: the value is off the reference's by a few ulp (image /
+// gradient tolerances), the decisions are not.
+constexpr float kLog2e = 1.44269504088896341f;
+constexpr float kLog2_255 = 7.99435343685885793f;
+// The render kernels stage a record as pc = (mx, my, -a/2, -c/2) and bo = (b, t_o): with the halves folded into
 // the staged conic, (-a/2 dx) dx + (-c/2 dy) dy is exactly -0.5f * (a dx dx + c dy dy) (scaling by a power of
 // two commutes with rounding), so power below has the reference's bits with one multiply fewer per pair.
 __device__ __forceinline__ float4 stage_pc(float2 xy, float4 co) {
     return make_float4(xy.x, xy.y, -0.5f * co.x, -0.5f * co.z);
 }
-// Returns min(0.99, o G); the record is skipped where power > 0 (`keep` false) or alpha < 1/255 -- the
-// callers fold both tests into their take / valid masks (NaN power passes, as in the reference).
-__device__ __forceinline__ float record_alpha(float4 pc, float2 bo, float pxf, float pyf, float& G, bool& keep) {
+// Returns o G = exp(power - t_o) / 255 (alpha before the 0.99 clamp); `keep` is false where power > 0 (skipped)
+// and `over` false where power < t_o (alpha < 1/255) -- the callers fold both into their take / valid masks; a NaN
+// power passes both, as in the reference (alpha = fminf(0.99, NaN) = 0.99).
+__device__ __forceinline__ float record_og(float4 pc, float2 bt, float pxf, float pyf, bool& keep, bool& over) {
     const float dx = pc.x - pxf;
     const float dy = pc.y - pyf;
-    const float power = (pc.z * dx * dx + pc.w * dy * dy) - bo.x * dx * dy;
-    G = gauss_exp(power);
+    const float power = (pc.z * dx * dx + pc.w * dy * dy) - bt.x * dx * dy;
+    const float d = power - bt.y;  // its sign is exact: a float difference is 0 only for equal operands
     keep = !(power > 0.0f);
-    return fminf(0.99f, bo.y * G);
+    over = !(d < 0.0f);
+#ifdef GSD_PRECISE_EXP
+    return expf(d) * (1.0f / 255.0f);
+#else
+    return __builtin_amdgcn_exp2f(fmaf(d, kLog2e, -kLog2_255));
+#endif
 }
 
 // 1/d from v_rcp_f32 (1 ulp) plus one Newton step: ~0.5 ulp in 3 VALU ops instead of the ~10 of the
@@ -293,7 +279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             const RenderRec* r = p.rec + p.point_list[k];  // one 64-B record per gathered instance
             const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
             s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
-            s_bo[tid] = make_float2(q0.w, q1.y);
+            s_bo[tid] = make_float2(q0.w, q2.y);  // b, t_o
             s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, 0.f);
             s_box[tid] = r->box;
         } else {  // slots past the tile's list: finite zeros (the walk below reads list bytes past a group's end)
@@ -315,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             if (done_m == ~0ull) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
             float a[kBatch];
-            bool keep[kBatch];
+            bool keep[kBatch], over[kBatch];
             int slot[kBatch];
             static_assert(kBatch == 4, "one LDS word of list entries per batch");
             const uint32_t w4 = *reinterpret_cast<const uint32_t*>(list + j0);
@@ -334,8 +320,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 in_m[u] = wave_ballot(j0 + u < mine);
 #endif
                 slot[u] = (int)((w4 >> (8 * u)) & 0xffu);
-                float G;
-                a[u] = record_alpha(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, G, keep[u]);
+                a[u] = fminf(0.99f, record_og(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u]));
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
             // One wave-uniform branch per record (skipped when no lane takes it), the lane decisions as selects:
@@ -344,13 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 if (j0 + u >= m) break;
-                unsigned long long take_m = ~done_m & in_m[u] & wave_ballot(keep[u]) & wave_ballot(a[u] >= kAlphaLo);
-                const unsigned long long near_m = take_m & wave_ballot(a[u] < kAlphaHi);
-                if (near_m) {  // rare: o G within the fast exp's error band of 1/255 -- decide on the accurate exp
-                    const bool near = __builtin_amdgcn_inverse_ballot_w64(near_m);
-                    if (near) a[u] = fminf(0.99f, record_og_precise(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf));
-                    take_m &= ~(near_m & wave_ballot(!(a[u] >= kAlphaThr)));
-                }
+                unsigned long long take_m = ~done_m & in_m[u] & wave_ballot(keep[u]) & wave_ballot(over[u]);
                 if (!take_m) continue;
                 const float alpha = a[u];
                 const float test_T = T * (1 - alpha);
@@ -467,7 +446,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
             s_id[tid] = g;
             s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
-            s_bo[tid] = make_float4(q0.w, q1.y, q2.y, q2.z);   // b, o, ellipse threshold, 1 / a
+            s_bo[tid] = make_float4(q0.w, q2.y, q1.y, q2.z);   // b, t_o, o, 1 / a
             s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q2.w);  // r, g, b, 1 / c
             s_box[tid] = r->box;
         }
@@ -514,20 +493,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                         const float4 pc = make_float4(row_bcast<U>(rpc.x), row_bcast<U>(rpc.y), row_bcast<U>(rpc.z),
                                                       row_bcast<U>(rpc.w));
                         const float2 bo = make_float2(row_bcast<U>(rbo.x), row_bcast<U>(rbo.y));
-                        float G;
-                        bool keep;
-                        record_alpha(pc, bo, pxf, pyf, G, keep);
-                        float OG = bo.y * G;  // o G: alpha before the 0.99 clamp (the same product)
-                        // backward.cu:487-488 (list position below the pixel's last contributor); alpha =
-                        // min(0.99, o G) >= 1/255 <=> !(o G < 1/255), NaN included (fminf(0.99, NaN) = 0.99)
-                        unsigned long long valid_m = (U < nv ? ~0ull : 0ull) & wave_ballot(j0 + U >= first_valid) &
-                                                     wave_ballot(keep) & wave_ballot(!(OG < kAlphaLo));
-                        const unsigned long long near_m = valid_m & wave_ballot(OG < kAlphaHi);
-                        if (near_m) {  // rare: the forward's band recomputation, so both passes decide alike
-                            if (__builtin_amdgcn_inverse_ballot_w64(near_m))
-                                OG = record_og_precise(pc, bo, pxf, pyf);
-                            valid_m &= ~(near_m & wave_ballot(OG < kAlphaThr));
-                        }
+                        bool keep, over;
+                        const float OG = record_og(pc, bo, pxf, pyf, keep, over);  // alpha before the 0.99 clamp
+                        // backward.cu:487-488 (list position below the pixel's last contributor), :490-501
+                        const unsigned long long valid_m = (U < nv ? ~0ull : 0ull) &
+                                                           wave_ballot(j0 + U >= first_valid) & wave_ballot(keep) &
+                                                           wave_ballot(over);
                         any_m |= valid_m;
                         {
 #pragma clang fp contract(fast)
@@ -608,8 +579,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
             const float4 pc = s_pc[tid];
-            const float2 bo = *reinterpret_cast<const float2*>(&s_bo[tid]);
-            const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.y);  // exact: (a, b, c, o)
+            const float4 bo = s_bo[tid];
+            const float4 co = make_float4(-2.f * pc.z, bo.x, -2.f * pc.w, bo.z);  // exact: (a, b, c, o)
             const float o = co.w;  // the sums are over q = o G dL/dalpha; dL/dopacity = sum G dL/dalpha = S0 / o
             // phase 2 summed the first moments over x - mx, y - my: the reference's dx = mx - x flips them
             const float m0 = -s_acc[0][tid], m1 = -s_acc[1][tid];

@@ -208,6 +208,9 @@ class _MLPTrainF32(torch.autograd.Function):
                                                            _ptr(ws), _ptr(out), _stream(dev)))
         ctx.ws, ctx.wc, ctx.P = ws, wc, P
         ctx.shapes = [w.shape for w in wc] + [b.shape for b in bc]
+        # saved for autograd's version check: an in-place optimizer step between this forward and its backward
+        # (the activations in ws would then belong to other weights) raises instead of mixing them
+        ctx.save_for_backward(*params)
         return out
 
     @staticmethod
@@ -215,6 +218,10 @@ class _MLPTrainF32(torch.autograd.Function):
         from . import _native
         from ._C import _ptr, _stream
         lib = _native.load()
+        if ctx.ws is None:
+            raise RuntimeError("deform_mlp: backward through the f32 training path called a second time (its "
+                               "workspace is released by the first; retain_graph is not supported)")
+        ctx.saved_tensors   # noqa: B018 -- raises if a parameter was modified in place since the forward
         P, dev = ctx.P, ctx.ws.device
         g = gout.detach().to(torch.float32).contiguous()
         dx = torch.empty(P, 3, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
@@ -265,7 +272,12 @@ class DirectTemporalNeRF(nn.Module):
 
     def _use_train_f32(self, x: torch.Tensor) -> bool:
         """The f32 network on a HIP device (the reference's training precision) runs the hand-written training
-        path (gsd_mlp_train.hip: BF16x6 on the matrix cores, forward and backward); GSD_MLP_TORCH=1 keeps torch."""
+        path (gsd_mlp_train.hip: BF16x6 on the matrix cores, forward and backward) when a backward can follow --
+        its forward stores every hidden layer for that backward (~10.6 KB per Gaussian), which an evaluation
+        (no_grad, or nothing requiring grad) would allocate for nothing, so that runs on torch's f32 GEMMs.
+        GSD_MLP_TORCH=1 keeps torch."""
+        if not (torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
+            return False
         return (self.compute_dtype == torch.float32 and x.device.type == "cuda" and self._reference_arch()
                 and not os.environ.get("GSD_MLP_TORCH") and all(p.dtype == torch.float32 for p in self.parameters()))
 

@@ -322,9 +322,8 @@ class FusedAdam(torch.optim.Optimizer):
             p.data = view
             off += n
         self.param_slab, self.exp_avg, self.exp_avg_sq = param_slab, exp_avg, exp_avg_sq
-        self.flat.remove_hooks()
-        self.flat = FlatGrads(ps, device=dev)
-        self.flat.invalidate()   # the reference's surgery makes new nn.Parameters: no gradient yet
+        # the reference's surgery makes new nn.Parameters: no gradient yet; one layout exchange per step per rank
+        self.flat = self.flat.successor(ps, device=dev)
         self._layout()   # per-parameter step counts carry over (the reference keeps stored_state['step'])
 
     def reset_state(self):

@@ -145,6 +145,7 @@ class FlatGrads:
         self._view_of = {id(p): v for p, v in zip(self.params, self.views)}
         self.hooks = [p.register_hook(self._before_accumulate(p)) for p in self.params if p.requires_grad]
         self._sig_pending = None
+        self._verified = False   # this step's layout check is done (reset at the step boundary)
         self.attach()
 
     # ---- the layout check of the data-parallel path ----
@@ -160,9 +161,10 @@ class FlatGrads:
 
     def post_layout_check(self):
         """Start this step's layout check: an asynchronous host-side all-gather of layout_signature() on the gloo
-        signature group (its latency overlaps the forward).  Posted at most once between verifications, at the
-        start of a step (invalidate / zero)."""
-        if self._sig_pending is not None or not dp_active():
+        signature group, its latency overlapping the forward.  The rasterizer's forward posts it for the FlatGrads
+        of its inputs (gsd_amd.rasterizer), i.e. after any densification between steps, so the signature is the
+        layout the step's collectives will use; at most one post per step."""
+        if self._sig_pending is not None or self._verified or not dp_active():
             return
         sig = torch.tensor(self.layout_signature(), dtype=torch.int64)
         outs = [torch.empty_like(sig) for _ in range(dist.get_world_size())]
@@ -172,16 +174,36 @@ class FlatGrads:
     def verify_layout(self):
         """Before the first collective of a step: every rank's signature must equal this rank's -- otherwise every
         rank raises here (each sees all signatures) instead of entering collectives of different sizes, which
-        would hang or sum unrelated memory."""
-        if self._sig_pending is None:
+        would hang or sum unrelated memory.  Without a posted check (no forward went through the rasterizer) the
+        exchange is made here, synchronously.  Every rank makes exactly one exchange per step, so a rank that
+        rebuilt its slab (a densification on that rank only) cannot leave the signature group's collectives
+        paired across different steps."""
+        if self._verified or not dp_active():
             return
+        if self._sig_pending is None:
+            self.post_layout_check()
         sig, outs, work = self._sig_pending
         self._sig_pending = None
+        self._verified = True
         work.wait()
         if any(not torch.equal(o, sig) for o in outs):
             raise RuntimeError("FlatGrads: the data-parallel ranks' gradient slabs differ (per rank [numel, "
                                f"params, shapes hash, bucket floats, SH views]: {[o.tolist() for o in outs]}); "
                                "every rank must hold the same Gaussians (densify on every rank) and settings")
+        if sig.tolist() != self.layout_signature():
+            raise RuntimeError("FlatGrads: this rank's gradient slab changed between the forward's layout check and "
+                               "the step's collectives")
+
+    def successor(self, params, device=None):
+        """The slab replacing this one after a layout change (FusedAdam.rebuild: densification): this one's hooks
+        removed, the new one stale (no gradient yet) and holding this step's layout-check state, so the rank still
+        makes exactly one exchange per step -- a check posted before the change then fails on this rank."""
+        self.remove_hooks()
+        new = FlatGrads(params, device=device)
+        new.invalidate()
+        new._sig_pending, self._sig_pending = self._sig_pending, None
+        new._verified = self._verified
+        return new
 
     def _fused_guard(self, ids):
         if self.fused.intersection(ids) or self.early_ids.intersection(ids):
@@ -217,7 +239,7 @@ class FlatGrads:
         self.reduced = set()
         self.addends = {}
         self.attach()
-        self.post_layout_check()
+        self._verified = False   # a new step: its layout check is still to come
 
     def invalidate(self):
         """Mark every view stale (no memory traffic): the next gradient producer stores instead of adding."""
@@ -226,7 +248,7 @@ class FlatGrads:
         self.reduced = set()
         self.addends = {}
         self._version = self.slab._version
-        self.post_layout_check()
+        self._verified = False   # a new step: its layout check is still to come
 
     def add_after_reduce(self, p, t):
         """A term of ``p``'s gradient that is already the sum over every rank (gsd_sh_grad_views_ex's view-direction

@@ -24,8 +24,21 @@ def cpu_deep_copy_tuple(input_tuple):
     return tuple(copied)
 
 
+def _post_layout_checks(*tensors):
+    """Post the data-parallel layout check (parallel.FlatGrads.post_layout_check) of every gradient slab among a
+    forward's inputs: the check then describes the layout this step's collectives will use and its host-side
+    exchange overlaps the forward.  No-op without a data-parallel group."""
+    seen = set()
+    for t in tensors:
+        f = getattr(t, "_gsd_flat", None)
+        if f is not None and id(f) not in seen:
+            seen.add(id(f))
+            f.post_layout_check()
+
+
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings):
+    _post_layout_checks(means3D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                                      cov3Ds_precomp, raster_settings)
 
@@ -95,6 +108,7 @@ def rasterize_gaussians_split_sh(means3D, means2D, f_dc, f_rest, sh_offset, opac
     deformation).  Then, with more than one rank, the backward exchanges each view's masked dL/dRGB (12 B per
     Gaussian, one all_gather) and every rank sums the SH gradient of all views itself (gsd_sh_grad_views)
     instead of all-reducing the 192-B SH gradient (parallel.FlatGrads leaves it out of its all-reduce)."""
+    _post_layout_checks(means3D, f_dc, f_rest, sh_offset, opacities, scales, rotations)
     return _RasterizeSplitSH.apply(means3D, means2D, f_dc, f_rest, sh_offset, opacities, scales, rotations,
                                    raster_settings, sh_views)
 
@@ -129,6 +143,7 @@ def rasterize_gaussians_raw(xyz, means2D, f_dc, f_rest, scaling, rotation, opaci
     _scaling, _rotation, _opacity) go straight to the rasterizer, which applies exp / normalize / sigmoid itself
     (gsd_activation) and whose backward writes their gradients -- into ``.grad`` for FlatGrads parameters.
     Replaces the preamble kernels of gsd_amd.activate (gaussian_renderer/__init__.py:79-140). -> (color, radii)"""
+    _post_layout_checks(xyz, f_dc, f_rest, scaling, rotation, opacity)
     return _RasterizeRaw.apply(xyz, means2D, f_dc, f_rest, scaling, rotation, opacity, raster_settings, sh_views)
 
 

@@ -29,9 +29,8 @@ def main():
     def step():
         if a.bwd:
             sum(o.sum() for o in net(xg, t, 10_000)).backward()
-        else:
-            with torch.no_grad():
-                net(x, t, 10_000)
+        else:   # the training forward (a backward may follow: the HIP path stores the hidden layers)
+            net(xg, t, 10_000)
 
     for _ in range(3):
         step()

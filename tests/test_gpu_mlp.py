@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import pytest
 import torch
 
@@ -250,3 +251,73 @@ def test_train_f32_matches_float64_oracle_like_torch_f32(P, scale):
     for name, h, tt, r in zip(names, [hip[0]] + hip[1], [tor[0]] + tor[1], [ref_out] + ref_grads):
         e_hip, e_torch = err(h, r), err(tt, r)
         assert e_hip <= max(2e-5, 2.0 * e_torch), (name, e_hip, e_torch)
+
+
+def test_train_f32_matches_reference_network_fixture():
+    """The HIP f32 training path against the reference's own DirectTemporalNeRF run (tests/golden/mlp.npz:
+    gaussian_model.py:242-316 with a seeded init, float32 forward + autograd on the CPU): the four heads, dL/dx and
+    every parameter gradient, each within 2e-5 of its tensor's scale (max |err| / max |value|); the iteration-2000
+    call returns exact zeros."""
+    from conftest import golden
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    g = golden("mlp.npz")
+    names = [str(n) for n in g["names"]]
+    net = DirectTemporalNeRF()
+    net.load_state_dict({n: torch.from_numpy(g["w:" + n]) for n in names})
+    net = net.cuda()
+    heads = ("dx", "dscale", "drot", "dshs")
+    x = torch.from_numpy(g["x"]).cuda()
+    t = torch.from_numpy(g["t"]).cuda()
+    w = [torch.from_numpy(g["upstream:" + k]).cuda() for k in heads]
+    out, grads = _train_run(net, x, t, w, False)
+    want_out = np.concatenate([g["out:" + k] for k in heads], -1)
+    assert np.abs(out.cpu().numpy() - want_out).max() <= 2e-5 * np.abs(want_out).max()
+    for n, gr in zip(["x"] + names, grads):
+        want = g["grad:" + n]
+        err = float(np.abs(gr.cpu().numpy() - want).max()) / max(float(np.abs(want).max()), 1e-30)
+        assert err <= 2e-5, (n, err)
+    zero = net(x, t, 2000)
+    assert all(float(z.abs().max()) == 0.0 and z.shape == g["zero2000:" + k].shape for z, k in zip(zero, heads))
+
+
+def test_train_f32_nan_and_autograd_contracts():
+    """(1) a NaN pre-activation propagates through the HIP path as through torch's F.relu (the ReLU is
+    NaN-preserving, the backward mask passes a NaN's gradient as threshold_backward does): NaN outputs and
+    gradients in the same places as the torch f32 path; (2) an in-place parameter update between the forward and
+    the backward raises autograd's version error; (3) a second backward raises a clear error; (4) without grad the
+    forward takes torch's path (no 10.6-KB-per-Gaussian workspace)."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    torch.manual_seed(5)
+    net = DirectTemporalNeRF().cuda()
+    with torch.no_grad():
+        net._time[3].weight[7, :] = float("nan")   # one hidden unit of layer 3 is NaN for every Gaussian
+    P = 300
+    x = (torch.rand(P, 3, device="cuda") * 2 - 1)
+    t = torch.full((P, 1), 0.4, device="cuda")
+    w = [torch.randn(P, n, device="cuda") for n in (3, 3, 4, 48)]
+    hip = _train_run(net, x, t, w, False)
+    from oracle import deform_mlp_ref   # float64, torch.relu: NaN-propagating forward, threshold_backward masks
+    sd = {k: v.detach().cpu().double().requires_grad_(True) for k, v in net.state_dict().items()}
+    x64 = x.cpu().double().requires_grad_(True)
+    ref = deform_mlp_ref.forward(sd, x64, t.cpu().double(), 5000)
+    sum((o * wi.cpu().double()).sum() for o, wi in zip(ref, w)).backward()
+    ref_out = torch.cat([r.detach() for r in ref], -1)
+    assert torch.equal(torch.isnan(hip[0]).cpu(), torch.isnan(ref_out)) and bool(torch.isnan(ref_out).any())
+    names = ["x"] + [k for k, _ in net.named_parameters()]
+    for n, a, b in zip(names, hip[1], [x64.grad] + [sd[k].grad for k, _ in net.named_parameters()]):
+        assert torch.equal(torch.isnan(a).cpu(), torch.isnan(b)), n
+    net2 = DirectTemporalNeRF().cuda()
+    xg = x.clone().requires_grad_(True)
+    outs = net2(xg, t, 5000)
+    with torch.no_grad():
+        net2._time[0].weight.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        sum(o.sum() for o in outs).backward()
+    outs = net2(xg, t, 5000)
+    loss = sum(o.sum() for o in outs)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="second time"):
+        loss.backward()
+    with torch.no_grad():
+        _, names = _launched(lambda: net2(x, t, 5000))
+    assert "deform_mlp_train_fwd" not in names

@@ -665,3 +665,64 @@ def test_densify_and_prune_carries_the_se3_twist():
     out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV))
     l1_ssim_loss(out["render"], torch.zeros_like(out["render"])).backward()
     assert pc._twist.grad.shape == (Pn, 6) and torch.isfinite(pc._twist.grad).all()
+
+
+def test_densify_and_prune_matches_reference_gaussian_model_fixture(monkeypatch):
+    """gsd_amd.densify + FusedAdam on the GPU against the reference's own GaussianModel + torch.optim.Adam run
+    (tests/golden/densify.npz, gaussian_model.py:1027-1257 and train.py:613-616): two Adam steps, three views of
+    statistics, densify_and_prune with the reference's split samples, reset_opacity and one more step -- the same
+    point count, and parameters / moments / statistics within the FusedAdam-vs-torch bars of
+    test_densify_and_prune_matches_reference."""
+    from test_oracle_golden import _densify_fixture_run
+    from conftest import golden
+    from gsd_amd import DeformableGaussians
+    from gsd_amd.densify import GaussianDensifier
+    from gsd_amd.optim import FusedAdam
+    from gsd_amd.scene import GaussianParams
+    names = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
+
+    class M:
+        pass
+
+    def make(init, lrs, pd):
+        m = M()
+        t = [torch.from_numpy(v).to(DEV) for v in init]
+        prm = GaussianParams(xyz=t[0], features_dc=t[1], features_rest=t[2], opacity=t[3], scaling=t[4],
+                             rotation=t[5])
+        m.pc = DeformableGaussians(prm, sh_degree=3)
+        ps = [m.pc._xyz, m.pc._features_dc, m.pc._features_rest, m.pc._opacity, m.pc._scaling, m.pc._rotation]
+        m.opt = FusedAdam([{"params": [p], "lr": lr, "name": n} for p, lr, n in zip(ps, lrs, names)], lr=0.0,
+                          eps=1e-15)
+        m.dens = GaussianDensifier(m.pc, m.opt, percent_dense=pd)
+        return m
+
+    def params(m):
+        return [m.pc._xyz, m.pc._features_dc, m.pc._features_rest, m.pc._opacity, m.pc._scaling, m.pc._rotation]
+
+    def step(m, gs):
+        for p, gr in zip(params(m), gs):
+            p.grad.copy_(torch.from_numpy(gr).to(DEV))
+        m.opt.step()
+
+    def stats(m, vg, radii):
+        holder = torch.zeros(vg.shape, device=DEV, requires_grad=True)
+        holder.grad = torch.from_numpy(vg).to(DEV)
+        m.dens.add_densification_stats(holder, torch.from_numpy(radii).to(DEV))
+
+    def densify(m, max_grad, min_op, extent, mss, samples):
+        monkeypatch.setattr(torch, "normal", lambda mean, std: torch.from_numpy(samples).to(mean.device, mean.dtype))
+        m.dens.densify_and_prune(max_grad, min_op, extent, mss)
+        monkeypatch.undo()
+
+    def snapshot(m):
+        out = {}
+        for n, p in zip(names, params(m)):
+            out[n] = p.detach().cpu().numpy()
+            mo, v = m.opt.moments(p)
+            out[n + ":exp_avg"], out[n + ":exp_avg_sq"] = mo.cpu().numpy(), v.cpu().numpy()
+        for n in ("xyz_gradient_accum", "xyz_gradient_accum_3vec", "denom", "max_radii2D"):
+            out["stat:" + n] = getattr(m.dens, n).cpu().numpy().reshape(-1, *getattr(m.dens, n).shape[1:])
+        return out
+
+    _densify_fixture_run(golden("densify.npz"), make, step, stats, densify, lambda m: m.dens.reset_opacity(),
+                         snapshot, dict(param=1e-5, m=1e-6, v=1e-9, stat=1e-6))

@@ -406,3 +406,183 @@ def test_rank_divergent_layouts_raise_on_every_rank(tmp_path):
     for r in range(world):
         got = (tmp_path / f"rank{r}.txt").read_text().splitlines()
         assert got == ["P: raised True", "bucket: raised True", "same: ok 800.0"], (r, got)
+
+
+def _worker_one_rank_rebuilds(rank, world, port, out_dir):
+    """a densification that runs on one rank only (FusedAdam.rebuild -> FlatGrads.successor) between
+    steps.  The next step's forward posts the layout check (rasterizer._post_layout_checks) with the new layout on
+    that rank and the old one elsewhere, so every rank raises at its first collective -- and because each rank
+    makes exactly one exchange per step, the signature group's collectives stay paired: a following step where
+    both ranks rebuilt alike passes.  The same without a forward post (verify_layout's synchronous exchange)."""
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd import parallel
+    from gsd_amd.parallel import FlatGrads, init_from_env
+    from gsd_amd.rasterizer import _post_layout_checks
+    r, _, w = init_from_env(backend="gloo")
+    parallel.BUCKET_FLOATS = 1 << 10
+    params = [torch.nn.Parameter(torch.zeros(100, 3)), torch.nn.Parameter(torch.zeros(100, 1))]
+    fg = FlatGrads(params, device="cpu")
+    msgs = []
+
+    def run(fg, forward_post, tag):
+        if forward_post:
+            _post_layout_checks(*fg.params)
+        for p in fg.params:
+            p.grad.fill_(1.0)
+        try:
+            for _, _, wk in fg.allreduce_buckets(parallel.BUCKET_FLOATS):
+                if wk is not None:
+                    wk.wait()
+            msgs.append(f"{tag}: ok {float(fg.slab.sum()):.1f}")
+        except RuntimeError as e:
+            msgs.append(f"{tag}: raised {'differ' in str(e)}")
+        fg.invalidate()            # the step's end (FusedAdam marks the slab stale)
+
+    for forward_post in (True, False):
+        run(fg, forward_post, f"same{int(forward_post)}")
+        if r == 1:                 # densify on rank 1 only: fewer Gaussians
+            params = [torch.nn.Parameter(torch.zeros(90, 3)), torch.nn.Parameter(torch.zeros(90, 1))]
+            fg = fg.successor(params, device="cpu")
+        run(fg, forward_post, f"diverged{int(forward_post)}")
+        if r == 0:                 # rank 0 catches up: the layouts agree again
+            params = [torch.nn.Parameter(torch.zeros(90, 3)), torch.nn.Parameter(torch.zeros(90, 1))]
+            fg = fg.successor(params, device="cpu")
+        run(fg, forward_post, f"agreed{int(forward_post)}")
+        params = [torch.nn.Parameter(torch.zeros(100, 3)), torch.nn.Parameter(torch.zeros(100, 1))]
+        fg = fg.successor(params, device="cpu")
+    with open(os.path.join(out_dir, f"rank{r}.txt"), "w") as fh:
+        fh.write("\n".join(msgs))
+    _teardown(rank, world, out_dir)
+
+
+def test_one_rank_densify_raises_on_every_rank_and_stays_paired(tmp_path):
+    world = 2
+    mp.spawn(_worker_one_rank_rebuilds, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = []
+    for fp in (1, 0):
+        want += [f"same{fp}: ok 800.0", f"diverged{fp}: raised True", f"agreed{fp}: ok 720.0"]
+    for r in range(world):
+        got = (tmp_path / f"rank{r}.txt").read_text().splitlines()
+        assert got == want, (r, got)
+
+
+def _view_grads_at(params, yaw):
+    """The oracle's per-view gradients at the current parameters (activated means / SH / opacity / scales /
+    rotations), plus this view's masked dL/dRGB row and camera centre -- what the rasterizer backward hands the
+    SH-view exchange (gsd_sh_split.d_rgb)."""
+    from gsd_amd.camera import synthetic_camera
+    from oracle import oracle
+    xyz, sh, op, sc, rot = (p.detach().numpy() for p in params)
+    cam = synthetic_camera(W, H, yaw_deg=yaw)
+    kw = dict(shs=sh, scales=sc, rotations=rot, viewmatrix=cam.world_view_transform.numpy(),
+              projmatrix=cam.full_proj_transform.numpy(), campos=cam.camera_center.numpy(), W=W, H=H,
+              tanfovx=float(np.tan(cam.FoVx * 0.5)), tanfovy=float(np.tan(cam.FoVy * 0.5)), sh_degree=DEG)
+    fwd = oracle.forward(xyz, op, **kw)
+    dpix = np.random.default_rng(int(yaw * 10) + 1).standard_normal((3, H, W)).astype(np.float32)
+    b = oracle.backward(fwd, dpix, xyz, **kw)
+    row = b["dL_dcolors"].reshape(P, 3) * (1 - fwd["clamped"].reshape(P, 3))
+    return b, row.astype(np.float32), cam.camera_center.numpy().astype(np.float32)
+
+
+def _assemble_sh(xyz, sh_shape, rows, campos):
+    """sum_v B(dir_v) (x) dL/dRGB_v (backward.cu:20-139 per view, summed) -- a float64 restatement of
+    gsd_sh_grad_views: the SH colour is linear in the coefficients, so autograd of it gives the basis."""
+    from oracle.torch_ref import sh_rgb
+    x = torch.from_numpy(xyz).double()
+    total = torch.zeros(sh_shape, dtype=torch.float64)
+    for row, c in zip(rows, campos):
+        d = x - torch.from_numpy(c).double()
+        sh = torch.zeros(sh_shape, dtype=torch.float64, requires_grad=True)
+        (sh_rgb(DEG, sh, d / d.norm(dim=1, keepdim=True)) * torch.from_numpy(row).double()).sum().backward()
+        total += sh.grad
+    return total.float()
+
+
+def _worker_eight(rank, world, port, out_dir, sh_views):
+    """SURVEY.md 8(e) at cfg4's shape: 8 ranks, one view each (yaw k * 2 deg), three data-parallel steps of the
+    bench's protocol -- the SH gradient assembled from the all-gathered per-view dL/dRGB rows (sh_views) or
+    all-reduced with the rest, the raw parameters' early all-reduce, the bucketed all-reduce of the remainder,
+    and an identical Adam step on every rank.  Saves the first step's assembled gradient slab and a checksum of
+    the parameters after the three steps."""
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from gsd_amd import parallel
+    from gsd_amd.parallel import FlatGrads, init_from_env, mark_reduced
+    from gsd_amd.rasterizer import _post_layout_checks
+    from oracle import oracle
+    oracle.set_threads(1)
+    r, _, w = init_from_env(backend="gloo")
+    parallel.SH_VIEWS = bool(sh_views)
+    d = scene_inputs(P, W, H, DEG, seed=5)
+    params = [torch.nn.Parameter(d[k].clone().contiguous()) for k in
+              ("means3D", "shs", "opacities", "scales", "rotations")]
+    fg = FlatGrads(params, device="cpu")
+    opt = torch.optim.Adam([{"params": [p], "lr": lr} for p, lr in zip(params, (1e-4, 2.5e-3, 5e-2, 5e-3, 1e-3))],
+                           eps=1e-15)
+    for it in range(3):
+        fg.invalidate()
+        b, row, campos = _view_grads_at(params, 2.0 * r)
+        grads = [b["dL_dmeans3D"], b["dL_dsh"], b["dL_dopacity"], b["dL_dscales"], b["dL_drotations"]]
+        _post_layout_checks(*params)                    # the forward's layout check
+        for i, (p, g) in enumerate(zip(params, grads)):
+            if i == 1 and sh_views:
+                continue
+            assert fg.claim([p]) is False               # store mode: the first producer of the step
+            p.grad.copy_(torch.from_numpy(g).reshape(p.shape))
+        if sh_views:   # the row exchange: every rank assembles the all-view SH gradient itself
+            fg.verify_layout()
+            mine = torch.from_numpy(np.concatenate([row.reshape(-1), campos]))
+            parts = [torch.empty_like(mine) for _ in range(w)]
+            dist.all_gather(parts, mine)
+            rows = [q[:3 * P].numpy().reshape(P, 3) for q in parts]
+            cams = [q[3 * P:].numpy() for q in parts]
+            assert fg.claim([params[1]]) is False
+            params[1].grad.copy_(_assemble_sh(params[0].detach().numpy(), tuple(params[1].shape), rows, cams))
+            mark_reduced([params[1]])
+        fg.early_allreduce([params[0], params[2]], bucket_floats=700)   # the raw parameters, inside the backward
+        for a, bb, work in fg.allreduce_buckets(bucket_floats=900):
+            if work is not None:
+                work.wait()
+        if it == 0:
+            np.save(os.path.join(out_dir, f"{sh_views}grad{r}.npy"), fg.slab.numpy().copy())
+        opt.step()
+    ck = np.concatenate([p.detach().numpy().reshape(-1) for p in params]).view(np.uint32).astype(np.uint64).sum()
+    with open(os.path.join(out_dir, f"{sh_views}ck{r}.txt"), "w") as fh:
+        fh.write(str(int(ck)))
+    _teardown(rank, world, out_dir)
+
+
+def _eight_rank(tmp_path, sh_views):
+    from oracle import oracle
+    oracle.build()
+    world = 8
+    mp.spawn(_worker_eight, args=(world, _free_port(), str(tmp_path), sh_views), nprocs=world, join=True)
+    d = scene_inputs(P, W, H, DEG, seed=5)
+    params = [d[k].clone().contiguous() for k in ("means3D", "shs", "opacities", "scales", "rotations")]
+    want = 0
+    for k in range(world):
+        b, _, _ = _view_grads_at(params, 2.0 * k)
+        want = want + np.concatenate([b[n].reshape(-1) for n in ("dL_dmeans3D", "dL_dsh", "dL_dopacity",
+                                                                 "dL_dscales", "dL_drotations")]).astype(np.float64)
+    got = [np.load(tmp_path / f"{sh_views}grad{r}.npy") for r in range(world)]
+    for r in range(world):   # every rank holds the sum of the eight single-view oracle gradients
+        np.testing.assert_allclose(got[r], want, rtol=1e-5, atol=1e-6 * np.abs(want).max())
+    cks = {(tmp_path / f"{sh_views}ck{r}.txt").read_text() for r in range(world)}
+    assert len(cks) == 1, cks   # replicas bit-identical after three steps
+
+
+def test_eight_rank_sh_view_exchange_matches_sum_of_views(tmp_path):
+    _eight_rank(tmp_path, 1)
+
+
+def test_eight_rank_plain_allreduce_matches_sum_of_views(tmp_path):
+    _eight_rank(tmp_path, 0)
