@@ -28,9 +28,22 @@
 // one set of global atomics per (Gaussian, tile) instance.
 #include <type_traits>
 
+#include "../../include/gsd_raster.h"
+
 #include "gsd_kernels.h"
 
 namespace gsd {
+
+#ifdef GSD_COUNT_WORK
+// gsd_work_counters (include/gsd_raster.h): fwd steps, fwd pairs, bwd steps, bwd pairs
+__device__ unsigned long long g_work[4];
+__device__ __forceinline__ void count_work(int i, unsigned long long steps, unsigned long long pairs) {
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_work[i], steps);
+        atomicAdd(&g_work[i + 1], pairs);
+    }
+}
+#endif
 
 
 // forward: records whose alphas are evaluated together (ILP across the exps); measured 2/3/4/6/8/16 ->
@@ -175,10 +188,11 @@ __device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel, shared by both passes so their
 // decisions are identical.  power is evaluated exactly as the reference writes it (no contraction), so it has the
 // reference's bits.  The threshold decision alpha = min(0.99, o exp(power)) >= 1/255 is taken as power >= t_o, with
-// t_o = -ln(255 o) rounded once from double by the preprocess (RenderRec.q2.y): the exact boundary, up to t_o's
-// half ulp (~2 ulp of alpha) -- where the reference's own rounded o * expf(power) decides the same way except
-// within its ulps of 1/255 (the borderline pixels of the parity tests).  A hardware exp (v_exp_f32, a few ulp)
-// deciding on o G itself had flipped decisions outside that band.  With ln o = -t_o - ln 255 the unclamped alpha
+// t_o = -ln(255 o) computed in double and rounded up to a float by the preprocess (RenderRec.q2.y): for a float
+// power that is the exact real comparison, so it differs from the reference's rounded o * expf(power) >= 1/255 only
+// where that product lies within its own rounding (~1 ulp) of 1/255 (the borderline pixels of the parity tests).
+// A hardware exp (v_exp_f32, a few ulp) deciding on o G itself flipped decisions outside that band; recomputing
+// such alphas with expf cost 5 % of both kernels.  With ln o = -t_o - ln 255 the unclamped alpha
 // o G = exp(power - t_o) / 255 is one v_exp_f32 of an FMA: the value is off the reference's by a few ulp (image /
 // gradient tolerances), the decisions are not.
 constexpr float kLog2e = 1.44269504088896341f;
@@ -270,6 +284,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     uint32_t last_contributor = 0;
     uint8_t* list = s_list[tg.wave][tg.lane / (64 / kFwdGroups)];
+#ifdef GSD_COUNT_WORK
+    unsigned long long n_steps = 0, n_pairs = 0;
+#endif
 
     for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
         // forward.cu:309-311: stop once every pixel of the tile is saturated
@@ -329,6 +346,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
             for (int u = 0; u < kBatch; ++u) {
                 if (j0 + u >= m) break;
+#ifdef GSD_COUNT_WORK
+                ++n_steps;
+#endif
                 unsigned long long take_m = ~done_m & in_m[u] & wave_ballot(keep[u]) & wave_ballot(over[u]);
                 if (!take_m) continue;
                 const float alpha = a[u];
@@ -336,6 +356,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 const unsigned long long fin_m = take_m & wave_ballot(test_T < 0.0001f);
                 done_m |= fin_m;
                 take_m &= ~fin_m;
+#ifdef GSD_COUNT_WORK
+                n_pairs += __popcll(take_m);
+#endif
                 const bool take = __builtin_amdgcn_inverse_ballot_w64(take_m);
                 const float4 c = s_rgb[slot[u]];
                 // C += c alpha T (forward.cu:356-357) as one FMA per channel on the weight alpha T, selected to 0
@@ -352,6 +375,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             }
         }
     }
+#ifdef GSD_COUNT_WORK
+    count_work(0, n_steps, n_pairs);
+#endif
     if (tg.inside) {
         const int pid = p.W * tg.py + tg.px;
         const int plane = p.H * p.W;
@@ -434,6 +460,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
     const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     uint8_t* list = s_list[tg.wave];
+#ifdef GSD_COUNT_WORK
+    unsigned long long n_steps = 0, n_pairs = 0;
+#endif
     // phase 2: the first pixel of the lane's half-row of four
     const float ph2_x0 = tg.qx0 + (float)(4 * ((lane >> 2) & 1)), ph2_y0 = tg.qy0 + (float)(lane >> 3);
 
@@ -500,6 +529,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
                                                            wave_ballot(j0 + U >= first_valid) & wave_ballot(keep) &
                                                            wave_ballot(over);
                         any_m |= valid_m;
+#ifdef GSD_COUNT_WORK
+                        n_steps += U < nv ? 1 : 0;
+                        n_pairs += __popcll(valid_m);
+#endif
                         {
 #pragma clang fp contract(fast)
                             const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
@@ -601,6 +634,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
             if (a != 0.f) atomicAdd(p.grad_rec + (size_t)s_id[r] * kGradRec + q, a);
         }
     }
+#ifdef GSD_COUNT_WORK
+    count_work(2, n_steps, n_pairs);
+#endif
 }
 
 void launch_render_fwd(const RenderParams& p, hipStream_t s) {
@@ -612,3 +648,19 @@ void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
 
 }  // namespace gsd
 
+extern "C" int gsd_work_counters(int32_t n, uint64_t* out, int32_t reset) {
+    if (n < 0 || (n > 0 && !out)) return GSD_ERR_ARG;
+    unsigned long long v[4] = {0, 0, 0, 0};
+#ifdef GSD_COUNT_WORK
+    if (hipDeviceSynchronize() != hipSuccess) return GSD_ERR_HIP;
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(gsd::g_work), sizeof(v)) != hipSuccess) return GSD_ERR_HIP;
+    if (reset) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gsd::g_work), z, sizeof(z)) != hipSuccess) return GSD_ERR_HIP;
+    }
+#else
+    (void)reset;
+#endif
+    for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+    return GSD_OK;
+}

@@ -395,6 +395,15 @@ int gsd_timing_enable(int32_t on);
 int gsd_timing_collect(int32_t max_kernels, char* names, double* total_ms, int64_t* launches);
 void gsd_timing_reset(void);
 
+/* Work counters of the compositing kernels (the roofline's useful-work figures; no reference counterpart).
+ * Counted only by a library built with -DGSD_COUNT_WORK -- otherwise the kernels carry no counting code and
+ * every counter reads 0:
+ *   [0] render_fwd (wave, record) steps    [1] render_fwd (pixel, record) pairs composited
+ *   [2] render_bwd (wave, record) steps    [3] render_bwd (pixel, record) pairs replayed
+ * Copies min(n, 4) counters into out after synchronising the device; zeroes them when reset != 0.
+ * Returns GSD_OK, or GSD_ERR_ARG for n < 0 or a NULL out with n > 0. */
+int gsd_work_counters(int32_t n, uint64_t* out, int32_t reset);
+
 #ifdef __cplusplus
 }
 #endif
