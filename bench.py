@@ -117,6 +117,31 @@ def pmc_traffic(kernel, workload):
     return None
 
 
+# FP32 vector peak (MI355X_MICROARCH.md: 157.3 TFLOP/s, v_pk_fma_f32) for the compositing kernels' useful-work figure
+FP32_VALU_PEAK_TFLOPS = 157.3
+# the reference's arithmetic per useful (pixel, Gaussian) pair, counted from its expressions: forward.cu:332-357 for a
+# composited pair (offset 2, power 9, alpha 3, test_T 2, colour 9) and backward.cu:490-555 for a replayed pair
+# (offset, power, G, alpha 14; T and alpha T 3; the three channels' accum_rec / dL/dalpha / dL/dcolor 27; dL/dalpha
+# scaling and the background term 5; dL/dG, G dx, G dy, dG/d delta 9; the nine gradient sums with their factors 20),
+# loop invariants (bg . dL/dpixel) excluded
+FLOP_PER_PAIR = {"render_fwd": 25, "render_bwd": 78}
+
+
+def work_counts(kernel, workload):
+    """The useful-work counts of ``kernel`` on ``workload`` from the newest committed count
+    (profiles/**/work_counts*.json, scripts/count_work.py with a -DGSD_COUNT_WORK build), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "work_counts*.json"), recursive=True))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("_workload") == workload and kernel in d:
+            return dict(d[kernel], source=os.path.relpath(f, ROOT))
+    return None
+
+
 def roofline(kernel, ms, nbytes, workload):
     """The dominant kernel against its binding roof.  HBM: algorithmic bytes / the live average launch time vs
     8 TB/s.  VALU issue (when a PMC pass of this workload counted the kernel's instructions): the counted wave64
@@ -145,6 +170,20 @@ def roofline(kernel, ms, nbytes, workload):
             roof["hbm"] = hbm
         else:
             roof["valu"] = valu
+    wc = work_counts(kernel, workload)
+    if wc and kernel in FLOP_PER_PAIR:
+        # SURVEY.md 8(d)'s secondary figure: useful (pixel, Gaussian) pairs x the reference's FLOPs per pair / the
+        # live launch time, against the FP32 vector peak; and the issue figure scaled by the fraction of lanes
+        # doing useful work (counted pairs / (64 x counted wave-steps))
+        fl = wc["pixel_record_pairs"] * FLOP_PER_PAIR[kernel]
+        ach = fl / (ms * 1e-3) / 1e12
+        pairs = {"pairs_per_launch": wc["pixel_record_pairs"], "flop_per_pair": FLOP_PER_PAIR[kernel],
+                 "achieved": round(ach, 3), "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(ach / FP32_VALU_PEAK_TFLOPS, 4), "wave_record_steps": wc["wave_record_steps"],
+                 "useful_lane_fraction": wc["useful_lane_fraction"], "source": wc["source"]}
+        if roof.get("valu"):
+            pairs["valu_issue_x_useful_lanes"] = round(roof["valu"]["frac"] * wc["useful_lane_fraction"], 4)
+        roof["pairs"] = pairs
     return roof
 
 
@@ -234,8 +273,13 @@ def cpu_baseline(cfg, seed, min_seconds=10.0, max_views=64):
         dt = time.perf_counter() - t0
         if dt >= min_seconds or n >= max_views:
             break
+    share = os.environ.get("OMP_NUM_THREADS")
     return {"value": n / dt, "unit": "views/s", "cores": threads, "kind": "port",
-            "host": {"model": model, "cpus_available": avail, "omp_threads": threads},
+            "host": {"model": model, "cpus_available": avail, "omp_threads": threads,
+                     "threads_why": (f"OMP_NUM_THREADS={share}: the CPU share of one GPU's process on this host (the "
+                                     "GPU box sets it; its affinity mask shows every CPU of the machine, shared by the "
+                                     "other GPUs' jobs) -- the baseline uses the cores a one-GPU job owns"
+                                     if share else "OpenMP's default: every CPU in the affinity mask")},
             "sample": f"{n} full views of the bench workload (P={P}, {W}x{H}, SH{D}) forward+backward with the "
                       f"OpenMP C oracle on {threads} threads ({model}): {dt:.1f} s"}
 
