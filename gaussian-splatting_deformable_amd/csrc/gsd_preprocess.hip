@@ -202,11 +202,13 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     RenderRec* rr = p.rec + idx;  // what the render kernels gather per instance (RenderRec)
     rr->q0 = make_float4(pix.x, pix.y, co.x, co.y);
     rr->q1 = make_float4(co.z, co.w, col.x, col.y);
-    // t_o = -ln(255 o) in double, rounded up to a float: for a float power, power >= t_o is then exactly the real
-    // comparison power >= -ln(255 o), i.e. o exp(power) >= 1/255 -- the render kernels' alpha threshold
+    // t_o = -ln(255 o) in double, rounded to the nearest float: for a float power, power >= t_o is the real
+    // comparison power >= -ln(255 o), i.e. o exp(power) >= 1/255, except where power equals t_o exactly (then
+    // alpha lies within half an ulp of t_o of the threshold) -- the render kernels' alpha threshold
     // (gsd_render.hip record_og) -- and, with slack, the backward's ellipse culling (Q <= -2 t_o); the hardware
-    // reciprocals of a and c
-    rr->q2 = make_float4(col.z, __double2float_ru(-log(255.0 * (double)co.w)), __builtin_amdgcn_rcpf(co.x),
+    // reciprocals of a and c.  (Rounded up, t_o made the comparison exact at ties too, but biased every alpha VALUE
+    // low by up to an ulp of t_o, which the transmittance accumulates: 10 instead of 1 n_contrib flips at cfg4.)
+    rr->q2 = make_float4(col.z, __double2float_rn(-log(255.0 * (double)co.w)), __builtin_amdgcn_rcpf(co.x),
                          __builtin_amdgcn_rcpf(co.z));
     rr->box = alpha_box(pix, co);
     // per-tile instance counts by global atomics -- only on the fallback path for very

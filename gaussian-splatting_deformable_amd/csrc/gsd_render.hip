@@ -188,9 +188,10 @@ __device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel, shared by both passes so their
 // decisions are identical.  power is evaluated exactly as the reference writes it (no contraction), so it has the
 // reference's bits.  The threshold decision alpha = min(0.99, o exp(power)) >= 1/255 is taken as power >= t_o, with
-// t_o = -ln(255 o) computed in double and rounded up to a float by the preprocess (RenderRec.q2.y): for a float
-// power that is the exact real comparison, so it differs from the reference's rounded o * expf(power) >= 1/255 only
-// where that product lies within its own rounding (~1 ulp) of 1/255 (the borderline pixels of the parity tests).
+// t_o = -ln(255 o) computed in double and rounded to a float by the preprocess (RenderRec.q2.y): for a float power
+// that is the real comparison (up to exact ties, where alpha is within half an ulp of t_o of 1/255), so it differs
+// from the reference's rounded o * expf(power) >= 1/255 only where that product lies within its own rounding of 1/255
+// (the borderline pixels of the parity tests).
 // A hardware exp (v_exp_f32, a few ulp) deciding on o G itself flipped decisions outside that band; recomputing
 // such alphas with expf cost 5 % of both kernels.  With ln o = -t_o - ln 255 the unclamped alpha
 // o G = exp(power - t_o) / 255 is one v_exp_f32 of an FMA: the value is off the reference's by a few ulp (image /
