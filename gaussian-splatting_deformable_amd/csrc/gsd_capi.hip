@@ -1026,10 +1026,40 @@ extern "C" {
 
 size_t gsd_deform_mlp_train_workspace_bytes(int64_t P) { return P > 0 ? carve_mlp(nullptr, P, nullptr) : kAlign; }
 
+static gsd::MlpHeads heads_of(float* out) {   // the (P, 58) layout of the heads as four views
+    gsd::MlpHeads h{};
+    for (int k = 0; k < 4; ++k) {
+        h.out[k] = out + gsd::kMlpHeadCol[k];
+        h.ld[k] = 58;
+    }
+    return h;
+}
+
+static int mlp_train_forward(int64_t P, const float* x, const float* t, const float* const* weights,
+                             const float* const* biases, void* workspace, const gsd::MlpHeads& heads, void* stream);
+
 int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, const float* const* weights,
                                  const float* const* biases, void* workspace, float* out, void* stream) {
+    if (!out) return fail(GSD_ERR_ARG, "null pointer argument");
+    return mlp_train_forward(P, x, t, weights, biases, workspace, heads_of(out), stream);
+}
+
+int gsd_deform_mlp_train_forward_heads(int64_t P, const float* x, const float* t, const float* const* weights,
+                                       const float* const* biases, void* workspace, float* const* heads, void* stream) {
+    if (!heads) return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::MlpHeads h{};
+    for (int k = 0; k < 4; ++k) {
+        if (!heads[k]) return fail(GSD_ERR_ARG, "deform_mlp_train: 4 head outputs needed");
+        h.out[k] = heads[k];
+        h.ld[k] = gsd::kMlpHeadCol[k + 1] - gsd::kMlpHeadCol[k];
+    }
+    return mlp_train_forward(P, x, t, weights, biases, workspace, h, stream);
+}
+
+static int mlp_train_forward(int64_t P, const float* x, const float* t, const float* const* weights,
+                             const float* const* biases, void* workspace, const gsd::MlpHeads& heads, void* stream) {
     if (P <= 0 || P >= (1ll << 31) - 256) return fail(GSD_ERR_ARG, "deform_mlp_train: need 0 < P < 2^31 - 256");
-    if (!x || !t || !weights || !biases || !workspace || !out) return fail(GSD_ERR_ARG, "null pointer argument");
+    if (!x || !t || !weights || !biases || !workspace) return fail(GSD_ERR_ARG, "null pointer argument");
     for (int i = 0; i < 12; ++i)
         if (!weights[i] || !biases[i]) return fail(GSD_ERR_ARG, "deform_mlp_train: 12 weights and 12 biases needed");
     MlpWs ws;
@@ -1059,7 +1089,7 @@ int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, cons
                 f.bits[l] = ws.bits[l + 1];
             }
             f.bias_heads = ws.bias_heads;
-            f.out = out;
+            f.heads = heads;
             gsd::launch_mlp_fwd_fused(f, s);
             return;
         }
@@ -1083,8 +1113,7 @@ int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, cons
                 gsd::launch_mlp_gemm(g, gsd::kMlpFwdRelu, s);
             } else {
                 g.bias = ws.bias_heads;
-                g.dst = out;
-                g.n_out = 58;
+                g.heads = heads;
                 gsd::launch_mlp_gemm(g, gsd::kMlpFwdHeads, s);
             }
         }
@@ -1093,10 +1122,38 @@ int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, cons
     return GSD_OK;
 }
 
+static int mlp_train_backward(int64_t P, const gsd::MlpHeadsIn& gin, const float* const* weights, void* workspace,
+                              float* dx, int dx_accumulate, float* const* d_weights, float* const* d_biases,
+                              int accumulate, void* stream);
+
 int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float* const* weights, void* workspace,
                                   float* dx, float* const* d_weights, float* const* d_biases, void* stream) {
+    if (!grad_out) return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::MlpHeadsIn g{};
+    for (int k = 0; k < 4; ++k) {
+        g.src[k] = grad_out + gsd::kMlpHeadCol[k];
+        g.ld[k] = 58;
+    }
+    return mlp_train_backward(P, g, weights, workspace, dx, 0, d_weights, d_biases, 0, stream);
+}
+
+int gsd_deform_mlp_train_backward_heads(int64_t P, const float* const* grad_heads, const float* const* weights,
+                                        void* workspace, float* dx, int32_t dx_accumulate, float* const* d_weights,
+                                        float* const* d_biases, int32_t accumulate, void* stream) {
+    if (!grad_heads) return fail(GSD_ERR_ARG, "null pointer argument");
+    gsd::MlpHeadsIn g{};
+    for (int k = 0; k < 4; ++k) {
+        g.src[k] = grad_heads[k];   // NULL: a zero gradient
+        g.ld[k] = gsd::kMlpHeadCol[k + 1] - gsd::kMlpHeadCol[k];
+    }
+    return mlp_train_backward(P, g, weights, workspace, dx, dx_accumulate, d_weights, d_biases, accumulate, stream);
+}
+
+static int mlp_train_backward(int64_t P, const gsd::MlpHeadsIn& gin, const float* const* weights, void* workspace,
+                              float* dx, int dx_accumulate, float* const* d_weights, float* const* d_biases,
+                              int accumulate, void* stream) {
     if (P <= 0 || P >= (1ll << 31) - 256) return fail(GSD_ERR_ARG, "deform_mlp_train: need 0 < P < 2^31 - 256");
-    if (!grad_out || !weights || !workspace || !d_weights || !d_biases) return fail(GSD_ERR_ARG, "null pointer argument");
+    if (!weights || !workspace || !d_weights || !d_biases) return fail(GSD_ERR_ARG, "null pointer argument");
     for (int i = 0; i < 12; ++i)
         if (!weights[i] || !d_weights[i] || !d_biases[i])
             return fail(GSD_ERR_ARG, "deform_mlp_train: 12 weights and 12 weight / bias gradients needed");
@@ -1107,10 +1164,10 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
     const int ldp = (int)ws.ldp;
     const int chunks = (int)((P + kMlpChunk - 1) / kMlpChunk);
     auto wgrad = [&](int l, const float* G, int n_rb, const float* X0, const float* X1, int k_rb, int k_rb0,
-                     int k_off = 0) {
+                     int k_off = 0, int skip_bias = 0) {
         gsd::MlpWgradParams q{};
         q.P = (int)P; q.ldp = ldp; q.G = G; q.n_rb = n_rb; q.X0 = X0; q.X1 = X1; q.k_rb = k_rb; q.k_rb0 = k_rb0;
-        q.k_off = k_off;
+        q.k_off = k_off; q.accumulate = accumulate; q.skip_bias = skip_bias;
         q.tiles_n = (n_rb + 3) / 4; q.tiles_k = (k_rb + 3) / 4; q.chunk = kMlpChunk;
         q.partial = ws.partial; q.bias_partial = ws.bias_partial;
         gsd::launch_mlp_wgrad(q, mlp_weight(l, d_weights), mlp_weight(l, d_biases, 1), s);
@@ -1126,7 +1183,7 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
     (void)chunks;
     timed(kMlpTrainBwd, s, [&] {
         mlp_pack_all(W, ws, true, false, s);
-        gsd::launch_mlp_rows_to_features((int)P, ldp, 58, grad_out, ws.Gh, 64, s);
+        gsd::launch_mlp_rows_to_features((int)P, ldp, gin, ws.Gh, 64, s);
         wgrad(8, ws.Gh, 2, ws.H[8], nullptr, 8, 8);
         dgemm(8, ws.Gh, 4, 8, ws.ga, 0, 0);   // g of layer 7's pre-activation
         float* g = ws.ga;
@@ -1135,7 +1192,7 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
             if (l == 0) wgrad(0, g, 8, ws.E, ws.ET, 3, 2);
             else if (l == 5) {   // columns 0-63 (enc(x)) and 64-319 (h5) as two calls (both bias gradients equal)
                 wgrad(5, g, 8, ws.E, nullptr, 2, 2, 0);
-                wgrad(5, g, 8, ws.H[5], nullptr, 8, 8, 64);
+                wgrad(5, g, 8, ws.H[5], nullptr, 8, 8, 64, 1);
             }
             else wgrad(l, g, 8, ws.H[l], nullptr, 8, 8);
             if (l == 5) dgemm(5, g, 16, 5, other, 64, 0);   // rows 0-63: d enc(x); the rest masked by h5
@@ -1145,7 +1202,7 @@ int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float*
             g = other;
             other = tmp;
         }
-        if (dx) gsd::launch_mlp_encode_bwd((int)P, ldp, ws.E, ws.dE, dx, 0, s);
+        if (dx) gsd::launch_mlp_encode_bwd((int)P, ldp, ws.E, ws.dE, dx, dx_accumulate, s);
     });
     GSD_CHECK(false, s);
     return GSD_OK;

@@ -326,6 +326,24 @@ struct MlpPackParams {
 // The layer-fused training forward (k_mlp_fwd_fused): the encoding in, every hidden layer's output, its ReLU words
 // and the heads out; the weights packed with the accumulator-order k permutation (perm_from 0; layer 5: 4; layer 0:
 // natural).
+// The four heads' outputs (dx 3, d log-scale 3, d quaternion 4, dSH 48: columns [0,3) [3,6) [6,10) [10,58) of the
+// 58-wide head layer), each a row-major (P, ld[k]) array: separate tensors (ld = width), or views into one (P, 58)
+// array (ld = 58, out[k] offset by the head's first column).  Inputs (the backward's incoming gradients) likewise,
+// NULL: a zero gradient.
+constexpr int kMlpHeadCol[5] = {0, 3, 6, 10, 58};
+struct MlpHeads {
+    float* out[4];
+    int ld[4];
+};
+struct MlpHeadsIn {
+    const float* src[4];
+    int ld[4];
+};
+__device__ __forceinline__ void mlp_store_head(const MlpHeads& o, long long g, int n, float v) {
+    const int k = n < 3 ? 0 : (n < 6 ? 1 : (n < 10 ? 2 : 3));
+    const int c0 = k == 0 ? 0 : (k == 1 ? 3 : (k == 2 ? 6 : 10));
+    o.out[k][g * o.ld[k] + (n - c0)] = v;
+}
 struct MlpFusedParams {
     int P, ldp;
     const float* E;          // [64][ldp]: enc(x), row 63 zero
@@ -335,7 +353,7 @@ struct MlpFusedParams {
     const float* bias_heads; // 64 (58 used)
     float* H[8];             // layer l's output: [256][ldp]
     unsigned short* bits[8]; // its ReLU words: [(rb * 2 + h) * ldp + g]
-    float* out;              // (P, 58) row-major
+    MlpHeads heads;          // the four heads' outputs
 };
 enum { kMlpFwdRelu = 0, kMlpFwdHeads = 1, kMlpBwdMask = 2 };
 struct MlpGemmParams {
@@ -348,8 +366,8 @@ struct MlpGemmParams {
     int rb;                         // output row blocks of 32 (of the packed A)
     int rb_off;                     // launch-internal: first row block of this workgroup row (grid.y)
     const float* bias;              // forward: 32 rb floats
-    float* dst;                     // forward hidden: [32 rb][ldp]; heads: (P, n_out) row-major; backward: g rows
-    int n_out;                      // heads: outputs written (58)
+    float* dst;                     // forward hidden: [32 rb][ldp]; backward: g rows
+    MlpHeads heads;                 // heads: the four outputs (58 columns)
     int n_a;                        // backward: rows below n_a go to dst_a (the encoding's gradient, no ReLU)
     float* dst_a;
     int accumulate_a;
@@ -372,6 +390,8 @@ struct MlpWgradParams {
     int chunk;                      // Gaussians per wave (multiple of 16)
     float* partial;                 // [chunks][32 n_rb][32 k_rb]
     float* bias_partial;            // [chunks][32 n_rb]
+    int accumulate;                 // the reduction adds into the destination pieces instead of storing
+    int skip_bias;                  // the bias gradient is another call's (layer 5's second column range)
 };
 void launch_mlp_pack(const MlpPackParams& p, hipStream_t s);
 void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E, float* ET, hipStream_t s);
@@ -380,7 +400,7 @@ void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s);
 void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s);
 // dW scattered into the reference-shaped weight pieces (dst.W; map/rows as the forward weight), db into dst_b
 void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s);
-void launch_mlp_rows_to_features(int P, int ldp, int n, const float* src, float* dst, int dst_rows, hipStream_t s);
+void launch_mlp_rows_to_features(int P, int ldp, const MlpHeadsIn& src, float* dst, int dst_rows, hipStream_t s);
 void launch_mlp_gather_bias(const MlpWeightRef& b, float* dst, int n_pad, hipStream_t s);
 
 constexpr int kAdamMaxGroups = 16;

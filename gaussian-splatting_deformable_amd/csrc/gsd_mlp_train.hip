@@ -108,20 +108,25 @@ __global__ void k_mlp_gather_bias(MlpWeightRef b, float* __restrict__ dst, int n
     dst[n] = e ? *e : 0.f;
 }
 
-// (P, n) row-major -> [dst_rows][ldp] feature-major (rows past n zero): the heads' incoming gradient.  A workgroup
-// takes 64 Gaussians: their n-float rows are one contiguous run, read coalesced into LDS, then written per feature.
-__global__ __launch_bounds__(256) void k_mlp_rows_to_features(int P, int ldp, int n, const float* __restrict__ src,
-                                                              float* __restrict__ dst, int dst_rows) {
+// The heads' incoming gradients -> [dst_rows][ldp] feature-major (rows past 58 zero).  A workgroup takes 64
+// Gaussians: each head's 64 rows are one contiguous run, read coalesced into LDS, then written per feature.
+__global__ __launch_bounds__(256) void k_mlp_rows_to_features(int P, int ldp, MlpHeadsIn src, float* __restrict__ dst,
+                                                              int dst_rows) {
     __shared__ float tile[64][65];
     const int g0 = blockIdx.x * 64;
-    const int cnt = min(64, P - g0) * n;   // floats of the run (<= 0 past P)
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int gg = i / 64, r = i % 64;
-        tile[gg][r] = 0.f;
-        (void)r;
-    }
+    const int ng = min(64, P - g0);   // Gaussians of this block (<= 0 past P)
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) tile[i / 64][i % 64] = 0.f;
     __syncthreads();
-    for (int i = threadIdx.x; i < cnt; i += 256) tile[i / n][i % n] = src[(size_t)g0 * n + i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float* sp = src.src[k];
+        const int w = kMlpHeadCol[k + 1] - kMlpHeadCol[k], ld = src.ld[k];
+        if (!sp || ng <= 0) continue;
+        for (int i = threadIdx.x; i < ng * w; i += 256) {
+            const int gg = i / w, col = i - gg * w;
+            tile[gg][kMlpHeadCol[k] + col] = sp[(size_t)(g0 + gg) * ld + col];
+        }
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * dst_rows; i += 256) {
         const int r = i / 64, gg = i % 64;
@@ -192,7 +197,7 @@ __device__ __forceinline__ void gemm_epilogue(const MlpGemmParams& p, const f32x
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         const int nb = 32 * (rb0 + r);   // the block's first row
-        if (MODE == kMlpFwdHeads) {      // (P, n_out) row-major per Gaussian: 58 floats, written as is
+        if (MODE == kMlpFwdHeads) {      // the four heads' outputs per Gaussian: 58 floats, written as is
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float4 b4 = *reinterpret_cast<const float4*>(p.bias + nb + 8 * j + 4 * h);
@@ -200,7 +205,7 @@ __device__ __forceinline__ void gemm_epilogue(const MlpGemmParams& p, const f32x
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int n = nb + 8 * j + 4 * h + i;
-                    if (n < p.n_out && g < p.P) p.dst[(size_t)g * p.n_out + n] = acc[r][4 * j + i] + bq[i];
+                    if (n < 58 && g < p.P) mlp_store_head(p.heads, g, n, acc[r][4 * j + i] + bq[i]);
                 }
             }
             continue;
@@ -651,7 +656,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int n = 32 * r + 8 * q4 + 4 * h + i;
-                    if (n < 58) p.out[(size_t)g * 58 + n] = ho[r][4 * q4 + i] + bq[i];
+                    if (n < 58) mlp_store_head(p.heads, g, n, ho[r][4 * q4 + i] + bq[i]);
                 }
             }
     }
@@ -829,7 +834,8 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
 // owns 32 consecutive outputs; its 8 thread groups sum the chunks c = g, g + 8, ... (loads four chunks ahead) and
 // the 8 group sums are combined in group order through LDS.
 __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_rows, int k_cols, int k_off,
-                                                          const float* __restrict__ partial, MlpWeightRef dst) {
+                                                          const float* __restrict__ partial, MlpWeightRef dst,
+                                                          int accumulate) {
     __shared__ float red[8][32];
     const long long n_el = (long long)n_rows * k_cols;
     const int grp = threadIdx.x >> 5, l = threadIdx.x & 31;
@@ -852,7 +858,7 @@ __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_ro
         for (int g = 1; g < 8; ++g) t += red[g][l];
         const int n = (int)(e / k_cols), k = (int)(e - (long long)n * k_cols);
         float* d = mlp_elem(dst, n, mlp_col(dst.map, k_off + k));
-        if (d) *d = t;
+        if (d) *d = accumulate ? *d + t : t;
     }
 }
 
@@ -906,13 +912,14 @@ void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const Ml
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
     hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 31) / 32)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
-                       32 * p.k_rb, p.k_off, (const float*)p.partial, dst);
-    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 31) / 32), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1, 0,
-                       (const float*)p.bias_partial, dst_b);
+                       32 * p.k_rb, p.k_off, (const float*)p.partial, dst, p.accumulate);
+    if (!p.skip_bias)
+        hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 31) / 32), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1,
+                           0, (const float*)p.bias_partial, dst_b, p.accumulate);
 }
 
-void launch_mlp_rows_to_features(int P, int ldp, int n, const float* src, float* dst, int dst_rows, hipStream_t s) {
-    hipLaunchKernelGGL(k_mlp_rows_to_features, dim3(ldp / 64), dim3(256), 0, s, P, ldp, n, src, dst, dst_rows);
+void launch_mlp_rows_to_features(int P, int ldp, const MlpHeadsIn& src, float* dst, int dst_rows, hipStream_t s) {
+    hipLaunchKernelGGL(k_mlp_rows_to_features, dim3(ldp / 64), dim3(256), 0, s, P, ldp, src, dst, dst_rows);
 }
 
 void launch_mlp_gather_bias(const MlpWeightRef& b, float* dst, int n_pad, hipStream_t s) {

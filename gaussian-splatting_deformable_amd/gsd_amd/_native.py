@@ -11,7 +11,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -107,6 +107,11 @@ SIGNATURES = {
     "gsd_deform_mlp_train_forward": (_i32, [_i64, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp, _vp]),
     "gsd_deform_mlp_train_backward": (_i32, [_i64, _vp, ctypes.POINTER(_vp), _vp, _vp, ctypes.POINTER(_vp),
                                              ctypes.POINTER(_vp), _vp]),
+    "gsd_deform_mlp_train_forward_heads": (_i32, [_i64, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp,
+                                                  ctypes.POINTER(_vp), _vp]),
+    "gsd_deform_mlp_train_backward_heads": (_i32, [_i64, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp, _i32,
+                                                   ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i32, _vp]),
+    "gsd_work_counters": (_i32, [_i32, ctypes.POINTER(ctypes.c_uint64), _i32]),
     "gsd_timing_enable": (_i32, [_i32]),
     "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),
     "gsd_timing_reset": (None, []),

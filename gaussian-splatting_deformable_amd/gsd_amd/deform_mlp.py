@@ -182,10 +182,17 @@ def _ptr_array(ts):
     return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
 
 
+_HEADS = (3, 3, 4, 48)   # dx, d log-scale, d quaternion, dSH
+
+
 class _MLPTrainF32(torch.autograd.Function):
     """DirectTemporalNeRF forward + backward as the reference trains it (float32 with autograd), each GEMM on the
     bf16 matrix cores with the operands split into three bf16 terms (BF16x6, f32-level accuracy): three HIP
-    kernels per layer direction instead of torch's GEMMs, every activation kept feature-major in one workspace."""
+    kernels per layer direction instead of torch's GEMMs, every activation kept feature-major in one workspace.
+    The four heads come out as separate tensors (no (P, 58) array to split and copy, and autograd concatenates no
+    gradients for the backward, which reads the four gradients -- a missing one as zero -- in place).  Parameters
+    (and x) whose .grad is a FlatGrads view get their gradients written there by the backward (stored when the view
+    is stale, added otherwise: autograd's accumulation without a zero-fill and an add kernel per parameter)."""
 
     @staticmethod
     def forward(ctx, x, t, *params):
@@ -202,43 +209,63 @@ class _MLPTrainF32(torch.autograd.Function):
         xc = x.detach().to(torch.float32).contiguous()
         tc = t.detach().to(torch.float32).reshape(-1).expand(P).contiguous()
         ws = torch.empty(lib.gsd_deform_mlp_train_workspace_bytes(P), dtype=torch.uint8, device=dev)
-        out = torch.empty(P, 58, dtype=torch.float32, device=dev)
+        heads = [torch.empty(P, n, dtype=torch.float32, device=dev) for n in _HEADS]
         with torch.cuda.device(dev):
-            _native.check(lib.gsd_deform_mlp_train_forward(P, _ptr(xc), _ptr(tc), _ptr_array(wc), _ptr_array(bc),
-                                                           _ptr(ws), _ptr(out), _stream(dev)))
+            _native.check(lib.gsd_deform_mlp_train_forward_heads(P, _ptr(xc), _ptr(tc), _ptr_array(wc),
+                                                                 _ptr_array(bc), _ptr(ws), _ptr_array(heads),
+                                                                 _stream(dev)))
         ctx.ws, ctx.wc, ctx.P = ws, wc, P
         ctx.shapes = [w.shape for w in wc] + [b.shape for b in bc]
+        ctx.x, ctx.params = x, params
+        ctx.set_materialize_grads(False)
         # saved for autograd's version check: an in-place optimizer step between this forward and its backward
         # (the activations in ws would then belong to other weights) raises instead of mixing them
         ctx.save_for_backward(*params)
-        return out
+        return tuple(heads)
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, *g_heads):
         from . import _native
         from ._C import _ptr, _stream
+        from .activate import _sinks
         lib = _native.load()
         if ctx.ws is None:
             raise RuntimeError("deform_mlp: backward through the f32 training path called a second time (its "
                                "workspace is released by the first; retain_graph is not supported)")
         ctx.saved_tensors   # noqa: B018 -- raises if a parameter was modified in place since the forward
         P, dev = ctx.P, ctx.ws.device
-        g = gout.detach().to(torch.float32).contiguous()
-        dx = torch.empty(P, 3, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
-        dW = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in ctx.shapes[:12]]
-        db = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in ctx.shapes[12:]]
+        gh = [None if g is None else g.detach().to(torch.float32).contiguous() for g in g_heads]
+        if all(g is None for g in gh):
+            ctx.ws = None
+            return (None,) * (2 + len(ctx.params))
+        # FlatGrads sinks for the parameters (all or none) and for x
+        sinks, acc = _sinks(list(ctx.params)) if all(p.requires_grad for p in ctx.params) else (None, True)
+        xs, xacc = (_sinks([ctx.x]) if ctx.needs_input_grad[0] else (None, True))
+        if sinks is not None:
+            dW, db = sinks[:12], sinks[12:]
+        else:
+            dW = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in ctx.shapes[:12]]
+            db = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in ctx.shapes[12:]]
+            acc = False
+        if xs is not None:
+            dx = xs[0]
+        else:
+            dx = torch.empty(P, 3, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+            xacc = False
+        gptr = (_native.ctypes.c_void_p * 4)(*[None if g is None else g.data_ptr() for g in gh])
         with torch.cuda.device(dev):
-            _native.check(lib.gsd_deform_mlp_train_backward(P, _ptr(g), _ptr_array(ctx.wc), _ptr(ctx.ws),
-                                                            None if dx is None else _ptr(dx), _ptr_array(dW),
-                                                            _ptr_array(db), _stream(dev)))
+            _native.check(lib.gsd_deform_mlp_train_backward_heads(
+                P, gptr, _ptr_array(ctx.wc), _ptr(ctx.ws), None if dx is None else _ptr(dx), int(bool(xacc)),
+                _ptr_array(dW), _ptr_array(db), int(bool(acc)), _stream(dev)))
         ctx.ws = None
-        return (dx, None, *dW, *db)
+        gx = None if (xs is not None or dx is None) else dx
+        gp = (None,) * len(ctx.params) if sinks is not None else (*dW, *db)
+        return (gx, None, *gp)
 
 
 def _train_forward(net: "DirectTemporalNeRF", x: torch.Tensor, ts: torch.Tensor):
     ws, bs = _param_list(net)
-    out = _MLPTrainF32.apply(x, ts, *ws, *bs)
-    return tuple(o.contiguous() for o in out.split([3, 3, 4, 48], dim=-1))
+    return _MLPTrainF32.apply(x, ts, *ws, *bs)
 
 
 def positional_encoding(x: torch.Tensor, n_freqs: int = 10) -> torch.Tensor:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 14
+#define GSD_ABI_VERSION 15
 
 enum {
     GSD_OK = 0,
@@ -383,6 +383,17 @@ int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, cons
  * (d_weights[12], d_biases[12], the parameters' shapes; stored, not accumulated).  weights: the forward's. */
 int gsd_deform_mlp_train_backward(int64_t P, const float* grad_out, const float* const* weights, void* workspace,
                                   float* dx, float* const* d_weights, float* const* d_biases, void* stream);
+
+/* The same with the four heads as separate row-major outputs (dx (P,3), d log-scale (P,3), d quaternion (P,4),
+ * dSH (P,48)) instead of one (P,58) array: what render() consumes, with no split copies. */
+int gsd_deform_mlp_train_forward_heads(int64_t P, const float* x, const float* t, const float* const* weights,
+                                       const float* const* biases, void* workspace, float* const* heads, void* stream);
+/* Backward from the four heads' gradients (grad_heads[4], same shapes; a NULL entry is a zero gradient).  dx: stored,
+ * or added to when dx_accumulate != 0; the weight / bias gradients likewise with accumulate != 0 (a parameter's
+ * existing .grad as the destination, as autograd's accumulation would leave it). */
+int gsd_deform_mlp_train_backward_heads(int64_t P, const float* const* grad_heads, const float* const* weights,
+                                        void* workspace, float* dx, int32_t dx_accumulate, float* const* d_weights,
+                                        float* const* d_biases, int32_t accumulate, void* stream);
 
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead
