@@ -952,9 +952,11 @@ struct MlpWs {
     int64_t ldp;
     void* ffrag[9];   // forward A = W
     void* bfrag[9];   // backward A = W^T
+    void* cfrag[8];   // the backward chain's W^T in the accumulator k order: layers 1-7 (layer 5: rows 64-319), [0]: W0^T's enc(x) rows
     float* bias_heads;
     float *E, *ET, *H[9];   // H[1..8]: the hidden layers' outputs
     float *Gh, *ga, *gb, *dE;
+    float* G[9];      // the backward chain's gradients: G[0] = g8 (Gh), G[i] = g_{8-i} (G[1], G[2] = ga, gb)
     float *partial, *bias_partial;
     unsigned short* bits[9];   // bits[1..8]: the ReLU masks of H[1..8] (16 row blocks x 2 halves x ldp words)
 };
@@ -971,6 +973,7 @@ size_t carve_mlp(void* base, int64_t P, MlpWs* w) {
     const size_t row = sizeof(float) * (size_t)v.ldp;
     for (int l = 0; l < 9; ++l) v.ffrag[l] = take(mlp_frag_bytes(kMlpOut[l], kMlpIn[l]));
     for (int l = 0; l < 9; ++l) v.bfrag[l] = take(mlp_frag_bytes(kMlpIn[l], kMlpOut[l]));
+    for (int l = 0; l < 8; ++l) v.cfrag[l] = take(mlp_frag_bytes(l == 0 ? 64 : 256, 256));
     v.bias_heads = reinterpret_cast<float*>(take(64 * sizeof(float)));
     v.E = reinterpret_cast<float*>(take(64 * row));
     v.ET = reinterpret_cast<float*>(take(32 * row));
@@ -980,6 +983,10 @@ size_t carve_mlp(void* base, int64_t P, MlpWs* w) {
     v.ga = reinterpret_cast<float*>(take(256 * row));
     v.gb = reinterpret_cast<float*>(take(256 * row));
     v.dE = reinterpret_cast<float*>(take(64 * row));
+    v.G[0] = v.Gh;
+    v.G[1] = v.ga;
+    v.G[2] = v.gb;
+    for (int i = 3; i < 9; ++i) v.G[i] = reinterpret_cast<float*>(take(256 * row));
     const int64_t chunks = (P + kMlpChunk - 1) / kMlpChunk;
     v.partial = reinterpret_cast<float*>(take(sizeof(float) * (size_t)chunks * 256 * 320));
     v.bias_partial = reinterpret_cast<float*>(take(sizeof(float) * (size_t)chunks * 256));
@@ -1018,6 +1025,31 @@ void mlp_pack_all(float* const* weights, const MlpWs& ws, bool backward, bool fu
         pp.M = backward ? kMlpIn[l] : kMlpOut[l];
         pp.K = backward ? kMlpOut[l] : kMlpIn[l];
         pp.out = backward ? ws.bfrag[l] : ws.ffrag[l];
+        gsd::launch_mlp_pack(pp, s);
+    }
+}
+// the backward chain's W^T packs (k_mlp_bwd_chain) and the two natural-order ones it still needs: W8^T (its first
+// step) and W5^T (the enc(x) rows' GEMM of g5)
+void mlp_pack_chain(float* const* weights, const MlpWs& ws, hipStream_t s) {
+    for (int l = 0; l < 8; ++l) {
+        gsd::MlpPackParams pp{};
+        pp.w = mlp_weight(l, weights);
+        pp.transpose = 1;
+        pp.perm_from = 0;
+        pp.M = l == 0 ? 64 : 256;
+        pp.m_off = l == 5 ? 64 : 0;
+        pp.K = 256;
+        pp.out = ws.cfrag[l];
+        gsd::launch_mlp_pack(pp, s);
+    }
+    for (int l : {5, 8}) {
+        gsd::MlpPackParams pp{};
+        pp.perm_from = 1 << 30;
+        pp.w = mlp_weight(l, weights);
+        pp.transpose = 1;
+        pp.M = kMlpIn[l];
+        pp.K = kMlpOut[l];
+        pp.out = ws.bfrag[l];
         gsd::launch_mlp_pack(pp, s);
     }
 }
@@ -1181,6 +1213,45 @@ static int mlp_train_backward(int64_t P, const gsd::MlpHeadsIn& gin, const float
         gsd::launch_mlp_gemm(g, gsd::kMlpBwdMask, s);
     };
     (void)chunks;
+    // GSD_MLP_BWD=chain: the fused dX chain (k_mlp_bwd_chain) instead of the layer-by-layer dX GEMMs
+    static const bool chain = [] {
+        const char* e = getenv("GSD_MLP_BWD");
+        return e && strcmp(e, "chain") == 0;
+    }();
+    if (chain) {
+        timed(kMlpTrainBwd, s, [&] {
+            mlp_pack_chain(W, ws, s);
+            gsd::MlpChainParams c{};
+            c.P = (int)P;
+            c.ldp = ldp;
+            c.heads = gin;
+            c.frags[0] = ws.bfrag[8];
+            for (int i = 1; i < 8; ++i) c.frags[i] = ws.cfrag[8 - i];
+            c.frags_e = ws.cfrag[0];
+            for (int i = 0; i < 8; ++i) c.bits[i] = ws.bits[8 - i];
+            for (int i = 0; i < 9; ++i) c.G[i] = ws.G[i];
+            c.dE = ws.dE;
+            gsd::launch_mlp_bwd_chain(c, s);
+            if (dx) {   // d enc(x) += W5^T[enc(x) rows] g5
+                gsd::MlpGemmParams g{};
+                g.P = (int)P; g.ldp = ldp; g.src0 = ws.G[3]; g.ks0 = 16; g.frags = ws.bfrag[5]; g.rb = kMlpIn[5] / 32;
+                g.rb_launch = 2; g.n_a = 64; g.dst_a = ws.dE; g.accumulate_a = 1;
+                gsd::launch_mlp_gemm(g, gsd::kMlpBwdMask, s);
+                gsd::launch_mlp_encode_bwd((int)P, ldp, ws.E, ws.dE, dx, dx_accumulate, s);
+            }
+            wgrad(8, ws.G[0], 2, ws.H[8], nullptr, 8, 8);
+            for (int l = 7; l >= 0; --l) {
+                const float* g = ws.G[8 - l];
+                if (l == 0) wgrad(0, g, 8, ws.E, ws.ET, 3, 2);
+                else if (l == 5) {
+                    wgrad(5, g, 8, ws.E, nullptr, 2, 2, 0);
+                    wgrad(5, g, 8, ws.H[5], nullptr, 8, 8, 64, 1);
+                } else wgrad(l, g, 8, ws.H[l], nullptr, 8, 8);
+            }
+        });
+        GSD_CHECK(false, s);
+        return GSD_OK;
+    }
     timed(kMlpTrainBwd, s, [&] {
         mlp_pack_all(W, ws, true, false, s);
         gsd::launch_mlp_rows_to_features((int)P, ldp, gin, ws.Gh, 64, s);

@@ -322,6 +322,7 @@ struct MlpPackParams {
     // half h is column 8 (j >> 2) + 4 h + (j & 3) of the step), for a B operand read straight from the previous
     // layer's accumulators (k_mlp_fwd_fused); natural order below it
     int perm_from;
+    int m_off;             // transpose: A row m is W^T row m + m_off (layer 5's h rows for the backward chain)
 };
 // The layer-fused training forward (k_mlp_fwd_fused): the encoding in, every hidden layer's output, its ReLU words
 // and the heads out; the weights packed with the accumulator-order k permutation (perm_from 0; layer 5: 4; layer 0:
@@ -355,6 +356,20 @@ struct MlpFusedParams {
     unsigned short* bits[8]; // its ReLU words: [(rb * 2 + h) * ldp + g]
     MlpHeads heads;          // the four heads' outputs
 };
+// The backward's dX chain (k_mlp_bwd_chain): step i = layer 8 - i multiplies W^T by g_{8-i} (frags[i]: W8^T natural
+// k order, K = 64; then W7^T .. W1^T in the accumulator order, layer 5's rows 64-319), masks by the forward's ReLU
+// words of h_{8-i} (bits[i]) and stores its input g_{8-i} to G[i] (G[0]: [64][ldp], the rest [256][ldp]); the final
+// step stores g0 to G[8] and W0^T's enc(x) rows times g0 to dE ([64][ldp]).
+struct MlpChainParams {
+    int P, ldp;
+    MlpHeadsIn heads;                 // the heads' incoming gradients
+    const void* frags[8];
+    const void* frags_e;              // W0^T rows 0-63 (accumulator order, K = 256)
+    const unsigned short* bits[8];
+    float* G[9];
+    float* dE;
+};
+void launch_mlp_bwd_chain(const MlpChainParams& p, hipStream_t s);
 enum { kMlpFwdRelu = 0, kMlpFwdHeads = 1, kMlpBwdMask = 2 };
 struct MlpGemmParams {
     int P, ldp;                     // Gaussians; row stride of the feature-major matrices (P rounded up to 256)
@@ -365,6 +380,7 @@ struct MlpGemmParams {
     const void* frags;              // k_mlp_pack output: [ks][rb][split][lane]
     int rb;                         // output row blocks of 32 (of the packed A)
     int rb_off;                     // launch-internal: first row block of this workgroup row (grid.y)
+    int rb_launch;                  // nonzero: only row blocks 0 .. rb_launch - 1 of the packed A (2 supported)
     const float* bias;              // forward: 32 rb floats
     float* dst;                     // forward hidden: [32 rb][ldp]; backward: g rows
     MlpHeads heads;                 // heads: the four outputs (58 columns)

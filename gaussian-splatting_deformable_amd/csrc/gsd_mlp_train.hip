@@ -26,6 +26,15 @@
 
 #include "gsd_kernels.h"
 
+// GSD_ABLATE (timing experiments only, never a product build): bit 1 drops the GEMM epilogue's global stores, 2 its
+// MFMAs, 4 the fused forward's activation stores, 8 its MFMAs, 16 the weight-gradient MFMAs, 64 the fused forward's
+// weight copies, 128 the GEMM's copies, 256 the fused forward's per-k-step wait + barrier, 512 five of its six
+// copies per k-step, 2048 the fused forward's weight copies through registers
+// (a load one k-step ahead, then a ds_write; results exact).  The results are then garbage; the durations say what each part costs.
+#ifndef GSD_ABLATE
+#define GSD_ABLATE 0
+#endif
+
 namespace gsd {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -60,6 +69,15 @@ __device__ __forceinline__ f32x16 mfma_x6(const Split8& a, const Split8& b, f32x
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, acc, 0, 0, 0);
     return acc;
 }
+template <int ABL>
+__device__ __forceinline__ f32x16 mfma_x6_abl(const Split8& a, const Split8& b, f32x16 acc) {
+    if constexpr (ABL != 0) {
+        acc[0] += (float)a.hi[0] * (float)b.hi[0] + (float)a.lo[1] * (float)b.lo[1];
+        return acc;
+    } else {
+        return mfma_x6(a, b, acc);
+    }
+}
 
 // ---- weights: the reference's pieces, the padded input layout ----
 __device__ __forceinline__ int mlp_col(int map, int k) {
@@ -90,7 +108,8 @@ __global__ __launch_bounds__(256) void k_mlp_pack(MlpPackParams p) {
         const int h = lane >> 5;
         const int k = 16 * ks + (ks >= p.perm_from ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j);
         // forward: A = W, rows m = output features, columns k = (padded) input features; backward: A = W^T
-        const float* e = p.transpose ? mlp_elem(p.w, k, mlp_col(p.w.map, m)) : mlp_elem(p.w, m, mlp_col(p.w.map, k));
+        const float* e = p.transpose ? mlp_elem(p.w, k, mlp_col(p.w.map, m + p.m_off))
+                                     : mlp_elem(p.w, m, mlp_col(p.w.map, k));
         v[j] = e ? *e : 0.f;
     }
     const Split8 s = split8(v);
@@ -263,7 +282,8 @@ __device__ __forceinline__ void gemm_epilogue(const MlpGemmParams& p, const f32x
                 const float4 old = *reinterpret_cast<const float4*>(d);
                 o = make_float4(old.x + y.x, old.y + y.y, old.z + y.z, old.w + y.w);
             }
-            *reinterpret_cast<float4*>(d) = o;
+            if constexpr (!(GSD_ABLATE & 1)) *reinterpret_cast<float4*>(d) = o;
+            else if (o.x == 1234.5f) *reinterpret_cast<float4*>(d) = o;
         }
         wave_lds_handoff();   // the next block's writes stay behind these reads
     }
@@ -363,7 +383,7 @@ __global__ __launch_bounds__(512) void k_mlp_gemm_dma(MlpGemmParams p) {
     for (int ks = 0; ks < KS; ++ks) {
         const int slot = ks & 3;
         // k-step ks + 3 into the slot k-step ks - 1 read (every wave is past it)
-        GSD_GEMM_DMA_ISSUE(ks + 3, (ks + 3) & 3);
+        if constexpr (!(GSD_ABLATE & 128)) GSD_GEMM_DMA_ISSUE(ks + 3, (ks + 3) & 3);
         const float* xrow = reinterpret_cast<const float*>(s_mem + L::kX0 + slot * L::kXSlot) + wave * 32 + c;
         float xv[8];
 #pragma unroll
@@ -376,7 +396,7 @@ __global__ __launch_bounds__(512) void k_mlp_gemm_dma(MlpGemmParams p) {
             a.hi = sa[(r * 3) * 64 + lane];
             a.mid = sa[(r * 3 + 1) * 64 + lane];
             a.lo = sa[(r * 3 + 2) * 64 + lane];
-            acc[r] = mfma_x6(a, b, acc[r]);
+            acc[r] = mfma_x6_abl<GSD_ABLATE & 2>(a, b, acc[r]);
         }
         wait_vm<2 * L::kPerStage>();   // k-step ks + 1 landed; ks + 2 and ks + 3 stay in flight across the barrier
         raw_barrier();
@@ -437,30 +457,64 @@ __device__ __forceinline__ void wait_vm_u(int n) {
     }
 }
 
-// global stores a k-step of a fused layer issues (the layer before's output rows and ReLU words, see below)
+// global stores a k-step of a fused layer issues (the layer before's output rows and ReLU words, see below): all of
+// them, and those issued after the k-step's last weight copy (row blocks 5-7 and the ReLU word)
 constexpr int kActStores = 8;   // 4-B row stores per activation k-step (a 16-B form via a quad transpose was 1.5 % slower)
 __device__ __forceinline__ constexpr int fused_stores(int kse, int ks, int prev) {
     return ks < 0 ? prev : (ks < kse ? 0 : kActStores + (ks - kse < 8 ? 1 : 0));
 }
+__device__ __forceinline__ constexpr int fused_stores_late(int kse, int ks, int prev) {
+    return ks < 0 ? (prev ? 3 : 0) : (ks < kse ? 0 : 3 + (ks - kse < 8 ? 1 : 0));
+}
 
+// elements 2 jp, 2 jp + 1 of split8 (one dword of each plane)
+__device__ __forceinline__ void split_pair(const float (&v)[8], int jp, Split8& s) {
+#pragma unroll
+    for (int j = 2 * jp; j < 2 * jp + 2; ++j) {
+        const __bf16 h = (__bf16)v[j];
+        const float r1 = v[j] - (float)h;
+        const __bf16 m = (__bf16)r1;
+        s.hi[j] = h;
+        s.mid[j] = m;
+        s.lo[j] = (__bf16)(r1 - (float)m);
+    }
+}
+
+// MFMA m (0-5, smallest product first) of mfma_x6
+template <int M>
+__device__ __forceinline__ f32x16 mfma_x6_part(const Split8& a, const Split8& b, f32x16 acc) {
+    if constexpr (GSD_ABLATE & 8) {
+        acc[M] += (float)a.hi[M] * (float)b.hi[M];
+        return acc;
+    }
+    if constexpr (M == 0) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, acc, 0, 0, 0);
+    if constexpr (M == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, acc, 0, 0, 0);
+    if constexpr (M == 2) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, acc, 0, 0, 0);
+    if constexpr (M == 3) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, acc, 0, 0, 0);
+    if constexpr (M == 4) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, acc, 0, 0, 0);
+}
 
 // One hidden layer's k-steps -- KSE from the encoding registers (xe: enc(x) k-steps 0-3, then xt: enc(t) k-steps
 // 4-5), then KSA from the activation registers -- fully unrolled so that every register-array index is a constant.
-// s: the global k-step of the layer's first (its ring slot is s & 3).  Each k-step:
-//  1. copies k-step s + ks + 3 (of this layer, or of the next one's first three) into the slot k-step s + ks - 1
-//     read: 24 chunks of 1 KB, six per wave, shared by the four waves;
-//  2. per row block: the next block's three fragments read from LDS, then this block's six MFMAs; beside them one
-//     of the eight rows of the PREVIOUS layer's output this k-step consumes (act[ks - KSE]) goes to HBM (and on the
-//     first eight of them, that row block's ReLU word): the output stores ride under the MFMAs instead of stalling
-//     an epilogue, and act is live anyway;
-//  3. s_waitcnt vmcnt(stores and copies issued after k-step s + ks + 1's copies) and a raw barrier.
+// s: the global k-step of the layer's first (its ring slot is s & 3).  A k-step is 48 MFMAs (8 row blocks x 6), and
+// everything else it does is placed one piece per MFMA gap (sched_barriers fix the order), where its issue hides
+// under the MFMA's 32 cycles instead of adding to them:
+//  - the next row block's three fragments, read from LDS at the row block's start;
+//  - the copy of k-step s + ks + 3 (of this layer, or of the next one's first three) into the slot k-step
+//    s + ks - 1 read: 24 chunks of 1 KB, six per wave (shared by the four waves), one per row block 0-5 (gap 1);
+//  - one of the eight rows of the PREVIOUS layer's output this k-step consumes (act[ks - KSE]) to HBM per row block
+//    (gap 3), and on the first eight k-steps that row block's ReLU word (row block 7, gap 5): the output stores ride
+//    under the MFMAs instead of stalling an epilogue, and act is live anyway;
+//  - the three-term split of the NEXT k-step's B operand, a pair of elements per gap (row blocks 1-4, gap 5);
+// then s_waitcnt vmcnt(the stores and copies issued after k-step s + ks + 1's last copy) and a raw barrier.
 // PREV: the stores of each of the layer before's last two k-steps (0 after layer 0).
 template <int KSE, int KSA, int PREV>
 __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsigned char* s_mem, int s, int l,
                                                    int wave, int lane, unsigned voff_h, unsigned voff_b,
                                                    const float (&xe)[4][8], const float (&xt)[2][8],
                                                    const float (&act)[16][8], const unsigned (&bits)[8],
-                                                   f32x16 (&acc)[8]) {
+                                                   f32x16 (&acc)[8], bf16x8 (&R)[6]) {
     constexpr int KS = KSE + KSA;
     const bf16x8* fc = reinterpret_cast<const bf16x8*>(p.frags[l]) + lane;
     // past the last hidden layer: its own last k-step again (a harmless re-copy keeps the per-step count uniform)
@@ -470,22 +524,21 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
     unsigned short* Bp = KSA ? p.bits[l - 1] : nullptr;
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f32x16{};
+    // the B operand of k-step ks (a constant index after unrolling)
+    auto operand = [&](int ks) -> const float(&)[8] {
+        if (ks < KSE) return ks < 4 ? xe[ks < 4 ? ks : 0] : xt[ks >= 4 && ks < 6 ? ks - 4 : 0];
+        return act[ks >= KSE ? ks - KSE : 0];
+    };
+    Split8 b = split8(operand(0));
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-        {
-            const int kk = ks + 3;
-            const bf16x8* f = kk < KS ? fc + kk * kFusedStep : (l < 7 ? fn + (kk - KS) * kFusedStep : fn);
-            const unsigned dst = lds_addr(s_mem) + ((s + kk) & 3) * (24 * 1024);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const int ch = wave + 4 * i;
-                dma16_asm(f + ch * 64, __builtin_amdgcn_readfirstlane(dst + ch * 1024));
-            }
-        }
-        Split8 b;
-        if (ks < KSE) b = ks < 4 ? split8(xe[ks < 4 ? ks : 0]) : split8(xt[ks >= 4 && ks < 6 ? ks - 4 : 0]);
-        else b = split8(act[ks >= KSE ? ks - KSE : 0]);
+        const int kk = ks + 3;
+        const bf16x8* f = kk < KS ? fc + kk * kFusedStep : (l < 7 ? fn + (kk - KS) * kFusedStep : fn);
+        const unsigned dst = lds_addr(s_mem) + ((s + kk) & 3) * (24 * 1024);
         const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + ((s + ks) & 3) * (24 * 1024));
+        const int k2 = ks >= KSE ? ks - KSE : 0;   // act[k2][r]: row 16 k2 + 8 (r >> 2) + 4 h + (r & 3)
+        const bool stores = ks >= KSE && !(GSD_ABLATE & 4);
+        Split8 bn = b;
         Split8 a;
         a.hi = sa[lane];
         a.mid = sa[64 + lane];
@@ -498,22 +551,46 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
                 an.mid = sa[((r + 1) * 3 + 1) * 64 + lane];
                 an.lo = sa[((r + 1) * 3 + 2) * 64 + lane];
             }
-            __builtin_amdgcn_sched_barrier(0);   // the next block's reads issue ahead of this block's MFMAs
-            if (ks >= KSE) {
-                const int k2 = ks >= KSE ? ks - KSE : 0;   // act[k2][r]: row 16 k2 + 8 (r >> 2) + 4 h + (r & 3)
-                // nontemporal: the 8 GB of hidden outputs stream past L2 instead of evicting the weights every
-                // workgroup re-reads from it (2 % faster than plain stores)
-                __builtin_nontemporal_store(act[k2][r], Hp + (size_t)(16 * k2 + 8 * (r >> 2) + (r & 3)) * ldp + voff_h);
-                if (r == 0 && k2 < 8)
-                    __builtin_nontemporal_store((unsigned short)bits[k2 < 8 ? k2 : 0], Bp + (size_t)(2 * k2) * ldp + voff_b);
-            }
-            acc[r] = mfma_x6(a, b, acc[r]);
-            a = an;
             __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<0>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<1>(a, b, acc[r]);
+            if (r < ((GSD_ABLATE & 512) ? 1 : 6) && !(GSD_ABLATE & 64)) {
+                const int ch = wave + 4 * r;
+                if constexpr (GSD_ABLATE & 2048) {
+                    // k-step ks + 2's chunk (loaded one k-step ago) to LDS, then k-step ks + 3's into the register
+                    *reinterpret_cast<bf16x8*>(s_mem + ((s + ks + 2) & 3) * (24 * 1024) + ch * 1024 + 16 * lane) = R[r];
+                    R[r] = f[ch * 64];
+                } else {
+                    dma16_asm(f + ch * 64, __builtin_amdgcn_readfirstlane(dst + ch * 1024));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<2>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<3>(a, b, acc[r]);
+            // nontemporal: the 8 GB of hidden outputs stream past L2 instead of evicting the weights every
+            // workgroup re-reads from it (2 % faster than plain stores)
+            if (stores)
+                __builtin_nontemporal_store(act[k2][r], Hp + (size_t)(16 * k2 + 8 * (r >> 2) + (r & 3)) * ldp + voff_h);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<4>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<5>(a, b, acc[r]);
+            if (r >= 1 && r <= 4 && ks + 1 < KS) split_pair(operand(ks + 1 < KS ? ks + 1 : 0), r - 1, bn);
+            if (r == 7 && stores && k2 < 8)
+                __builtin_nontemporal_store((unsigned short)bits[k2 < 8 ? k2 : 0], Bp + (size_t)(2 * k2) * ldp + voff_b);
+            __builtin_amdgcn_sched_barrier(0);
+            a = an;
         }
-        wait_vm_u(fused_stores(KSE, ks - 2, PREV) + fused_stores(KSE, ks - 1, PREV) + fused_stores(KSE, ks, PREV) +
-                  12);
-        raw_barrier();
+        b = bn;
+        if constexpr (GSD_ABLATE & 2048) {
+            raw_barrier();   // the ds_writes (lgkmcnt) before it; the loads and stores stay in flight
+        } else if constexpr (!(GSD_ABLATE & 256)) {
+            wait_vm_u(fused_stores_late(KSE, ks - 2, PREV) + fused_stores(KSE, ks - 1, PREV) +
+                      fused_stores(KSE, ks, PREV) + 12);
+            raw_barrier();
+        }
     }
 }
 
@@ -569,7 +646,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     float act[16][8];
     unsigned bits[8];
     f32x16 acc[8];
-    {
+    bf16x8 R[6];
+    if constexpr (GSD_ABLATE & 2048) {
+        const bf16x8* f0 = reinterpret_cast<const bf16x8*>(p.frags[0]) + lane;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int ch = wave + 4 * i;
+                R[i] = f0[k * kFusedStep + ch * 64];
+                if (k < 2) *reinterpret_cast<bf16x8*>(s_mem + k * (24 * 1024) + ch * 1024 + 16 * lane) = R[i];
+            }
+        __syncthreads();
+    } else {
         const bf16x8* f0 = reinterpret_cast<const bf16x8*>(p.frags[0]) + lane;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
@@ -579,24 +668,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
                 dma16_asm(f0 + k * kFusedStep + ch * 64,
                           __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + k * (24 * 1024) + ch * 1024));
             }
+        wait_vm_c<12>();
+        raw_barrier();
     }
-    wait_vm_c<12>();
-    raw_barrier();
-    fused_hidden_layer<6, 0, 0>(p, s_mem, 0, 0, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+    fused_hidden_layer<6, 0, 0>(p, s_mem, 0, 0, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
     fused_hidden_epilogue(s_bias, h, acc, act, bits);
-    fused_hidden_layer<0, 16, 0>(p, s_mem, 6, 1, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+    fused_hidden_layer<0, 16, 0>(p, s_mem, 6, 1, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
     fused_hidden_epilogue(s_bias + 256, h, acc, act, bits);
 #pragma unroll 1
     for (int l = 2; l <= 4; ++l) {
-        fused_hidden_layer<0, 16, 8>(p, s_mem, 6 + 16 * (l - 1), l, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+        fused_hidden_layer<0, 16, 8>(p, s_mem, 6 + 16 * (l - 1), l, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
         fused_hidden_epilogue(s_bias + 256 * l, h, acc, act, bits);
     }
-    fused_hidden_layer<4, 16, 8>(p, s_mem, 70, 5, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc);
+    fused_hidden_layer<4, 16, 8>(p, s_mem, 70, 5, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
     fused_hidden_epilogue(s_bias + 256 * 5, h, acc, act, bits);
 #pragma unroll 1
     for (int l = 6; l <= 7; ++l) {
         fused_hidden_layer<0, 16, 8>(p, s_mem, 90 + 16 * (l - 6), l, wave, lane, voff_h, voff_b, xe, xt, act, bits,
-                                     acc);
+                                     acc, R);
         fused_hidden_epilogue(s_bias + 256 * l, h, acc, act, bits);
     }
     // the heads (58 outputs, two row blocks): their own ring over the same LDS, 6 chunks per k-step (two copies per
@@ -662,6 +751,193 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     }
 }
 
+// ---- the backward's dX chain fused across the layers ----
+// g_{l-1} = (W_l^T g_l) masked by the forward's ReLU words of h_l, from the heads' gradient g8 down to g0, in one
+// kernel the way k_mlp_fwd_fused runs the forward: a wave keeps its 32 Gaussians' gradient in registers, layer l's
+// accumulators becoming (masked) layer l - 1's B operand with no lane movement (W^T packed with the accumulator-order
+// k permutation, k_mlp_pack perm_from 0; the first step's g8 comes in natural order from the heads' row-major
+// gradients), the packed W^T k-steps (24 KB) shared by the four waves through a four-slot LDS ring.  Every g_l goes
+// to HBM once (the weight gradients' operand), its rows stored under the next step's MFMAs; nothing is re-read.
+// A final two-row-block step multiplies g0 by W0^T's enc(x) rows: the encoding's gradient (layer 5's enc(x) rows
+// are the separate k_mlp_gemm_dma of g5 that adds to it).  The ring's copies go through registers (a 16-B load of
+// k-step ks + 3 one k-step ahead, its ds_write the next), so every memory operation is the compiler's to wait for.
+
+// one step's k-steps.  B operand k-step ks = act[ks]: natural row order (NAT: lane half h holds rows 16 ks + 8 h + j)
+// or the accumulator order (rows 16 ks + 8 (j >> 2) + 4 h + (j & 3)); the rows are stored to Gp (+ voff) under the
+// MFMAs.  s: the global k-step of the step's first; the ring is fed with k-steps of this step, then of the next
+// (fn), or re-copies of this step's last when LAST.
+template <int KS, bool NAT, bool LAST>
+__device__ __forceinline__ void chain_step(const bf16x8* fc, const bf16x8* fn, float* __restrict__ Gp, unsigned voff,
+                                           int ldp, unsigned char* s_mem, int s, int wave, int lane,
+                                           const float (&act)[16][8], f32x16 (&acc)[8], bf16x8 (&R)[6]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = f32x16{};
+    Split8 b = split8(act[0]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int kk = ks + 3;
+        const bf16x8* f = kk < KS ? fc + kk * kFusedStep : (LAST ? fc + (KS - 1) * kFusedStep : fn + (kk - KS) * kFusedStep);
+        unsigned char* wslot = s_mem + ((s + ks + 2) & 3) * (24 * 1024) + 16 * lane;
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + ((s + ks) & 3) * (24 * 1024));
+        Split8 bn = b;
+        Split8 a;
+        a.hi = sa[lane];
+        a.mid = sa[64 + lane];
+        a.lo = sa[128 + lane];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            Split8 an = a;
+            if (r + 1 < 8) {
+                an.hi = sa[((r + 1) * 3) * 64 + lane];
+                an.mid = sa[((r + 1) * 3 + 1) * 64 + lane];
+                an.lo = sa[((r + 1) * 3 + 2) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<0>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<1>(a, b, acc[r]);
+            if (r < 6) {   // k-step ks + 2's chunk (loaded one k-step ago) to LDS, then k-step ks + 3's into R
+                const int ch = wave + 4 * r;
+                *reinterpret_cast<bf16x8*>(wslot + ch * 1024) = R[r];
+                R[r] = f[ch * 64];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<2>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<3>(a, b, acc[r]);
+            {
+                const int roff = NAT ? r : 8 * (r >> 2) + (r & 3);
+                __builtin_nontemporal_store(act[ks][r], Gp + (size_t)(16 * ks + roff) * ldp + voff);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<4>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma_x6_part<5>(a, b, acc[r]);
+            if (r >= 1 && r <= 4 && ks + 1 < KS) split_pair(act[ks + 1 < KS ? ks + 1 : 0], r - 1, bn);
+            __builtin_amdgcn_sched_barrier(0);
+            a = an;
+        }
+        b = bn;
+        raw_barrier();   // the ds_writes before it; loads and stores stay in flight
+    }
+}
+
+// threshold_backward by the forward's ReLU words: act (the next step's B operand, accumulator order) = acc where h > 0
+__device__ __forceinline__ void chain_mask(const unsigned (&w)[8], const f32x16 (&acc)[8], float (&act)[16][8]) {
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) act[2 * rb + (q >> 3)][q & 7] = (w[rb] >> q) & 1u ? acc[rb][q] : 0.f;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_bwd_chain(MlpChainParams p) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[4 * 24 * 1024];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
+    const int g = blockIdx.x * 128 + wave * 32 + c;   // < ldp (the grid covers ldp / 128 workgroups)
+    const int ldp = p.ldp;
+    const unsigned voff_n = (unsigned)(8 * h) * (unsigned)ldp + (unsigned)g;   // natural order: row 8 h
+    const unsigned voff_a = (unsigned)(4 * h) * (unsigned)ldp + (unsigned)g;   // accumulator order: row 4 h
+    float act[16][8];
+    f32x16 acc[8];
+    bf16x8 R[6];
+    unsigned w[8];
+    // g8, natural order: act[ks][j] = row 16 ks + 8 h + j of the heads' gradient (58 rows; zero past them and P)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = 16 * ks + 8 * h + j;
+            const int k = n < 3 ? 0 : (n < 6 ? 1 : (n < 10 ? 2 : 3));
+            const int c0 = k == 0 ? 0 : (k == 1 ? 3 : (k == 2 ? 6 : 10));
+            const float* src = p.heads.src[k];
+            act[ks][j] = (g < p.P && n < 58 && src) ? src[(size_t)g * p.heads.ld[k] + (n - c0)] : 0.f;
+        }
+#pragma unroll
+    for (int ks = 4; ks < 16; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) act[ks][j] = 0.f;
+    {   // the ring's first three k-steps: two to LDS now, the third held in R (chain_step writes it at k-step 0)
+        const bf16x8* f0 = reinterpret_cast<const bf16x8*>(p.frags[0]) + lane;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int ch = wave + 4 * i;
+                R[i] = f0[k * kFusedStep + ch * 64];
+                if (k < 2) *reinterpret_cast<bf16x8*>(s_mem + k * (24 * 1024) + ch * 1024 + 16 * lane) = R[i];
+            }
+    }
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) w[rb] = p.bits[0][(size_t)(2 * rb + h) * ldp + g];
+    __syncthreads();
+    const bf16x8* F[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) F[i] = reinterpret_cast<const bf16x8*>(p.frags[i]) + lane;
+    chain_step<4, true, false>(F[0], F[1], p.G[0], voff_n, ldp, s_mem, 0, wave, lane, act, acc, R);
+    chain_mask(w, acc, act);
+#pragma unroll 1
+    for (int i = 1; i < 7; ++i) {
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) w[rb] = p.bits[i][(size_t)(2 * rb + h) * ldp + g];
+        chain_step<16, false, false>(F[i], F[i + 1], p.G[i], voff_a, ldp, s_mem, 4 + 16 * (i - 1), wave, lane, act,
+                                     acc, R);
+        chain_mask(w, acc, act);
+    }
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) w[rb] = p.bits[7][(size_t)(2 * rb + h) * ldp + g];
+    chain_step<16, false, true>(F[7], F[7], p.G[7], voff_a, ldp, s_mem, 4 + 16 * 6, wave, lane, act, acc, R);
+    chain_mask(w, acc, act);   // g0
+    // the final step: W0^T's enc(x) rows (two row blocks) times g0, g0's rows stored under it.  Its own ring over the
+    // same LDS (6 chunks of 1 KB per k-step in 8-KB slots), fed the same way (waves 0 and 1 copy two chunks, 2 and 3
+    // one); R's last loads (re-copies) are abandoned
+    __syncthreads();   // every wave is past the ring's last reads
+    const bf16x8* fe = reinterpret_cast<const bf16x8*>(p.frags_e) + lane;
+    bf16x8 Re[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ch = wave + 4 * i;
+            if (ch < 6) {
+                Re[i] = fe[k * (2 * 3 * 64) + ch * 64];
+                if (k < 2) *reinterpret_cast<bf16x8*>(s_mem + k * (8 * 1024) + ch * 1024 + 16 * lane) = Re[i];
+            }
+        }
+    __syncthreads();
+    f32x16 ho[2] = {f32x16{}, f32x16{}};
+    float* G0 = p.G[8];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+        const Split8 b = split8(act[ks]);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (8 * 1024));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            __builtin_nontemporal_store(act[ks][j], G0 + (size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_a);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ch = wave + 4 * i;
+            if (ch < 6) {
+                *reinterpret_cast<bf16x8*>(s_mem + ((ks + 2) & 3) * (8 * 1024) + ch * 1024 + 16 * lane) = Re[i];
+                Re[i] = fe[min(ks + 3, 15) * (2 * 3 * 64) + ch * 64];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            Split8 a;
+            a.hi = sa[(r * 3) * 64 + lane];
+            a.mid = sa[(r * 3 + 1) * 64 + lane];
+            a.lo = sa[(r * 3 + 2) * 64 + lane];
+            ho[r] = mfma_x6(a, b, ho[r]);
+        }
+        raw_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            p.dE[(size_t)(32 * r + 8 * (q >> 2) + 4 * h + (q & 3)) * ldp + g] = ho[r][q];
+}
+
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
 // One workgroup per Gaussian chunk computes the whole (32 NRB) x (32 KRB) output, one wave per tile of TNB x TKB
 // blocks of 32 x 32 (four waves, one per SIMD with 512 registers; or eight, two per SIMD, on half-size tiles).  Each 16-Gaussian step, every thread loads 64 B of one or two feature rows (of G or X), splits
@@ -723,44 +999,45 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
     }
     // Each row's 32 Gaussians of two steps are loaded together (eight 16-B loads: whole 128-B lines; one 64-B
     // segment per row and step ran the staging at ~2.8 TB/s), and split + written to LDS one step ahead: step s + 1
-    // is staged while step s multiplies, the next pair loaded right after its predecessor's second half is staged.
+    // is staged while step s multiplies.
     // (One row per thread only: with more, e.g. layer 5's 576 rows on 256 threads, the pair of steps in registers
     // spills, so those shapes keep one 16-Gaussian segment per row and step, loaded two steps ahead.)
     constexpr bool kWide = S::RPT == 1;
     constexpr int kWid = kWide ? 32 : 16;
-    float raw[S::RPT][kWid];
-    auto load = [&](int p0) {
+    // wide shapes: two register sets of a pair of steps each (A: pairs 0, 2, ..; B: 1, 3, ..), so a pair is loaded
+    // two steps before its first half is staged and four before its second (one set: one step before the first half
+    // -- the loads then waited on HBM latency)
+    float raw[S::RPT][kWid], rawb[S::RPT][kWid];   // (rawb: wide shapes only; unused, it takes no registers)
+    auto load_into = [&](float (&dst)[S::RPT][kWid], int p0) {
 #pragma unroll
         for (int i = 0; i < S::RPT; ++i)
             if (tid + S::THREADS * i < S::ROWS) {
 #pragma unroll
                 for (int q = 0; q < kWid / 4; ++q) {
                     const float4 f = *reinterpret_cast<const float4*>(src[i] + p0 + 4 * q);
-                    raw[i][4 * q] = f.x; raw[i][4 * q + 1] = f.y; raw[i][4 * q + 2] = f.z; raw[i][4 * q + 3] = f.w;
+                    dst[i][4 * q] = f.x; dst[i][4 * q + 1] = f.y; dst[i][4 * q + 2] = f.z; dst[i][4 * q + 3] = f.w;
                 }
             }
     };
-    auto write = [&](int p0, int buf, int half) {   // half: compile-time after unrolling
+    auto load = [&](int p0) { load_into(raw, p0); };
+    auto write_from = [&](const float (&srcv)[S::RPT][kWid], int p0, int buf, int half) {   // half: compile-time
 #pragma unroll
         for (int i = 0; i < S::RPT; ++i) {
             const int r = tid + S::THREADS * i;
             if (r < S::ROWS) {
                 float v[16];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) v[j] = raw[i][16 * half + j];
+                for (int j = 0; j < 16; ++j) v[j] = srcv[i][16 * half + j];
                 stage_row(v, p0, p_hi, s_op[buf][r], r < 32 * NRB ? &bsum[i] : nullptr);
             }
         }
     };
+    auto write = [&](int p0, int buf, int half) { write_from(raw, p0, buf, half); };
     f32x16 acc[TNB][TKB];
 #pragma unroll
     for (int i = 0; i < TNB; ++i)
 #pragma unroll
         for (int j = 0; j < TKB; ++j) acc[i][j] = f32x16{};
-    load(p_lo);   // the chunk starts on a 32-Gaussian boundary; reads up to ldp stay inside the padded rows
-    write(p_lo, 0, 0);
-    if (!kWide && p_lo + 16 < p_hi) load(p_lo + 16);
-    __syncthreads();
     // one step's multiply: the fragments from LDS buffer bf, six MFMAs per block pair
 #define GSD_WGRAD_MMA(bf)                                                                                       \
     do {                                                                                                        \
@@ -774,30 +1051,39 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
             b_[j].hi = sl[0 + h]; b_[j].mid = sl[2 + h]; b_[j].lo = sl[4 + h];                                  \
         }                                                                                                       \
         _Pragma("unroll") for (int i = 0; i < TNB; ++i)                                                         \
-            _Pragma("unroll") for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6(a_[i], b_[j], acc[i][j]);       \
+            _Pragma("unroll") for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6_abl<GSD_ABLATE & 16>(a_[i], b_[j], acc[i][j]); \
     } while (0)
-    int buf = 0;
     if constexpr (kWide) {
-        // the two waves of a SIMD (w and w + 4) take the step's two phases in opposite orders, so that one's
-        // staging VALU runs beside the other's MFMAs instead of both staging, then both multiplying
+        float (&rA)[S::RPT][kWid] = raw;
+        float (&rB)[S::RPT][kWid] = rawb;
+        load_into(rA, p_lo);   // the chunk starts on a 32-Gaussian boundary; reads up to ldp stay inside the rows
+        if (p_lo + 32 < p_hi) load_into(rB, p_lo + 32);
+        write_from(rA, p_lo, 0, 0);
+        __syncthreads();
+        // the two waves of a SIMD (w and w + 4) take a step's two phases in opposite orders, so that one's staging
+        // VALU runs beside the other's MFMAs instead of both staging, then both multiplying
         const bool mma_first = S::WAVES == 8 && (wave & 4);
-        for (int pb2 = p_lo; pb2 < p_hi; pb2 += 32) {
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int pb = pb2 + 16 * hh;
-                if (pb < p_hi) {   // workgroup-uniform
-                    if (mma_first) GSD_WGRAD_MMA(buf);
-                    if (pb + 16 < p_hi) {
-                        write(pb + 16, buf ^ 1, hh ^ 1);
-                        if (hh == 0 && pb2 + 32 < p_hi) load(pb2 + 32);
-                    }
-                    if (!mma_first) GSD_WGRAD_MMA(buf);
-                    __syncthreads();
-                    buf ^= 1;
-                }
-            }
+        // step pb multiplies LDS buffer (pb / 16) & 1 and stages step pb + 16 into the other
+#define GSD_WGRAD_STEP(PB, BUF, STAGE)                                                                          \
+        if ((PB) < p_hi) {                                                                                      \
+            if (mma_first) GSD_WGRAD_MMA(BUF);                                                                  \
+            if ((PB) + 16 < p_hi) { STAGE; }                                                                    \
+            if (!mma_first) GSD_WGRAD_MMA(BUF);                                                                 \
+            __syncthreads();                                                                                    \
         }
+        for (int p4 = p_lo; p4 < p_hi; p4 += 64) {
+            GSD_WGRAD_STEP(p4, 0, { write_from(rA, p4 + 16, 1, 1); if (p4 + 64 < p_hi) load_into(rA, p4 + 64); })
+            GSD_WGRAD_STEP(p4 + 16, 1, write_from(rB, p4 + 32, 0, 0))
+            GSD_WGRAD_STEP(p4 + 32, 0, { write_from(rB, p4 + 48, 1, 1); if (p4 + 96 < p_hi) load_into(rB, p4 + 96); })
+            GSD_WGRAD_STEP(p4 + 48, 1, write_from(rA, p4 + 64, 0, 0))
+        }
+#undef GSD_WGRAD_STEP
     } else {
+        int buf = 0;
+        load(p_lo);
+        write(p_lo, 0, 0);
+        if (p_lo + 16 < p_hi) load(p_lo + 16);
+        __syncthreads();
         for (int pb = p_lo; pb < p_hi; pb += 16, buf ^= 1) {
             if (pb + 16 < p_hi) {
                 write(pb + 16, buf ^ 1, 0);
@@ -879,6 +1165,10 @@ void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, floa
 // (1.72 ms with all 10 row blocks per workgroup)
 template <int MODE>
 static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
+    if (p.rb_launch == 2) {
+        hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 2>), dim3(p.ldp / 256), dim3(512), 0, s, p);
+        return;
+    }
     switch (p.rb) {   // 320 rows (layer 5's W^T): two workgroup rows of 5 blocks
         case 2: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 2>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;
         case 3: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 3>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;
@@ -890,6 +1180,10 @@ static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
 
 void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s) {
     if (p.P > 0) hipLaunchKernelGGL(k_mlp_fwd_fused, dim3(p.ldp / 128), dim3(256), 0, s, p);
+}
+
+void launch_mlp_bwd_chain(const MlpChainParams& p, hipStream_t s) {
+    if (p.P > 0) hipLaunchKernelGGL(k_mlp_bwd_chain, dim3(p.ldp / 128), dim3(256), 0, s, p);
 }
 
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s) {
