@@ -756,20 +756,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 // kernel the way k_mlp_fwd_fused runs the forward: a wave keeps its 32 Gaussians' gradient in registers, layer l's
 // accumulators becoming (masked) layer l - 1's B operand with no lane movement (W^T packed with the accumulator-order
 // k permutation, k_mlp_pack perm_from 0; the first step's g8 comes in natural order from the heads' row-major
-// gradients), the packed W^T k-steps (24 KB) shared by the four waves through a four-slot LDS ring.  Every g_l goes
-// to HBM once (the weight gradients' operand), its rows stored under the next step's MFMAs; nothing is re-read.
-// A final two-row-block step multiplies g0 by W0^T's enc(x) rows: the encoding's gradient (layer 5's enc(x) rows
-// are the separate k_mlp_gemm_dma of g5 that adds to it).  The ring's copies go through registers (a 16-B load of
-// k-step ks + 3 one k-step ahead, its ds_write the next), so every memory operation is the compiler's to wait for.
+// gradients), the packed W^T k-steps (24 KB) shared by the four waves through a four-slot LDS ring fed by LDS-DMA
+// three k-steps ahead (as the forward; copies through registers measured 1.3 % slower there).  Every g_l goes to HBM
+// once (the weight gradients' operand), its rows stored under the next step's MFMAs; nothing is re-read.  The
+// mask words of all eight steps (16 B per lane each) are loaded at the start: a load issued inside the ring would be
+// waited for by the next k-step's counted wait (the counter retires in order), at HBM latency.  A final two-row-block
+// step multiplies g0 by W0^T's enc(x) rows: the encoding's gradient (layer 5's enc(x) rows are the separate
+// k_mlp_gemm_dma of g5 that adds to it).
+
+// global stores of a chain k-step: all eight act rows, three of them (row blocks 5-7) after the k-step's last copy
+__device__ __forceinline__ constexpr int chain_stores(int ks, int prev) { return ks < 0 ? (prev ? 8 : 0) : 8; }
+__device__ __forceinline__ constexpr int chain_stores_late(int ks, int prev) { return ks < 0 ? (prev ? 3 : 0) : 3; }
 
 // one step's k-steps.  B operand k-step ks = act[ks]: natural row order (NAT: lane half h holds rows 16 ks + 8 h + j)
 // or the accumulator order (rows 16 ks + 8 (j >> 2) + 4 h + (j & 3)); the rows are stored to Gp (+ voff) under the
 // MFMAs.  s: the global k-step of the step's first; the ring is fed with k-steps of this step, then of the next
-// (fn), or re-copies of this step's last when LAST.
-template <int KS, bool NAT, bool LAST>
+// (fn), or re-copies of this step's last when LAST.  PREV: the step before stored rows (every step but the first).
+template <int KS, bool NAT, bool LAST, int PREV>
 __device__ __forceinline__ void chain_step(const bf16x8* fc, const bf16x8* fn, float* __restrict__ Gp, unsigned voff,
                                            int ldp, unsigned char* s_mem, int s, int wave, int lane,
-                                           const float (&act)[16][8], f32x16 (&acc)[8], bf16x8 (&R)[6]) {
+                                           const float (&act)[16][8], f32x16 (&acc)[8]) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = f32x16{};
     Split8 b = split8(act[0]);
@@ -777,7 +783,7 @@ __device__ __forceinline__ void chain_step(const bf16x8* fc, const bf16x8* fn, f
     for (int ks = 0; ks < KS; ++ks) {
         const int kk = ks + 3;
         const bf16x8* f = kk < KS ? fc + kk * kFusedStep : (LAST ? fc + (KS - 1) * kFusedStep : fn + (kk - KS) * kFusedStep);
-        unsigned char* wslot = s_mem + ((s + ks + 2) & 3) * (24 * 1024) + 16 * lane;
+        const unsigned dst = lds_addr(s_mem) + ((s + kk) & 3) * (24 * 1024);
         const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + ((s + ks) & 3) * (24 * 1024));
         Split8 bn = b;
         Split8 a;
@@ -796,10 +802,9 @@ __device__ __forceinline__ void chain_step(const bf16x8* fc, const bf16x8* fn, f
             acc[r] = mfma_x6_part<0>(a, b, acc[r]);
             __builtin_amdgcn_sched_barrier(0);
             acc[r] = mfma_x6_part<1>(a, b, acc[r]);
-            if (r < 6) {   // k-step ks + 2's chunk (loaded one k-step ago) to LDS, then k-step ks + 3's into R
+            if (r < 6) {
                 const int ch = wave + 4 * r;
-                *reinterpret_cast<bf16x8*>(wslot + ch * 1024) = R[r];
-                R[r] = f[ch * 64];
+                dma16_asm(f + ch * 64, __builtin_amdgcn_readfirstlane(dst + ch * 1024));
             }
             __builtin_amdgcn_sched_barrier(0);
             acc[r] = mfma_x6_part<2>(a, b, acc[r]);
@@ -818,16 +823,20 @@ __device__ __forceinline__ void chain_step(const bf16x8* fc, const bf16x8* fn, f
             a = an;
         }
         b = bn;
-        raw_barrier();   // the ds_writes before it; loads and stores stay in flight
+        // k-step ks + 1's copies (issued at k-step ks - 2) landed: wait for all but the younger stores and copies
+        wait_vm_u(chain_stores_late(ks - 2, PREV) + chain_stores(ks - 1, PREV) + chain_stores(ks, PREV) + 12);
+        raw_barrier();
     }
 }
 
-// threshold_backward by the forward's ReLU words: act (the next step's B operand, accumulator order) = acc where h > 0
-__device__ __forceinline__ void chain_mask(const unsigned (&w)[8], const f32x16 (&acc)[8], float (&act)[16][8]) {
+// threshold_backward by the forward's ReLU words (w: the step's eight 16-bit words, two per register): act (the
+// next step's B operand, accumulator order) = acc where h > 0
+__device__ __forceinline__ void chain_mask(const unsigned (&w)[4], const f32x16 (&acc)[8], float (&act)[16][8]) {
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) act[2 * rb + (q >> 3)][q & 7] = (w[rb] >> q) & 1u ? acc[rb][q] : 0.f;
+        for (int q = 0; q < 16; ++q)
+            act[2 * rb + (q >> 3)][q & 7] = (w[rb >> 1] >> (16 * (rb & 1) + q)) & 1u ? acc[rb][q] : 0.f;
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_bwd_chain(MlpChainParams p) {
@@ -837,10 +846,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     const int ldp = p.ldp;
     const unsigned voff_n = (unsigned)(8 * h) * (unsigned)ldp + (unsigned)g;   // natural order: row 8 h
     const unsigned voff_a = (unsigned)(4 * h) * (unsigned)ldp + (unsigned)g;   // accumulator order: row 4 h
+    // the mask words of every step (two 16-bit words per 32-bit word), each lane's own: registers would not fit
+    __shared__ uint4 s_w[8][256];
     float act[16][8];
     f32x16 acc[8];
-    bf16x8 R[6];
-    unsigned w[8];
     // g8, natural order: act[ks][j] = row 16 ks + 8 h + j of the heads' gradient (58 rows; zero past them and P)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -856,71 +865,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     for (int ks = 4; ks < 16; ++ks)
 #pragma unroll
         for (int j = 0; j < 8; ++j) act[ks][j] = 0.f;
-    {   // the ring's first three k-steps: two to LDS now, the third held in R (chain_step writes it at k-step 0)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        unsigned wq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned lo = p.bits[i][(size_t)(2 * (2 * q) + h) * ldp + g];
+            const unsigned hi = p.bits[i][(size_t)(2 * (2 * q + 1) + h) * ldp + g];
+            wq[q] = lo | (hi << 16);
+        }
+        s_w[i][tid] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+    }
+    // before the first copy: plain loads never wait behind one (vmcnt 0, the other counters free; the builtin, so
+    // the compiler knows them done)
+    __builtin_amdgcn_s_waitcnt(0xf70);
+    {
         const bf16x8* f0 = reinterpret_cast<const bf16x8*>(p.frags[0]) + lane;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const int ch = wave + 4 * i;
-                R[i] = f0[k * kFusedStep + ch * 64];
-                if (k < 2) *reinterpret_cast<bf16x8*>(s_mem + k * (24 * 1024) + ch * 1024 + 16 * lane) = R[i];
+                dma16_asm(f0 + k * kFusedStep + ch * 64,
+                          __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + k * (24 * 1024) + ch * 1024));
             }
     }
-#pragma unroll
-    for (int rb = 0; rb < 8; ++rb) w[rb] = p.bits[0][(size_t)(2 * rb + h) * ldp + g];
-    __syncthreads();
+    wait_vm_c<12>();
+    raw_barrier();
     const bf16x8* F[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) F[i] = reinterpret_cast<const bf16x8*>(p.frags[i]) + lane;
-    chain_step<4, true, false>(F[0], F[1], p.G[0], voff_n, ldp, s_mem, 0, wave, lane, act, acc, R);
-    chain_mask(w, acc, act);
+    auto mask = [&](int i) {
+        const uint4 wv = s_w[i][tid];
+        const unsigned wi[4] = {wv.x, wv.y, wv.z, wv.w};
+        chain_mask(wi, acc, act);
+    };
+    chain_step<4, true, false, 0>(F[0], F[1], p.G[0], voff_n, ldp, s_mem, 0, wave, lane, act, acc);
+    mask(0);
 #pragma unroll 1
     for (int i = 1; i < 7; ++i) {
-#pragma unroll
-        for (int rb = 0; rb < 8; ++rb) w[rb] = p.bits[i][(size_t)(2 * rb + h) * ldp + g];
-        chain_step<16, false, false>(F[i], F[i + 1], p.G[i], voff_a, ldp, s_mem, 4 + 16 * (i - 1), wave, lane, act,
-                                     acc, R);
-        chain_mask(w, acc, act);
+        chain_step<16, false, false, 1>(F[i], F[i + 1], p.G[i], voff_a, ldp, s_mem, 4 + 16 * (i - 1), wave, lane, act,
+                                        acc);
+        mask(i);
     }
-#pragma unroll
-    for (int rb = 0; rb < 8; ++rb) w[rb] = p.bits[7][(size_t)(2 * rb + h) * ldp + g];
-    chain_step<16, false, true>(F[7], F[7], p.G[7], voff_a, ldp, s_mem, 4 + 16 * 6, wave, lane, act, acc, R);
-    chain_mask(w, acc, act);   // g0
+    chain_step<16, false, true, 1>(F[7], F[7], p.G[7], voff_a, ldp, s_mem, 4 + 16 * 6, wave, lane, act, acc);
+    mask(7);   // g0
     // the final step: W0^T's enc(x) rows (two row blocks) times g0, g0's rows stored under it.  Its own ring over the
-    // same LDS (6 chunks of 1 KB per k-step in 8-KB slots), fed the same way (waves 0 and 1 copy two chunks, 2 and 3
-    // one); R's last loads (re-copies) are abandoned
-    __syncthreads();   // every wave is past the ring's last reads
+    // same LDS (6 chunks of 1 KB per k-step in 8-KB slots; waves 0 and 1 copy two chunks, 2 and 3 one and re-copy
+    // chunk 0 into the padding), after everything in flight has retired
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
     const bf16x8* fe = reinterpret_cast<const bf16x8*>(p.frags_e) + lane;
-    bf16x8 Re[2];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ch = wave + 4 * i;
-            if (ch < 6) {
-                Re[i] = fe[k * (2 * 3 * 64) + ch * 64];
-                if (k < 2) *reinterpret_cast<bf16x8*>(s_mem + k * (8 * 1024) + ch * 1024 + 16 * lane) = Re[i];
-            }
-        }
-    __syncthreads();
+#define GSD_E_ISSUE(KS)                                                                                        \
+    do {                                                                                                       \
+        const int k_ = min((KS), 15);                                                                          \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                                     \
+            const int ch_ = wave + 4 * i_;                                                                     \
+            dma16_asm(fe + k_ * (2 * 3 * 64) + (ch_ < 6 ? ch_ : 0) * 64,                                       \
+                      __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (8 * 1024) + ch_ * 1024));   \
+        }                                                                                                      \
+    } while (0)
     f32x16 ho[2] = {f32x16{}, f32x16{}};
+    GSD_E_ISSUE(0);
+    GSD_E_ISSUE(1);
+    GSD_E_ISSUE(2);
+    wait_vm_c<4>();
+    raw_barrier();
     float* G0 = p.G[8];
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
+        GSD_E_ISSUE(ks + 3);
         const Split8 b = split8(act[ks]);
         const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (8 * 1024));
 #pragma unroll
         for (int j = 0; j < 8; ++j)
             __builtin_nontemporal_store(act[ks][j], G0 + (size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_a);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ch = wave + 4 * i;
-            if (ch < 6) {
-                *reinterpret_cast<bf16x8*>(s_mem + ((ks + 2) & 3) * (8 * 1024) + ch * 1024 + 16 * lane) = Re[i];
-                Re[i] = fe[min(ks + 3, 15) * (2 * 3 * 64) + ch * 64];
-            }
-        }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             Split8 a;
@@ -929,8 +948,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
             a.lo = sa[(r * 3 + 2) * 64 + lane];
             ho[r] = mfma_x6(a, b, ho[r]);
         }
+        // stage ks + 1 (issued at k-step ks - 2, or in the prologue) landed: all but the younger copies and stores
+        wait_vm_u(4 + (ks >= 2 ? 8 : 0) + (ks >= 1 ? 8 : 0) + 8);
         raw_barrier();
     }
+#undef GSD_E_ISSUE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's re-copies: nothing left in flight at exit
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -1004,10 +1027,7 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
     // spills, so those shapes keep one 16-Gaussian segment per row and step, loaded two steps ahead.)
     constexpr bool kWide = S::RPT == 1;
     constexpr int kWid = kWide ? 32 : 16;
-    // wide shapes: two register sets of a pair of steps each (A: pairs 0, 2, ..; B: 1, 3, ..), so a pair is loaded
-    // two steps before its first half is staged and four before its second (one set: one step before the first half
-    // -- the loads then waited on HBM latency)
-    float raw[S::RPT][kWid], rawb[S::RPT][kWid];   // (rawb: wide shapes only; unused, it takes no registers)
+    float raw[S::RPT][kWid];
     auto load_into = [&](float (&dst)[S::RPT][kWid], int p0) {
 #pragma unroll
         for (int i = 0; i < S::RPT; ++i)
@@ -1054,30 +1074,31 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
             _Pragma("unroll") for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6_abl<GSD_ABLATE & 16>(a_[i], b_[j], acc[i][j]); \
     } while (0)
     if constexpr (kWide) {
-        float (&rA)[S::RPT][kWid] = raw;
-        float (&rB)[S::RPT][kWid] = rawb;
-        load_into(rA, p_lo);   // the chunk starts on a 32-Gaussian boundary; reads up to ldp stay inside the rows
-        if (p_lo + 32 < p_hi) load_into(rB, p_lo + 32);
-        write_from(rA, p_lo, 0, 0);
+        load(p_lo);   // the chunk starts on a 32-Gaussian boundary; reads up to ldp stay inside the padded rows
+        write(p_lo, 0, 0);
         __syncthreads();
-        // the two waves of a SIMD (w and w + 4) take a step's two phases in opposite orders, so that one's staging
-        // VALU runs beside the other's MFMAs instead of both staging, then both multiplying
+        // the two waves of a SIMD (w and w + 4) take the step's two phases in opposite orders, so that one's
+        // staging VALU runs beside the other's MFMAs instead of both staging, then both multiplying.  The next
+        // pair is loaded right after its predecessor's second half is staged (a second register set loading two
+        // steps earlier measured slower: 0.77 -> 0.79 ms per 256 x 256 layer, 0.33 -> 0.41 ms for 64 x 256)
         const bool mma_first = S::WAVES == 8 && (wave & 4);
-        // step pb multiplies LDS buffer (pb / 16) & 1 and stages step pb + 16 into the other
-#define GSD_WGRAD_STEP(PB, BUF, STAGE)                                                                          \
-        if ((PB) < p_hi) {                                                                                      \
-            if (mma_first) GSD_WGRAD_MMA(BUF);                                                                  \
-            if ((PB) + 16 < p_hi) { STAGE; }                                                                    \
-            if (!mma_first) GSD_WGRAD_MMA(BUF);                                                                 \
-            __syncthreads();                                                                                    \
+        int buf = 0;
+        for (int pb2 = p_lo; pb2 < p_hi; pb2 += 32) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int pb = pb2 + 16 * hh;
+                if (pb < p_hi) {   // workgroup-uniform
+                    if (mma_first) GSD_WGRAD_MMA(buf);
+                    if (pb + 16 < p_hi) {
+                        write(pb + 16, buf ^ 1, hh ^ 1);
+                        if (hh == 0 && pb2 + 32 < p_hi) load(pb2 + 32);
+                    }
+                    if (!mma_first) GSD_WGRAD_MMA(buf);
+                    __syncthreads();
+                    buf ^= 1;
+                }
+            }
         }
-        for (int p4 = p_lo; p4 < p_hi; p4 += 64) {
-            GSD_WGRAD_STEP(p4, 0, { write_from(rA, p4 + 16, 1, 1); if (p4 + 64 < p_hi) load_into(rA, p4 + 64); })
-            GSD_WGRAD_STEP(p4 + 16, 1, write_from(rB, p4 + 32, 0, 0))
-            GSD_WGRAD_STEP(p4 + 32, 0, { write_from(rB, p4 + 48, 1, 1); if (p4 + 96 < p_hi) load_into(rB, p4 + 96); })
-            GSD_WGRAD_STEP(p4 + 48, 1, write_from(rA, p4 + 64, 0, 0))
-        }
-#undef GSD_WGRAD_STEP
     } else {
         int buf = 0;
         load(p_lo);

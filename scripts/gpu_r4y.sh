@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 4 final pass, part 2: PMC passes over the cfg4 render step (FETCH_SIZE; WRITE_SIZE; the SQ group), every
+# BASELINE configuration's bench line, and the MLP-live line with its kernel statistics.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; export TMPDIR=/tmp
+O="gpurun_out/${OUT:-r4y}"; mkdir -p "$O"
+PMC_OUT="$O/pmc" PMC_PASSES="FETCH_SIZE;WRITE_SIZE;SQ_INSTS_VALU GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS" \
+    bash scripts/gpu_pmc.sh || exit 1
+OUT="${OUT:-r4y}/cfgs" STEPS=20 WARMUP=5 bash scripts/gpu_configs.sh || exit 1
+timeout -k 10 300 python bench.py --with-mlp --steps 10 --warmup 3 --cpu-baseline off > "$O/bench_mlp.log" 2>&1 \
+    || { tail -20 "$O/bench_mlp.log"; exit 1; }
+tail -1 "$O/bench_mlp.log" | cut -c1-300
+echo part2-done
