@@ -1213,10 +1213,10 @@ static int mlp_train_backward(int64_t P, const gsd::MlpHeadsIn& gin, const float
         gsd::launch_mlp_gemm(g, gsd::kMlpBwdMask, s);
     };
     (void)chunks;
-    // GSD_MLP_BWD=chain: the fused dX chain (k_mlp_bwd_chain) instead of the layer-by-layer dX GEMMs
+    // GSD_MLP_BWD=gemm: the layer-by-layer dX GEMMs (k_mlp_gemm_dma) instead of the fused chain, for comparison
     static const bool chain = [] {
         const char* e = getenv("GSD_MLP_BWD");
-        return e && strcmp(e, "chain") == 0;
+        return !(e && strcmp(e, "gemm") == 0);
     }();
     if (chain) {
         timed(kMlpTrainBwd, s, [&] {

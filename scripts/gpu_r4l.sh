@@ -2,7 +2,6 @@
 # Round 4: MLP kernel iteration -- the MLP GPU tests, then the kernel statistics of scripts/mlp_ablate.py (P = 1M).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; export TMPDIR=/tmp
-export GSD_MLP_BWD=${GSD_MLP_BWD:-chain}
 O="gpurun_out/${OUT:-r4l}"; mkdir -p "$O"
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_mlp.py \
     > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
