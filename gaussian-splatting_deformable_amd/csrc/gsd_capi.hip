@@ -953,6 +953,7 @@ struct MlpWs {
     void* ffrag[9];   // forward A = W
     void* bfrag[9];   // backward A = W^T
     void* cfrag[8];   // the backward chain's W^T in the accumulator k order: layers 1-7 (layer 5: rows 64-319), [0]: W0^T's enc(x) rows
+    void* cfrag_e5;   // W5^T's enc(x) rows, accumulator k order
     float* bias_heads;
     float *E, *ET, *H[9];   // H[1..8]: the hidden layers' outputs
     float *Gh, *ga, *gb, *dE;
@@ -974,6 +975,7 @@ size_t carve_mlp(void* base, int64_t P, MlpWs* w) {
     for (int l = 0; l < 9; ++l) v.ffrag[l] = take(mlp_frag_bytes(kMlpOut[l], kMlpIn[l]));
     for (int l = 0; l < 9; ++l) v.bfrag[l] = take(mlp_frag_bytes(kMlpIn[l], kMlpOut[l]));
     for (int l = 0; l < 8; ++l) v.cfrag[l] = take(mlp_frag_bytes(l == 0 ? 64 : 256, 256));
+    v.cfrag_e5 = take(mlp_frag_bytes(64, 256));
     v.bias_heads = reinterpret_cast<float*>(take(64 * sizeof(float)));
     v.E = reinterpret_cast<float*>(take(64 * row));
     v.ET = reinterpret_cast<float*>(take(32 * row));
@@ -1028,8 +1030,7 @@ void mlp_pack_all(float* const* weights, const MlpWs& ws, bool backward, bool fu
         gsd::launch_mlp_pack(pp, s);
     }
 }
-// the backward chain's W^T packs (k_mlp_bwd_chain) and the two natural-order ones it still needs: W8^T (its first
-// step) and W5^T (the enc(x) rows' GEMM of g5)
+// the backward chain's W^T packs (k_mlp_bwd_chain) and the natural-order W8^T of its first step
 void mlp_pack_chain(float* const* weights, const MlpWs& ws, hipStream_t s) {
     for (int l = 0; l < 8; ++l) {
         gsd::MlpPackParams pp{};
@@ -1042,7 +1043,17 @@ void mlp_pack_chain(float* const* weights, const MlpWs& ws, hipStream_t s) {
         pp.out = ws.cfrag[l];
         gsd::launch_mlp_pack(pp, s);
     }
-    for (int l : {5, 8}) {
+    {   // W5^T's enc(x) rows for the chain's layer-5 pass
+        gsd::MlpPackParams pp{};
+        pp.w = mlp_weight(5, weights);
+        pp.transpose = 1;
+        pp.perm_from = 0;
+        pp.M = 64;
+        pp.K = 256;
+        pp.out = ws.cfrag_e5;
+        gsd::launch_mlp_pack(pp, s);
+    }
+    for (int l : {8}) {
         gsd::MlpPackParams pp{};
         pp.perm_from = 1 << 30;
         pp.w = mlp_weight(l, weights);
@@ -1228,17 +1239,12 @@ static int mlp_train_backward(int64_t P, const gsd::MlpHeadsIn& gin, const float
             c.frags[0] = ws.bfrag[8];
             for (int i = 1; i < 8; ++i) c.frags[i] = ws.cfrag[8 - i];
             c.frags_e = ws.cfrag[0];
+            c.frags_e5 = ws.cfrag_e5;
             for (int i = 0; i < 8; ++i) c.bits[i] = ws.bits[8 - i];
             for (int i = 0; i < 9; ++i) c.G[i] = ws.G[i];
             c.dE = ws.dE;
             gsd::launch_mlp_bwd_chain(c, s);
-            if (dx) {   // d enc(x) += W5^T[enc(x) rows] g5
-                gsd::MlpGemmParams g{};
-                g.P = (int)P; g.ldp = ldp; g.src0 = ws.G[3]; g.ks0 = 16; g.frags = ws.bfrag[5]; g.rb = kMlpIn[5] / 32;
-                g.rb_launch = 2; g.n_a = 64; g.dst_a = ws.dE; g.accumulate_a = 1;
-                gsd::launch_mlp_gemm(g, gsd::kMlpBwdMask, s);
-                gsd::launch_mlp_encode_bwd((int)P, ldp, ws.E, ws.dE, dx, dx_accumulate, s);
-            }
+            if (dx) gsd::launch_mlp_encode_bwd((int)P, ldp, ws.E, ws.dE, dx, dx_accumulate, s);
             wgrad(8, ws.G[0], 2, ws.H[8], nullptr, 8, 8);
             for (int l = 7; l >= 0; --l) {
                 const float* g = ws.G[8 - l];

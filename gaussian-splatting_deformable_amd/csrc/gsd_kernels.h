@@ -359,12 +359,13 @@ struct MlpFusedParams {
 // The backward's dX chain (k_mlp_bwd_chain): step i = layer 8 - i multiplies W^T by g_{8-i} (frags[i]: W8^T natural
 // k order, K = 64; then W7^T .. W1^T in the accumulator order, layer 5's rows 64-319), masks by the forward's ReLU
 // words of h_{8-i} (bits[i]) and stores its input g_{8-i} to G[i] (G[0]: [64][ldp], the rest [256][ldp]); the final
-// step stores g0 to G[8] and W0^T's enc(x) rows times g0 to dE ([64][ldp]).
+// step stores g0 to G[8] and the encoding's gradient W5^T[enc rows] g5 + W0^T[enc rows] g0 to dE ([64][ldp]).
 struct MlpChainParams {
     int P, ldp;
     MlpHeadsIn heads;                 // the heads' incoming gradients
     const void* frags[8];
     const void* frags_e;              // W0^T rows 0-63 (accumulator order, K = 256)
+    const void* frags_e5;             // W5^T rows 0-63 (the enc(x) rows of the skip layer; accumulator order)
     const unsigned short* bits[8];
     float* G[9];
     float* dE;

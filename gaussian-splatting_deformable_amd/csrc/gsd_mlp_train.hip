@@ -839,6 +839,49 @@ __device__ __forceinline__ void chain_mask(const unsigned (&w)[4], const f32x16 
             act[2 * rb + (q >> 3)][q & 7] = (w[rb >> 1] >> (16 * (rb & 1) + q)) & 1u ? acc[rb][q] : 0.f;
 }
 
+// W^T's 64 enc(x) rows (2 row blocks, accumulator k order, K = 256) times the B operand in act, on a ring of its
+// own (s_e: four 8-KB slots; waves 0 and 1 copy two chunks per k-step, 2 and 3 one and re-copy chunk 0 into the
+// padding).  Its copies are younger than everything in flight, so its first wait also retires the main ring's
+// prefetched k-steps and the stores before it (once per workgroup); the counted waits after it over-wait by its
+// copies, never under-wait.  No stores: act's rows go out with the chain step that uses it.
+__device__ __forceinline__ void enc_pass(const void* frags, unsigned char* s_e, int wave, int lane,
+                                         const float (&act)[16][8], f32x16 (&ho)[2]) {
+    const bf16x8* fe = reinterpret_cast<const bf16x8*>(frags) + lane;
+#define GSD_E5_ISSUE(KS)                                                                                       \
+    do {                                                                                                       \
+        const int k_ = min((KS), 15);                                                                          \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                                     \
+            const int ch_ = wave + 4 * i_;                                                                     \
+            dma16_asm(fe + k_ * (2 * 3 * 64) + (ch_ < 6 ? ch_ : 0) * 64,                                       \
+                      __builtin_amdgcn_readfirstlane(lds_addr(s_e) + ((KS) & 3) * (8 * 1024) + ch_ * 1024));     \
+        }                                                                                                      \
+    } while (0)
+    ho[0] = f32x16{};
+    ho[1] = f32x16{};
+    GSD_E5_ISSUE(0);
+    GSD_E5_ISSUE(1);
+    GSD_E5_ISSUE(2);
+    wait_vm_c<4>();
+    raw_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+        GSD_E5_ISSUE(ks + 3);
+        const Split8 b = split8(act[ks]);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_e + (ks & 3) * (8 * 1024));
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            Split8 a;
+            a.hi = sa[(r * 3) * 64 + lane];
+            a.mid = sa[(r * 3 + 1) * 64 + lane];
+            a.lo = sa[(r * 3 + 2) * 64 + lane];
+            ho[r] = mfma_x6(a, b, ho[r]);
+        }
+        wait_vm_c<4>();   // stage ks + 1 landed; ks + 2 and ks + 3 (two copies each) stay in flight
+        raw_barrier();
+    }
+#undef GSD_E5_ISSUE
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_bwd_chain(MlpChainParams p) {
     __shared__ __attribute__((aligned(16))) unsigned char s_mem[4 * 24 * 1024];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
@@ -848,6 +891,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     const unsigned voff_a = (unsigned)(4 * h) * (unsigned)ldp + (unsigned)g;   // accumulator order: row 4 h
     // the mask words of every step (two 16-bit words per 32-bit word), each lane's own: registers would not fit
     __shared__ uint4 s_w[8][256];
+    // the ring of the layer-5 enc(x) pass (W5^T's rows 0-63 times g5): 6 chunks of 1 KB per k-step in 8-KB slots
+    __shared__ __attribute__((aligned(16))) unsigned char s_e5[4 * 8 * 1024];
     float act[16][8];
     f32x16 acc[8];
     // g8, natural order: act[ks][j] = row 16 ks + 8 h + j of the heads' gradient (58 rows; zero past them and P)
@@ -902,17 +947,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     };
     chain_step<4, true, false, 0>(F[0], F[1], p.G[0], voff_n, ldp, s_mem, 0, wave, lane, act, acc);
     mask(0);
+    // steps 1-6 (layers 7 .. 2); before step 3 (layer 5), act = g5: W5^T's enc(x) rows times g5 -> dE (added to at
+    // the end; held in registers that long, it spilled)
 #pragma unroll 1
-    for (int i = 1; i < 7; ++i) {
+    for (int i = 1; i < 3; ++i) {
+        chain_step<16, false, false, 1>(F[i], F[i + 1], p.G[i], voff_a, ldp, s_mem, 4 + 16 * (i - 1), wave, lane, act,
+                                        acc);
+        mask(i);
+    }
+    {
+        f32x16 he[2];
+        enc_pass(p.frags_e5, s_e5, wave, lane, act, he);
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) p.dE[(size_t)(32 * r + 8 * (q >> 2) + 4 * h + (q & 3)) * ldp + g] = he[r][q];
+    }
+#pragma unroll 1
+    for (int i = 3; i < 7; ++i) {
         chain_step<16, false, false, 1>(F[i], F[i + 1], p.G[i], voff_a, ldp, s_mem, 4 + 16 * (i - 1), wave, lane, act,
                                         acc);
         mask(i);
     }
     chain_step<16, false, true, 1>(F[7], F[7], p.G[7], voff_a, ldp, s_mem, 4 + 16 * 6, wave, lane, act, acc);
     mask(7);   // g0
-    // the final step: W0^T's enc(x) rows (two row blocks) times g0, g0's rows stored under it.  Its own ring over the
-    // same LDS (6 chunks of 1 KB per k-step in 8-KB slots; waves 0 and 1 copy two chunks, 2 and 3 one and re-copy
-    // chunk 0 into the padding), after everything in flight has retired
+    // the final step: W0^T's enc(x) rows (two row blocks) times g0, added to the layer-5 part in dE; g0's rows
+    // stored under it.  Its own ring over the same LDS (6 chunks of 1 KB per k-step in 8-KB slots; waves 0 and 1 copy
+    // two chunks, 2 and 3 one and re-copy chunk 0 into the padding), after everything in flight has retired
+    f32x16 ho[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) ho[r][q] = p.dE[(size_t)(32 * r + 8 * (q >> 2) + 4 * h + (q & 3)) * ldp + g];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier();
     const bf16x8* fe = reinterpret_cast<const bf16x8*>(p.frags_e) + lane;
@@ -925,7 +991,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
                       __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (8 * 1024) + ch_ * 1024));   \
         }                                                                                                      \
     } while (0)
-    f32x16 ho[2] = {f32x16{}, f32x16{}};
     GSD_E_ISSUE(0);
     GSD_E_ISSUE(1);
     GSD_E_ISSUE(2);
