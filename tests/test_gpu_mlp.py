@@ -321,3 +321,49 @@ def test_train_f32_nan_and_autograd_contracts():
     with torch.no_grad():
         _, names = _launched(lambda: net2(x, t, 5000))
     assert "deform_mlp_train_fwd" not in names
+
+
+def test_train_f32_inplace_gradients_and_unused_heads():
+    """The ABI-15 boundary of the training call (gsd_deform_mlp_train_forward_heads / _backward_heads): (1) heads the
+    loss does not use reach the backward as None (autograd's unmaterialised gradients) and are read as zero -- bit
+    for bit the gradients of the same loss with those heads weighted by explicit zeros; (2) parameters (and x) in a
+    FlatGrads get their gradients written into their views -- stored while the views are stale, bit for bit the
+    plain-autograd gradients; added on a second backward without an invalidate: exactly twice them."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    from gsd_amd.parallel import FlatGrads
+    torch.manual_seed(11)
+    net = DirectTemporalNeRF().cuda()
+    P = 5003
+    x = torch.rand(P, 3, device="cuda") * 4 - 2
+    t = torch.full((P, 1), 0.3, device="cuda")
+    w0, w3 = torch.randn(P, 3, device="cuda"), torch.randn(P, 48, device="cuda")
+
+    def run(explicit_zeros, flat=None):
+        xx = x.clone().requires_grad_(True)
+        if flat is None:
+            net.zero_grad(set_to_none=True)
+        outs, n1 = _launched(lambda: net(xx, t, 5000))
+        loss = (outs[0] * w0).sum() + (outs[3] * w3).sum()
+        if explicit_zeros:
+            loss = loss + (outs[1] * 0.0).sum() + (outs[2] * 0.0).sum()
+        _, n2 = _launched(lambda: loss.backward())
+        assert "deform_mlp_train_fwd" in n1 and "deform_mlp_train_bwd" in n2
+        return xx, [p.grad.clone() for p in net.parameters()]
+
+    xa, ga = run(False)
+    xb, gb = run(True)
+    assert torch.equal(xa.grad, xb.grad) and all(torch.equal(a, b) for a, b in zip(ga, gb))
+    # in place: x's gradient sink is a FlatGrads view as well
+    net.zero_grad(set_to_none=True)
+    xx = x.clone().requires_grad_(True)
+    params = list(net.parameters())
+    flat = FlatGrads(params + [xx])
+    flat.invalidate()
+    outs = net(xx, t, 5000)
+    ((outs[0] * w0).sum() + (outs[3] * w3).sum()).backward()
+    assert torch.equal(xx.grad, xa.grad) and all(torch.equal(p.grad, a) for p, a in zip(params, ga))
+    assert not flat.stale   # every view was claimed by the fused backward
+    outs = net(xx, t, 5000)
+    ((outs[0] * w0).sum() + (outs[3] * w3).sum()).backward()
+    assert torch.equal(xx.grad, 2 * xa.grad) and all(torch.equal(p.grad, 2 * a) for p, a in zip(params, ga))
+    flat.remove_hooks()
