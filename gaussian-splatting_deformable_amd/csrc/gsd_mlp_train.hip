@@ -23,6 +23,7 @@
 //   k_mlp_encode / k_mlp_encode_bwd   enc(x), enc(t) feature-major; dL/dx from dL/d enc(x) through the stored
 //                sin / cos (d sin(2^i x) = 2^i cos(2^i x) dx: no trig in the backward).
 #include <cstdlib>
+#include <cstring>
 
 #include "gsd_kernels.h"
 
@@ -1037,7 +1038,7 @@ constexpr int kWgSlots = 7;
 template <int NRB, int KRB, int TNB, int TKB>
 struct WgradShape {
     static constexpr int TN = NRB / TNB, TK = KRB / TKB, WAVES = TN * TK;
-    static_assert(TN * TNB == NRB && TK * TKB == KRB && WAVES <= 8, "wgrad tiling");
+    static_assert(TN * TNB == NRB && TK * TKB == KRB && WAVES <= 16, "wgrad tiling");
     static constexpr int ROWS = 32 * (NRB + KRB);                       // G rows then X rows
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int RPT = (ROWS + THREADS - 1) / THREADS;          // rows staged per thread
@@ -1066,7 +1067,8 @@ __device__ __forceinline__ void stage_row(const float (&raw)[16], int p0, int P,
 
 template <int NRB, int KRB, int TNB, int TKB>
 __global__ __launch_bounds__(64 * ((NRB / TNB) * (KRB / TKB)))
-__attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void k_mlp_wgrad(MlpWgradParams p) {
+__attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 8 ? 4 : ((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))))
+void k_mlp_wgrad(MlpWgradParams p) {
     typedef WgradShape<NRB, KRB, TNB, TKB> S;
     __shared__ bf16x8 s_op[2][S::ROWS][kWgSlots];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
@@ -1090,7 +1092,7 @@ __attribute__((amdgpu_waves_per_eu((NRB / TNB) * (KRB / TKB) > 4 ? 2 : 1))) void
     // is staged while step s multiplies.
     // (One row per thread only: with more, e.g. layer 5's 576 rows on 256 threads, the pair of steps in registers
     // spills, so those shapes keep one 16-Gaussian segment per row and step, loaded two steps ahead.)
-    constexpr bool kWide = S::RPT == 1;
+    constexpr bool kWide = S::RPT == 1 && S::WAVES <= 8;
     constexpr int kWid = kWide ? 32 : 16;
     float raw[S::RPT][kWid];
     auto load_into = [&](float (&dst)[S::RPT][kWid], int p0) {
@@ -1287,7 +1289,18 @@ void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const Ml
     // eight waves of half-size tiles, two per SIMD (8 x 8 at P = 1M: 0.92 ms per layer against 1.18 for four waves of
     // 4 x 4 blocks, one per SIMD: the second wave per SIMD hides the staging waits)
     // (layer 5's 320 columns run as two calls, 64 + 256, both on the wide-load 8-wave shapes: 1.47 ms as one call)
-    GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 2, 2, 1) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 3)
+    // 256 x 256: sixteen waves of 2 x 2 blocks (four per SIMD, 128 registers, 16-Gaussian loads) -- 0.73 ms per
+    // layer at 1M against 0.76 for eight waves of 4 x 2 (two per SIMD, 216 registers, 32-Gaussian loads), which
+    // GSD_WGRAD16=0 keeps
+    static const bool w16 = [] {
+        const char* e = getenv("GSD_WGRAD16");
+        return !(e && strcmp(e, "0") == 0);
+    }();
+    // (the narrow shapes with three or four waves per SIMD were slower: 64 x 256 as 16 waves of one block 0.40 ms
+    // against 0.30, 256 x 96 as 12 waves of 2 x 1 blocks 0.45 against 0.43)
+    if (w16 && p.n_rb == 8 && p.k_rb == 8)
+        hipLaunchKernelGGL((k_mlp_wgrad<8, 8, 2, 2>), grid, dim3(64 * WgradShape<8, 8, 2, 2>::WAVES), 0, s, p);
+    else GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 2, 2, 1) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 3)
     else GSD_WGRAD(2, 8, 1, 2)
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
