@@ -1019,21 +1019,23 @@ gsd::MlpWeightRef mlp_weight(int l, float* const* w, int ldw_override = -1) {
 // fused: the forward's weights for k_mlp_fwd_fused, whose B operands past the encoding are the layer before's
 // accumulators (the accumulator-order k permutation: layer 0 none, layer 5 from k-step 4, the rest from 0)
 void mlp_pack_all(float* const* weights, const MlpWs& ws, bool backward, bool fused, hipStream_t s) {
+    gsd::MlpPackBatch b{};
     for (int l = 0; l < 9; ++l) {
-        gsd::MlpPackParams pp{};
+        gsd::MlpPackParams& pp = b.job[b.n++];
         pp.perm_from = !fused || l == 0 ? 1 << 30 : (l == 5 ? 4 : 0);
         pp.w = mlp_weight(l, weights);
         pp.transpose = backward ? 1 : 0;
         pp.M = backward ? kMlpIn[l] : kMlpOut[l];
         pp.K = backward ? kMlpOut[l] : kMlpIn[l];
         pp.out = backward ? ws.bfrag[l] : ws.ffrag[l];
-        gsd::launch_mlp_pack(pp, s);
     }
+    gsd::launch_mlp_pack_batch(b, s);
 }
 // the backward chain's W^T packs (k_mlp_bwd_chain) and the natural-order W8^T of its first step
 void mlp_pack_chain(float* const* weights, const MlpWs& ws, hipStream_t s) {
+    gsd::MlpPackBatch b{};
     for (int l = 0; l < 8; ++l) {
-        gsd::MlpPackParams pp{};
+        gsd::MlpPackParams& pp = b.job[b.n++];
         pp.w = mlp_weight(l, weights);
         pp.transpose = 1;
         pp.perm_from = 0;
@@ -1041,28 +1043,26 @@ void mlp_pack_chain(float* const* weights, const MlpWs& ws, hipStream_t s) {
         pp.m_off = l == 5 ? 64 : 0;
         pp.K = 256;
         pp.out = ws.cfrag[l];
-        gsd::launch_mlp_pack(pp, s);
     }
     {   // W5^T's enc(x) rows for the chain's layer-5 pass
-        gsd::MlpPackParams pp{};
+        gsd::MlpPackParams& pp = b.job[b.n++];
         pp.w = mlp_weight(5, weights);
         pp.transpose = 1;
         pp.perm_from = 0;
         pp.M = 64;
         pp.K = 256;
         pp.out = ws.cfrag_e5;
-        gsd::launch_mlp_pack(pp, s);
     }
     for (int l : {8}) {
-        gsd::MlpPackParams pp{};
+        gsd::MlpPackParams& pp = b.job[b.n++];
         pp.perm_from = 1 << 30;
         pp.w = mlp_weight(l, weights);
         pp.transpose = 1;
         pp.M = kMlpIn[l];
         pp.K = kMlpOut[l];
         pp.out = ws.bfrag[l];
-        gsd::launch_mlp_pack(pp, s);
     }
+    gsd::launch_mlp_pack_batch(b, s);
 }
 }  // namespace
 extern "C" {

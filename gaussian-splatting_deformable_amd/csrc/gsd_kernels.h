@@ -324,6 +324,11 @@ struct MlpPackParams {
     int perm_from;
     int m_off;             // transpose: A row m is W^T row m + m_off (layer 5's h rows for the backward chain)
 };
+struct MlpPackBatch {   // up to 12 packs in one launch
+    MlpPackParams job[12];
+    int n;
+};
+void launch_mlp_pack_batch(const MlpPackBatch& b, hipStream_t s);
 // The layer-fused training forward (k_mlp_fwd_fused): the encoding in, every hidden layer's output, its ReLU words
 // and the heads out; the weights packed with the accumulator-order k permutation (perm_from 0; layer 5: 4; layer 0:
 // natural).

@@ -22,6 +22,7 @@
 //                bias gradient's row sums of g; k_mlp_wgrad_reduce sums the partials in a fixed order.
 //   k_mlp_encode / k_mlp_encode_bwd   enc(x), enc(t) feature-major; dL/dx from dL/d enc(x) through the stored
 //                sin / cos (d sin(2^i x) = 2^i cos(2^i x) dx: no trig in the backward).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -97,8 +98,13 @@ __device__ __forceinline__ float* mlp_elem(const MlpWeightRef& w, int row, int c
 
 // ---- weight packing: A[m][k] of a layer (W or W^T, zero-padded, input columns mapped) into split fragments ----
 // out[((ks * RB + rb) * 3 + s) * 64 + lane] = split s of A[32 rb + (lane & 31)][16 ks + 8 (lane >> 5) + 0..7]
-__global__ __launch_bounds__(256) void k_mlp_pack(MlpPackParams p) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void mlp_pack_one(const MlpPackParams& p, int t);
+__global__ __launch_bounds__(256) void k_mlp_pack(MlpPackParams p) { mlp_pack_one(p, blockIdx.x * 256 + threadIdx.x); }
+// several packs in one launch (grid.y = the job): one launch per direction instead of nine or ten ~6-us ones
+__global__ __launch_bounds__(256) void k_mlp_pack_multi(MlpPackBatch b) {
+    if ((int)blockIdx.y < b.n) mlp_pack_one(b.job[blockIdx.y], blockIdx.x * 256 + threadIdx.x);
+}
+__device__ __forceinline__ void mlp_pack_one(const MlpPackParams& p, int t) {
     const int RB = p.M / 32, KS = p.K / 16;
     if (t >= KS * RB * 64) return;
     const int lane = t & 63, rb = (t >> 6) % RB, ks = (t >> 6) / RB;
@@ -1204,23 +1210,32 @@ void k_mlp_wgrad(MlpWgradParams p) {
 }
 
 // dW[n][k] = sum over the chunks of partial[chunk][n][k], in a fixed order (deterministic), scattered into the
-// reference-shaped pieces (padded columns and rows dropped); the bias gradient likewise (k_cols = 1).  A workgroup
-// owns 32 consecutive outputs; its 8 thread groups sum the chunks c = g, g + 8, ... (loads four chunks ahead) and
-// the 8 group sums are combined in group order through LDS.
-__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_rows, int k_cols, int k_off,
-                                                          const float* __restrict__ partial, MlpWeightRef dst,
-                                                          int accumulate) {
+// reference-shaped pieces (padded columns and rows dropped); in the same launch the bias gradient likewise (the first
+// b_blocks workgroups, dispatched first: eight workgroups, each a 489-deep chain of loads, took ~9.5 us in a launch
+// of their own, and as the last blocks of this one they ran after the weights' instead of beside).  A workgroup
+// owns 32 consecutive outputs; its 8 thread groups sum the chunks c = g, g + 8, ... (loads four chunks ahead) and the
+// 8 group sums are combined in group order through LDS.
+struct WgradReduceJob {
+    int n_rows, k_cols, k_off;
+    const float* partial;
+    MlpWeightRef dst;
+};
+__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, WgradReduceJob w, WgradReduceJob b,
+                                                          int b_blocks, int accumulate) {
     __shared__ float red[8][32];
-    const long long n_el = (long long)n_rows * k_cols;
+    const bool is_w = (int)blockIdx.x >= b_blocks;
+    const WgradReduceJob& j = is_w ? w : b;
+    const long long n_el = (long long)j.n_rows * j.k_cols;
     const int grp = threadIdx.x >> 5, l = threadIdx.x & 31;
-    const long long e = (long long)blockIdx.x * 32 + l;
+    const long long e = (long long)(is_w ? blockIdx.x - b_blocks : blockIdx.x) * 32 + l;
+    const float* __restrict__ partial = j.partial;
     float s = 0.f;
     if (e < n_el) {
         int c = grp;
         for (; c + 24 < n_chunks; c += 32) {
-            const float a = partial[(size_t)c * n_el + e], b = partial[(size_t)(c + 8) * n_el + e];
+            const float a = partial[(size_t)c * n_el + e], bb = partial[(size_t)(c + 8) * n_el + e];
             const float d = partial[(size_t)(c + 16) * n_el + e], f = partial[(size_t)(c + 24) * n_el + e];
-            s += a; s += b; s += d; s += f;
+            s += a; s += bb; s += d; s += f;
         }
         for (; c < n_chunks; c += 8) s += partial[(size_t)c * n_el + e];
     }
@@ -1230,8 +1245,8 @@ __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_ro
         float t = red[0][l];
 #pragma unroll
         for (int g = 1; g < 8; ++g) t += red[g][l];
-        const int n = (int)(e / k_cols), k = (int)(e - (long long)n * k_cols);
-        float* d = mlp_elem(dst, n, mlp_col(dst.map, k_off + k));
+        const int n = (int)(e / j.k_cols), k = (int)(e - (long long)n * j.k_cols);
+        float* d = mlp_elem(j.dst, n, mlp_col(j.dst.map, j.k_off + k));
         if (d) *d = accumulate ? *d + t : t;
     }
 }
@@ -1239,6 +1254,11 @@ __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, int n_ro
 void launch_mlp_pack(const MlpPackParams& p, hipStream_t s) {
     const int n = (p.K / 16) * (p.M / 32) * 64;
     hipLaunchKernelGGL(k_mlp_pack, dim3((n + 255) / 256), dim3(256), 0, s, p);
+}
+void launch_mlp_pack_batch(const MlpPackBatch& b, hipStream_t s) {
+    int n = 0;
+    for (int i = 0; i < b.n; ++i) n = std::max(n, (b.job[i].K / 16) * (b.job[i].M / 32) * 64);
+    if (b.n > 0) hipLaunchKernelGGL(k_mlp_pack_multi, dim3((n + 255) / 256, b.n), dim3(256), 0, s, b);
 }
 
 void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E, float* ET, hipStream_t s) {
@@ -1304,11 +1324,11 @@ void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const Ml
     else GSD_WGRAD(2, 8, 1, 2)
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
-    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)((nw + 31) / 32)), dim3(256), 0, s, n_chunks, 32 * p.n_rb,
-                       32 * p.k_rb, p.k_off, (const float*)p.partial, dst, p.accumulate);
-    if (!p.skip_bias)
-        hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((32 * p.n_rb + 31) / 32), dim3(256), 0, s, n_chunks, 32 * p.n_rb, 1,
-                           0, (const float*)p.bias_partial, dst_b, p.accumulate);
+    const int w_blocks = (int)((nw + 31) / 32), b_blocks = p.skip_bias ? 0 : (32 * p.n_rb + 31) / 32;
+    const WgradReduceJob wj{32 * p.n_rb, 32 * p.k_rb, p.k_off, (const float*)p.partial, dst};
+    const WgradReduceJob bj{32 * p.n_rb, 1, 0, (const float*)p.bias_partial, dst_b};
+    hipLaunchKernelGGL(k_mlp_wgrad_reduce, dim3((unsigned)(w_blocks + b_blocks)), dim3(256), 0, s, n_chunks, wj, bj,
+                       b_blocks, p.accumulate);
 }
 
 void launch_mlp_rows_to_features(int P, int ldp, const MlpHeadsIn& src, float* dst, int dst_rows, hipStream_t s) {
