@@ -12,6 +12,8 @@
 // tile is exactly ascending (depth bits, id) -- a total order on unique keys,
 // so this produces the identical point_list.  HBM traffic: ~8 B (scatter) +
 // 8 B read + 4 B write (sort) per instance, vs ~150 B for 6 global passes.
+#include <type_traits>
+
 #include "gsd_kernels.h"
 
 namespace gsd {
@@ -361,8 +363,23 @@ __device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n
         const int e = t * E + r;
         x[r] = e < n ? src[e] : ~0ull;
     }
+    // a pass inside the thread, its distance J a compile-time constant: x[r | J] a register, not a scratch access
+    // (with a run-time j the looped E = 8 / 16 networks kept x in scratch memory)
+    auto intra = [&](auto jc, int k) {
+        constexpr int J = decltype(jc)::value;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            if ((r & J) == 0) {
+                const bool asc = (((t * E + r) & k) == 0);
+                const unsigned long long a = x[r], b = x[r | J];
+                const bool swap = (b < a) == asc;
+                x[r] = swap ? b : a;
+                x[r | J] = swap ? a : b;
+            }
+        }
+    };
     auto pass = [&](int k, int j) {
-        if (j < E) {
+        if (E == 16 && j < E) {   // (the 4096-key network keeps the looped form: its registers would cut occupancy)
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 if ((r & j) == 0) {
@@ -373,6 +390,11 @@ __device__ void sort_tile_regs(const unsigned long long* __restrict__ src, int n
                     x[r | j] = swap ? a : b;
                 }
             }
+        } else if (j < E) {
+            if (j == 1) intra(std::integral_constant<int, 1>{}, k);
+            if constexpr (E > 2) if (j == 2) intra(std::integral_constant<int, 2>{}, k);
+            if constexpr (E > 4) if (j == 4) intra(std::integral_constant<int, 4>{}, k);
+            if constexpr (E > 8) if (j == 8) intra(std::integral_constant<int, 8>{}, k);
         } else {
             const bool lds = j >= 64 * E;
             if (lds) {

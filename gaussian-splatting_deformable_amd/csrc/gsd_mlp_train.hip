@@ -1220,14 +1220,11 @@ struct WgradReduceJob {
     const float* partial;
     MlpWeightRef dst;
 };
-__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, WgradReduceJob w, WgradReduceJob b,
-                                                          int b_blocks, int accumulate) {
-    __shared__ float red[8][32];
-    const bool is_w = (int)blockIdx.x >= b_blocks;
-    const WgradReduceJob& j = is_w ? w : b;
+__device__ __forceinline__ void wgrad_reduce_block(int n_chunks, const WgradReduceJob& j, int blk, int accumulate,
+                                                   float (*red)[32]) {
     const long long n_el = (long long)j.n_rows * j.k_cols;
     const int grp = threadIdx.x >> 5, l = threadIdx.x & 31;
-    const long long e = (long long)(is_w ? blockIdx.x - b_blocks : blockIdx.x) * 32 + l;
+    const long long e = (long long)blk * 32 + l;
     const float* __restrict__ partial = j.partial;
     float s = 0.f;
     if (e < n_el) {
@@ -1249,6 +1246,13 @@ __global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, WgradRed
         float* d = mlp_elem(j.dst, n, mlp_col(j.dst.map, j.k_off + k));
         if (d) *d = accumulate ? *d + t : t;
     }
+}
+// (two call sites on the kernel arguments themselves: a selected reference to one of them put the job in scratch)
+__global__ __launch_bounds__(256) void k_mlp_wgrad_reduce(int n_chunks, WgradReduceJob w, WgradReduceJob b,
+                                                          int b_blocks, int accumulate) {
+    __shared__ float red[8][32];
+    if ((int)blockIdx.x < b_blocks) wgrad_reduce_block(n_chunks, b, blockIdx.x, accumulate, red);
+    else wgrad_reduce_block(n_chunks, w, blockIdx.x - b_blocks, accumulate, red);
 }
 
 void launch_mlp_pack(const MlpPackParams& p, hipStream_t s) {
