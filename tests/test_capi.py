@@ -96,3 +96,25 @@ def test_argument_errors_without_gpu():
     a.P = 0
     assert lib.gsd_rasterize_forward_bin(ctypes.byref(a), None, None, None, ctypes.byref(K), None) == 0
     assert K.value == 0
+
+
+def test_mlp_training_heads_argument_errors_without_gpu():
+    """The ABI-15 head-wise training entry points validate before any device work: a null head-pointer array, a
+    null head output, and (backward) null gradient sinks fail with GSD_ERR_ARG and a message; a NULL head GRADIENT
+    is legal (a zero gradient) and never reaches that check."""
+    from gsd_amd import _native
+    lib = _native.load()
+    vp = ctypes.c_void_p
+    W = (vp * 12)(*([8] * 12))
+    heads = (vp * 4)(8, 8, None, 8)
+    rc = lib.gsd_deform_mlp_train_forward_heads(10, 8, 8, W, W, 8, None, None)
+    assert rc == 1 and b"null pointer" in lib.gsd_last_error()
+    rc = lib.gsd_deform_mlp_train_forward_heads(10, 8, 8, W, W, 8, heads, None)
+    assert rc == 1 and b"4 head outputs" in lib.gsd_last_error()
+    rc = lib.gsd_deform_mlp_train_backward_heads(10, None, W, 8, 8, 0, W, W, 0, None)
+    assert rc == 1 and b"null pointer" in lib.gsd_last_error()
+    dW = (vp * 12)(*([8] * 11 + [None]))
+    rc = lib.gsd_deform_mlp_train_backward_heads(10, heads, W, 8, 8, 0, dW, W, 0, None)
+    assert rc == 1 and b"weight / bias gradients" in lib.gsd_last_error()
+    rc = lib.gsd_deform_mlp_train_backward_heads(0, heads, W, 8, 8, 0, W, W, 0, None)
+    assert rc == 1 and b"0 < P" in lib.gsd_last_error()
