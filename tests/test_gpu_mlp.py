@@ -214,7 +214,8 @@ def _train_run(net, x, t, w, torch_path):
     return torch.cat(outs, -1).detach(), [xx.grad] + [p.grad for p in net.parameters()]
 
 
-@pytest.mark.parametrize("P,scale", [(1, 2.0), (77, 2.0), (5003, 1.0), (5003, 2.0), (70_001, 1.0)])
+@pytest.mark.parametrize("P,scale", [(1, 2.0), (77, 2.0), (128, 1.0), (257, 2.0), (5003, 1.0), (5003, 2.0),
+                                     (70_001, 1.0)])
 def test_train_f32_matches_float64_oracle_like_torch_f32(P, scale):
     """The f32 training path (gsd_mlp_train.hip: BF16x6 GEMMs, forward and backward) against the float64
     restatement of DirectTemporalNeRF (oracle/deform_mlp_ref.py) and its float64 autograd, side by side with the
