@@ -31,6 +31,13 @@ constexpr int kSsimHalo = 5;                         // window radius
 constexpr int kSsimIn = kSsimTile + 2 * kSsimHalo;   // 42: staged edge
 constexpr int kSsimThreads = 256;
 constexpr int kSsimRows = kSsimTile * kSsimTile / kSsimThreads;  // 4 output rows per thread (one column)
+#ifndef GSD_SSIM_FWD_THREADS
+// k_ssim_fwd's workgroup size: 512 threads, two output rows each (54 VGPRs, six waves per SIMD) -- 50.3 us at
+// 1080p against 54.2 for 256 threads with four rows each (146 VGPRs, three waves); profiles/round4/r4k3/
+#define GSD_SSIM_FWD_THREADS 512
+#endif
+constexpr int kSsimFwdThreads = GSD_SSIM_FWD_THREADS;
+constexpr int kSsimFwdRows = kSsimTile * kSsimTile / kSsimFwdThreads;
 
 // 1/d from v_rcp_f32 plus one Newton step (the loss has no bit-exact contract)
 __device__ __forceinline__ float fast_rcp(float d) {
@@ -74,15 +81,17 @@ __device__ __forceinline__ void stage(const float* __restrict__ a, float (*sa)[k
         }
 }
 
-// stage() for the image and the ground truth at once, interleaved as (x, y) pairs
+// stage() for the image and the ground truth at once, interleaved as (x, y) pairs, by NT threads
+template <int NT>
 __device__ __forceinline__ void stage_pair(const float* __restrict__ a, const float* __restrict__ b,
                                            f2 (*sab)[kSsimIn], int H, int W, int ox, int oy) {
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-    constexpr int kRowIt = (kSsimIn + 7) / 8, kColIt = 2;
+    constexpr int kTy = NT / 32;
+    constexpr int kRowIt = (kSsimIn + kTy - 1) / kTy, kColIt = 2;
     f2 v[kRowIt][kColIt];
 #pragma unroll
     for (int i = 0; i < kRowIt; ++i) {
-        const int r = ty + 8 * i, gy = oy - kSsimHalo + r;
+        const int r = ty + kTy * i, gy = oy - kSsimHalo + r;
 #pragma unroll
         for (int j = 0; j < kColIt; ++j) {
             const int c = tx + 32 * j, gx = ox - kSsimHalo + c;
@@ -95,7 +104,7 @@ __device__ __forceinline__ void stage_pair(const float* __restrict__ a, const fl
     for (int i = 0; i < kRowIt; ++i)
 #pragma unroll
         for (int j = 0; j < kColIt; ++j) {
-            const int r = ty + 8 * i, c = tx + 32 * j;
+            const int r = ty + kTy * i, c = tx + 32 * j;
             if (r < kSsimIn && c < kSsimIn) sab[r][c] = v[i][j];
         }
 }
@@ -106,21 +115,23 @@ __device__ __forceinline__ void stage_pair(const float* __restrict__ a, const fl
 // read per tap, stage_pair) 0.0623 ms.  In k_ssim_bwd (three quantities, so one stays scalar) neither helps:
 // packed arithmetic 0.0592 -> 0.0599 ms; (g0, g1) interleaved in LDS 0.0595 -> 0.0600, with the packed vertical
 // pass 0.0606 -- not used there.
-template <int NQ>
+template <int NQ, int R>
 __device__ __forceinline__ void vertical_pass(const SsimArgs& p, const float (*sh)[kSsimIn][kSsimTile], int r0,
-                                              int c, float (&acc)[NQ][kSsimRows]) {
-    static_assert(kSsimRows == 4, "two row pairs per thread");
-    f2 a2[NQ][2];
+                                              int c, float (&acc)[NQ][R]) {
+    static_assert(R % 2 == 0, "row pairs per thread");
+    f2 a2[NQ][R / 2];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) a2[q][0] = a2[q][1] = f2{0.f, 0.f};
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
-    for (int t = 0; t < kSsimRows + 10; ++t) {
+        for (int jp = 0; jp < R / 2; ++jp) a2[q][jp] = f2{0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < R + 10; ++t) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const float h = sh[q][r0 + t][c];
             const f2 hh = {h, h};
 #pragma unroll
-            for (int jp = 0; jp < 2; ++jp) {
+            for (int jp = 0; jp < R / 2; ++jp) {
                 const int m = t - 2 * jp;
                 if (m >= 0 && m <= 11)
                     a2[q][jp] = __builtin_elementwise_fma(f2{p.wp[2 * m], p.wp[2 * m + 1]}, hh, a2[q][jp]);
@@ -128,28 +139,28 @@ __device__ __forceinline__ void vertical_pass(const SsimArgs& p, const float (*s
         }
     }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        acc[q][0] = a2[q][0].x;
-        acc[q][1] = a2[q][0].y;
-        acc[q][2] = a2[q][1].x;
-        acc[q][3] = a2[q][1].y;
-    }
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int jp = 0; jp < R / 2; ++jp) {
+            acc[q][2 * jp] = a2[q][jp].x;
+            acc[q][2 * jp + 1] = a2[q][jp].y;
+        }
 }
 
-__global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const float* __restrict__ img,
+__global__ __launch_bounds__(kSsimFwdThreads) void k_ssim_fwd(SsimArgs p, const float* __restrict__ img,
                                                              const float* __restrict__ gt, float* __restrict__ gmaps,
                                                              float* __restrict__ partial) {
     __shared__ f2 sxy[kSsimIn][kSsimIn];  // (x, y) interleaved: one 8-B LDS read per window tap
     __shared__ float sh[5][kSsimIn][kSsimTile];  // horizontal sums of x, y, x^2, y^2, xy
-    __shared__ float red[2][kSsimThreads / 64];
+    __shared__ float red[2][kSsimFwdThreads / 64];
     const int ch = blockIdx.z;
     const int ox = blockIdx.x * kSsimTile, oy = blockIdx.y * kSsimTile;
     const size_t plane = (size_t)p.H * p.W;
-    stage_pair(img + ch * plane, gt + ch * plane, sxy, p.H, p.W, ox, oy);
+    stage_pair<kSsimFwdThreads>(img + ch * plane, gt + ch * plane, sxy, p.H, p.W, ox, oy);
     __syncthreads();
     // horizontal pass: thread = (column c, row group); no integer division.  (x, y) as one packed pair: w x and
     // w y in one multiply, their sums and the squares' sums in two packed FMAs, xy scalar
-    for (int r = threadIdx.x >> 5; r < kSsimIn; r += kSsimThreads / 32) {
+    for (int r = threadIdx.x >> 5; r < kSsimIn; r += kSsimFwdThreads / 32) {
         const int c = threadIdx.x & 31;
         f2 ab = {0.f, 0.f}, cd = {0.f, 0.f};
         float e = 0.f;
@@ -171,12 +182,12 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
     constexpr float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
     float fsum = 0.f, l1sum = 0.f;
     // vertical pass: thread (c, g) produces rows 4g..4g+3 of column c from 14 staged rows (register reuse)
-    const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimRows;
-    float acc[5][kSsimRows];
-    vertical_pass<5>(p, sh, r0, c, acc);
+    const int c = threadIdx.x & (kSsimTile - 1), r0 = (threadIdx.x >> 5) * kSsimFwdRows;
+    float acc[5][kSsimFwdRows];
+    vertical_pass<5, kSsimFwdRows>(p, sh, r0, c, acc);
     const size_t map = (size_t)p.C * plane;  // gmaps = [dL/dA | dL/dC | dL/dE], each (C,H,W)
 #pragma unroll
-    for (int j = 0; j < kSsimRows; ++j) {
+    for (int j = 0; j < kSsimFwdRows; ++j) {
         const int r = r0 + j, gy = oy + r, gx = ox + c;
         if (gy >= p.H || gx >= p.W) continue;
         const float A = acc[0][j], B = acc[1][j], Cx = acc[2][j], Dy = acc[3][j], E = acc[4][j];
@@ -202,8 +213,14 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_fwd(SsimArgs p, const flo
     __syncthreads();
     if (threadIdx.x == 0) {
         const int blk = (ch * p.tiles_y + blockIdx.y) * p.tiles_x + blockIdx.x;
-        partial[2 * blk] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-        partial[2 * blk + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        float fs = 0.f, ls = 0.f;
+#pragma unroll
+        for (int w = 0; w < kSsimFwdThreads / 64; ++w) {
+            fs += red[0][w];
+            ls += red[1][w];
+        }
+        partial[2 * blk] = fs;
+        partial[2 * blk + 1] = ls;
     }
 }
 
@@ -348,7 +365,7 @@ void launch_l1_ssim(int C, int H, int W, const float* w11, float lambda, const f
     const SsimArgs p = ssim_args(C, H, W, w11, lambda);
     const double n = (double)C * H * W;
     const dim3 grid(p.tiles_x, p.tiles_y, C);
-    hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimThreads), 0, s, p, img, gt, gmaps, partial);
+    hipLaunchKernelGGL(k_ssim_fwd, grid, dim3(kSsimFwdThreads), 0, s, p, img, gt, gmaps, partial);
     hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(kSumThreads), 0, s, p.tiles_x * p.tiles_y * C, partial, (float)(1.0 / n),
                        lambda, out3);
     if (dimg)
