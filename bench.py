@@ -36,6 +36,13 @@ schedule's rate at that iteration).  A separate line (config.workload says "MLP 
 starts ``torch.distributed.run`` with N ranks on this node and exits with its status, before anything touches
 the GPU.  Under a launcher, WORLD_SIZE must equal N; fewer visible devices than ranks is refused unless
 GSD_DIST_BACKEND=gloo (the one-GPU rehearsal).
+
+Failure bound at N > 1 (gsd_amd.parallel.DIST_TIMEOUT_S): a rank that raises prints its traceback and exits with
+status 1 at once (no interpreter teardown of the process groups, which can block on a dead peer), and
+torch.distributed.run then stops the other ranks; a rank that hangs leaves its peers waiting in a collective for
+at most GSD_DIST_TIMEOUT_S (default 120 s: every process group is created with it, and RCCL's watchdog aborts the
+communicator, TORCH_NCCL_ASYNC_ERROR_HANDLING=1).  So the worst case is about 2 minutes plus start-up, not the
+default 10 (RCCL) or 30 (gloo) minutes.
 """
 from __future__ import annotations
 
@@ -621,4 +628,18 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        try:
+            main()
+        except SystemExit as e:   # a rank that stops early must not wait in teardown either
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(e.code if isinstance(e.code, int) else 1)
+        except BaseException:
+            import traceback
+            traceback.print_exc()
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(1)
+    else:
+        main()

@@ -26,7 +26,9 @@ __device__ __forceinline__ float4 alpha_box(float2 xy, float4 co) {
     const float a = co.x, b = co.y, c = co.z, o = co.w;
     const float det = a * c - b * b;
     const float lo = 255.0f * o;
-    if (!(lo >= 0.999f)) return make_float4(1e30f, -1e30f, 1e30f, -1e30f);  // alpha < 1/255 everywhere (or NaN)
+    // a NaN opacity composites at alpha = fminf(0.99, NaN) = 0.99 wherever power <= 0 (forward.cu:343): never cull
+    if (lo != lo) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
+    if (!(lo >= 0.999f)) return make_float4(1e30f, -1e30f, 1e30f, -1e30f);  // alpha < 1/255 everywhere
     if (!(det > 0.0f)) return make_float4(-1e30f, 1e30f, -1e30f, 1e30f); // degenerate: never cull
     const float t = 2.0f * 0.69314718f * __builtin_amdgcn_logf(lo);     // 2 ln(255 o), v_log_f32 = log2
     // hardware sqrt / reciprocal (1 ulp): far inside the 0.1 % inflation
@@ -386,7 +388,6 @@ struct MlpGemmParams {
     const void* frags;              // k_mlp_pack output: [ks][rb][split][lane]
     int rb;                         // output row blocks of 32 (of the packed A)
     int rb_off;                     // launch-internal: first row block of this workgroup row (grid.y)
-    int rb_launch;                  // nonzero: only row blocks 0 .. rb_launch - 1 of the packed A (2 supported)
     const float* bias;              // forward: 32 rb floats
     float* dst;                     // forward hidden: [32 rb][ldp]; backward: g rows
     MlpHeads heads;                 // heads: the four outputs (58 columns)

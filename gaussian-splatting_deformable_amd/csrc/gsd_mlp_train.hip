@@ -1277,10 +1277,6 @@ void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, floa
 // (1.72 ms with all 10 row blocks per workgroup)
 template <int MODE>
 static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
-    if (p.rb_launch == 2) {
-        hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 2>), dim3(p.ldp / 256), dim3(512), 0, s, p);
-        return;
-    }
     switch (p.rb) {   // 320 rows (layer 5's W^T): two workgroup rows of 5 blocks
         case 2: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 2>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;
         case 3: hipLaunchKernelGGL((k_mlp_gemm_dma<MODE, 3>), dim3(p.ldp / 256), dim3(512), 0, s, p); break;

@@ -208,8 +208,11 @@ __global__ __launch_bounds__(256) void k_preprocess_fwd(PreprocessParams p) {
     // (gsd_render.hip record_og) -- and, with slack, the backward's ellipse culling (Q <= -2 t_o); the hardware
     // reciprocals of a and c.  (Rounded up, t_o made the comparison exact at ties too, but biased every alpha VALUE
     // low by up to an ulp of t_o, which the transmittance accumulates: 10 instead of 1 n_contrib flips at cfg4.)
-    rr->q2 = make_float4(col.z, __double2float_rn(-log(255.0 * (double)co.w)), __builtin_amdgcn_rcpf(co.x),
-                         __builtin_amdgcn_rcpf(co.z));
+    // A negative opacity gives alpha = min(0.99, o G) < 1/255 at every pixel (forward.cu:343-345): t_o = +inf takes
+    // no pixel (power >= +inf is false) and culls the record from the backward's lists; -log of a negative would be
+    // NaN, which passes every decision.  A NaN opacity keeps NaN: alpha = fminf(0.99, NaN) = 0.99, as upstream.
+    const double t_o = co.w < 0.f ? INFINITY : -log(255.0 * (double)co.w);
+    rr->q2 = make_float4(col.z, __double2float_rn(t_o), __builtin_amdgcn_rcpf(co.x), __builtin_amdgcn_rcpf(co.z));
     rr->box = alpha_box(pix, co);
     // per-tile instance counts by global atomics -- only on the fallback path for very
     // large tile grids; normally k_tile_hist builds them from LDS histograms instead

@@ -640,11 +640,330 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
 #endif
 }
 
+// Transposed reduction steps inside a 16-lane row.  DPP bank b is lanes 4b .. 4b + 3 of each row, so a bank mask
+// selects by lane bits 3:2, and a DPP move with a partial bank mask writes only those lanes (the others keep
+// `old`).  row_ror:N gives lane l the value of lane (l - N) mod 16.
+// tstep8: lanes with bit 3 clear return a(l) + a(l ^ 8), lanes with bit 3 set b(l) + b(l ^ 8) -- three VALU ops
+// for a pair of quantities, no lane selects.
+__device__ __forceinline__ float tstep8(float a, float b) {
+    const int u = __builtin_amdgcn_update_dpp(__float_as_int(a), __float_as_int(b), 0x128, 0xf, 0xc, false);
+    const int v = __builtin_amdgcn_update_dpp(__float_as_int(b), __float_as_int(a), 0x128, 0xf, 0x3, false);
+    return __int_as_float(u) + __int_as_float(v);
+}
+// tstep4: lanes with bit 2 clear return a(l) + a(l ^ 4), lanes with bit 2 set b(l) + b(l ^ 4): the partner is
+// l - 4 (row_ror:4) for bit 2 set and l + 4 (row_ror:12) for bit 2 clear.
+__device__ __forceinline__ float tstep4(float a, float b) {
+    const int u = __builtin_amdgcn_update_dpp(__float_as_int(a), __float_as_int(b), 0x124, 0xf, 0xa, false);
+    const int v = __builtin_amdgcn_update_dpp(__float_as_int(b), __float_as_int(a), 0x12c, 0xf, 0x5, false);
+    return __int_as_float(u) + __int_as_float(v);
+}
+
+// Backward compaction into one list per 4x4 lane group (the forward's groups, fwd_lane_pixel): lists[g] receives, in
+// increasing slot order, the slots t >= t_min[g] (the group's last-contributor cut) whose alpha box meets group g's
+// block and whose alpha ellipse passes a linear bound over the block: with d the block centre minus the mean and
+// h = 1.5 px the block's half-size, min over the block of Q >= Q(d) - h |grad Q(d)|_1 = Q(d) - 3 (|u| + |v|),
+// (u, v) = (a dx + b dy, b dx + c dy) -- conservative for a positive-definite conic, so a culled record has
+// alpha < 1/255 at every pixel of the block (the same slack as the exact test: 0.1 % + 0.05 on 2 ln(255 o)).
+// Counted on the cfg4 scene (scripts/sim_bwd_lists.py): the wave then walks 0.708 of the per-quadrant lists' steps
+// (the exact ellipse test per block: 0.682, the alpha box alone: 0.817).
+__device__ __forceinline__ void bwd_compact_groups(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
+                                                   const float2* __restrict__ s_bo, uint8_t (*lists)[kTilePix], int n,
+                                                   float qx0, float qy0, int lane, const int (&t_min)[4],
+                                                   int (&cnt)[4]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) cnt[g] = 0;
+#pragma unroll
+    for (int k = 0; k < kTilePix / 64; ++k) {
+        const int t = k * 64 + lane;
+        const bool in = t < n;
+        const float4 bx = s_box[t];  // slots >= n hold stale values: every test below is masked by `in`
+        const float4 pc = s_pc[t];
+        const float2 bo = s_bo[t];
+        const float a = -2.f * pc.z, c = -2.f * pc.w, b = bo.x;
+        const float thr = fmaf(-2.002f, bo.y, 0.05f);
+        const bool pd = a > 0.f && c > 0.f && a * c - b * b > 0.f;
+        const float dx0 = (qx0 + 1.5f) - pc.x, dy0 = (qy0 + 1.5f) - pc.y;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float ox = (float)(4 * (g & 1)), oy = (float)(4 * (g >> 1));
+            const float x0 = qx0 + ox, y0 = qy0 + oy;
+            bool hit = in && t >= t_min[g] && bx.y >= x0 && bx.x <= x0 + 3.f && bx.w >= y0 && bx.z <= y0 + 3.f;
+            const float dx = dx0 + ox, dy = dy0 + oy;
+            const float u = a * dx + b * dy, v = b * dx + c * dy;
+            const float q = dx * u + dy * v;
+            const float lb = fmaf(-3.f, fabsf(u) + fabsf(v), q);
+            if (pd && lb > fmaf(1e-6f, q, thr)) hit = false;  // NaN-safe: keeps the record
+            const unsigned long long mask = wave_ballot(hit);
+            if (hit)
+                lists[g][cnt[g] + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0))] = (uint8_t)t;
+            cnt[g] += __popcll(mask);
+        }
+    }
+    wave_lds_handoff();
+}
+
+// Backward with one record list per 4x4 lane group.  The wave's four 16-lane rows are the forward's four 4x4 pixel
+// blocks, and each row walks its own list (bwd_compact_groups): a wave step serves four (block, record) pairs, one per
+// row, instead of one record over the 8x8 quadrant.  Everything per record stays row-local:
+// - lane u of a row loads its row's list entry j0 + u, and record U reaches the row's lanes by DPP row_newbcast:U
+//   (different records in different rows, one LDS read per lane per 16 entries, as in the quadrant kernel);
+// - phase 1 is unchanged: each lane replays its pixel and hands (o G dL/dalpha, alpha T) of four records to LDS;
+// - phase 2: lane 16 g + 4 r' + r sums record r of row g over the four pixels of block row r' (its own quad), then
+//   two transposed DPP steps inside the row (tstep8, tstep4: bank-masked moves, no selects) leave each lane two of
+//   the record's nine sums (and the ninth in the lanes with bits 3:2 clear): three LDS adds per lane and hand-off,
+//   as in the quadrant kernel, into the tile's accumulators.
+// LDS: 31.6 KB (the Gaussian ids of a batch wait in registers and go through the hand-off region for the flush), so
+// five workgroups per CU as before.
+// Round 5, measured at cfg4 (scripts/gpu_r5*.sh, profiles/round5/render_bwd/): 3.48M wave steps instead of 4.92M and
+// 0.545 useful lanes instead of 0.386 (GSD_COUNT_WORK), parity green -- but the accumulation bounds it.  Each (row,
+// record) pair now leaves nine sums (12.8M pairs instead of 4.9M (wave, record) pairs), and LDS float atomics cost
+// ~3 LDS cycles per lane on gfx950 (scripts/calib/lds_rate.hip): 0.735 ms with ds_add_f32, 0.489 with the
+// compare-and-swap adds below, 0.38 with plain stores in their place (timing only), against 0.48 for the quadrant
+// kernel.  Not the default (-DGSD_BWD_GROUPS); an accumulation at plain-store cost would make it 20 % faster.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_render_bwd_groups(RenderBwdParams p) {
+    __shared__ float4 s_pc[kTilePix];   // stage_pc: mx, my, -a/2, -c/2
+    __shared__ float2 s_bo[kTilePix];   // b, t_o
+    __shared__ float4 s_rgb[kTilePix];  // r, g, b, o
+    // record t's nine sums at [9 t + q]: an odd pitch, so the per-record accesses of a lane group (the flush's
+    // finishing step, phase 2's adds of consecutive slots) fall in distinct banks, and the flush reads it linearly
+    __shared__ float s_acc[kRecUsed * kTilePix];
+    __shared__ __attribute__((aligned(4))) uint8_t s_list[4][4][kTilePix];  // [wave][group][entry]
+    // the alpha boxes are read by the compaction only, the hand-off buffer by the walk only, the Gaussian ids by
+    // the flush only (barriers apart)
+    __shared__ union {
+        float4 box[kTilePix];
+        float2 qa[4][kBwdGroup][65];  // per wave: per record and pixel; +1 pad
+        uint32_t id[kTilePix];
+    } s_u;
+    __shared__ int s_tile_lc;
+    const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);  // the forward's 4x4-group lane map
+    const int tid = threadIdx.x;
+    const int lane = tg.lane, u16 = lane & 15, grp = lane >> 4;
+    const uint2 rg = p.ranges[tg.tile];
+    const int pid = p.W * tg.py + tg.px;
+    const int plane = p.H * p.W;
+    const bool inside = tg.inside;
+    // per-pixel replay state (backward.cu:441-461)
+    const float T_final = inside ? p.final_T[pid] : 0.f;
+    float T = T_final;
+    const int last_contributor = inside ? (int)p.n_contrib[pid] : 0;
+    // Every pixel skips list positions >= its last contributor (backward.cu:487-488): the replay starts at the
+    // tile's largest last contributor, and each group's list drops positions beyond its own largest.
+    int row_lc = last_contributor;
+    row_lc = max(row_lc, __shfl_xor(row_lc, 8));
+    row_lc = max(row_lc, __shfl_xor(row_lc, 4));
+    row_lc = max(row_lc, __shfl_xor(row_lc, 2));
+    row_lc = max(row_lc, __shfl_xor(row_lc, 1));
+    int glc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) glc[g] = __builtin_amdgcn_readlane(row_lc, 16 * g);
+    if (tid == 0) s_tile_lc = 0;
+    lds_barrier();
+    if (lane == 0) atomicMax(&s_tile_lc, max(max(glc[0], glc[1]), max(glc[2], glc[3])));
+    lds_barrier();
+    const int total = min((int)(rg.y - rg.x), s_tile_lc);
+    const uint32_t end = rg.x + (uint32_t)total;
+    const int rounds = (total + kTilePix - 1) / kTilePix;
+    int toDo = total;
+    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
+    if (inside) {
+        dpix0 = p.dL_dpix[pid];
+        dpix1 = p.dL_dpix[plane + pid];
+        dpix2 = p.dL_dpix[2 * plane + pid];
+    }
+    float2(*qa)[65] = s_u.qa[tg.wave];
+    // dL/dpixel of the four pixels of the lane's quad (DPP quad broadcasts), for phase 2 below
+    float3 dpq[4];
+    dpq[0] = make_float3(quad_bcast<0>(dpix0), quad_bcast<0>(dpix1), quad_bcast<0>(dpix2));
+    dpq[1] = make_float3(quad_bcast<1>(dpix0), quad_bcast<1>(dpix1), quad_bcast<1>(dpix2));
+    dpq[2] = make_float3(quad_bcast<2>(dpix0), quad_bcast<2>(dpix1), quad_bcast<2>(dpix2));
+    dpq[3] = make_float3(quad_bcast<3>(dpix0), quad_bcast<3>(dpix1), quad_bcast<3>(dpix2));
+    float adot = 0.f;  // accum_rec . dL/dpixel (accum_rec with last_color / last_alpha folded in)
+    const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
+    const float kbg = -T_final * bg_dot;
+    const bool any_bg = wave_ballot(kbg != 0.f) != 0;  // wave-uniform
+    const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
+    const float pxf = (float)tg.px, pyf = (float)tg.py;
+    const uint8_t* my_list = s_list[tg.wave][grp];
+#ifdef GSD_COUNT_WORK
+    unsigned long long n_steps = 0, n_pairs = 0;
+#endif
+    // phase 2: the first pixel of the lane's block row (the quad's four pixels are x0 .. x0 + 3 on row y0)
+    const float ph2_x0 = tg.qx0 + (float)(4 * (grp & 1)), ph2_y0 = tg.qy0 + (float)(4 * (grp >> 1) + ((lane >> 2) & 3));
+    // phase 2's accumulator rows: lane bits 3:2 = (1, 0) -> quantity 1, (0, 1) -> 2 (tstep8 keeps a pair's first
+    // member where bit 3 is clear, tstep4 where bit 2 is clear)
+    const int qsel = ((lane >> 3) & 1) | ((lane >> 1) & 2);
+
+    for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
+        lds_barrier();
+        const int progress = i * kTilePix + tid;
+        uint32_t gid = 0;
+        if (progress < total) {  // loaded back to front (backward.cu:466-478)
+            gid = p.point_list[end - progress - 1];
+            const RenderRec* r = p.rec + gid;
+            const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
+            s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
+            s_bo[tid] = make_float2(q0.w, q2.y);               // b, t_o
+            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q1.y);  // r, g, b, o
+            s_u.box[tid] = r->box;
+        }
+#pragma unroll
+        for (int q = 0; q < kRecUsed; ++q) s_acc[q * kTilePix + tid] = 0.f;
+        lds_barrier();
+        const int n = min(kTilePix, toDo);
+        // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
+        const int front_base = total - 1 - i * kTilePix;
+        int t_min[4], cnt[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) t_min[g] = front_base - glc[g] + 1;
+        bwd_compact_groups(s_u.box, s_pc, s_bo, s_list[tg.wave], n, tg.qx0, tg.qy0, lane, t_min, cnt);
+        const int m = max(max(cnt[0], cnt[1]), max(cnt[2], cnt[3]));  // the longest list (wave-uniform)
+        const int mine = grp == 0 ? cnt[0] : grp == 1 ? cnt[1] : grp == 2 ? cnt[2] : cnt[3];
+        // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor, i.e.
+        // slot t counts for this pixel iff t > t_cut
+        const int t_cut = front_base - last_contributor;
+        lds_barrier();  // every wave is done with the boxes before s_u.qa is written
+        auto walk = [&](auto with_bg) {
+            constexpr bool kBg = decltype(with_bg)::value;
+            for (int j0 = 0; j0 < m; j0 += 16) {
+                const int nv = m - j0;      // entries left in the longest list (wave-uniform)
+                const int nvm = mine - j0;  // entries left in the lane's group's list (row-uniform)
+                const bool in_list = u16 < nvm;
+                const int slot = (int)my_list[j0 + u16];
+                const int rslot = in_list ? slot : 0;  // slot 0 past the list: finite, never taken (rkey)
+                const int rkey = in_list ? slot : -__INT_MAX__ - 1;
+                const float4 rpc = s_pc[rslot];
+                const float2 rbo = s_bo[rslot];
+                const float4 rrgb = s_rgb[rslot];
+                auto hand_off = [&](auto kc) {
+                    constexpr int K = decltype(kc)::value;
+                    const int r = lane & 3;
+                    // phase 2's record (entry K + r of the row's list) and its mean, read ahead of phase 1
+                    const bool own = K + r < nvm;
+                    const int rs = own ? (int)my_list[j0 + K + r] : 0;
+                    const float2 mrec = *reinterpret_cast<const float2*>(&s_pc[rs]);
+                    float* acc = s_acc + kRecUsed * rs;
+                    unsigned long long any_m = 0;  // lanes that took any record of the hand-off
+                    auto rec = [&](auto uc) {
+                        constexpr int U = K + decltype(uc)::value;
+                        const float4 pc = make_float4(row_bcast<U>(rpc.x), row_bcast<U>(rpc.y), row_bcast<U>(rpc.z),
+                                                      row_bcast<U>(rpc.w));
+                        const float2 bo = make_float2(row_bcast<U>(rbo.x), row_bcast<U>(rbo.y));
+                        bool keep, over;
+                        const float OG = record_og(pc, bo, pxf, pyf, keep, over);  // alpha before the 0.99 clamp
+                        // backward.cu:487-488 (list position below the pixel's last contributor; INT_MIN past the
+                        // row's list), :490-501
+                        const unsigned long long valid_m =
+                            wave_ballot(row_bcast_i<U>(rkey) > t_cut) & wave_ballot(keep) & wave_ballot(over);
+                        any_m |= valid_m;
+#ifdef GSD_COUNT_WORK
+                        n_steps += U < nv ? 1 : 0;
+                        n_pairs += __popcll(valid_m);
+#endif
+                        {
+#pragma clang fp contract(fast)
+                            const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
+                            const float og = valid ? OG : 0.f;
+                            const float alpha = fminf(0.99f, og);
+                            const float inv1ma = fast_recip(1.f - alpha);
+                            T = T * inv1ma;  // backward.cu:503 (T recovered by division)
+                            const float cd = fmaf(row_bcast<U>(rrgb.z), dpix2,
+                                                  fmaf(row_bcast<U>(rrgb.y), dpix1, row_bcast<U>(rrgb.x) * dpix0));
+                            const float diff = cd - adot;
+                            // backward.cu:512-529 (kbg = 0: fmaf(diff, T, -0) is diff * T, bit for bit)
+                            const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
+                            qa[U & 3][lane] = make_float2(og * dL_dalpha, alpha * T);
+                            adot = fmaf(alpha, diff, adot);
+                        }
+                    };
+                    rec(std::integral_constant<int, 0>{});
+                    rec(std::integral_constant<int, 1>{});
+                    rec(std::integral_constant<int, 2>{});
+                    rec(std::integral_constant<int, 3>{});
+                    if (!any_m) return;  // wave-uniform: no pixel took any of these records
+                    wave_lds_handoff();
+                    // Phase 2 (record-major), as in the quadrant kernel: lane 4 G + r sums its row's record K + r over
+                    // the four pixels of its quad, (x0 + i, y0), i = 0..3, from the moments S0 = sum v,
+                    // X1 = sum v i, X2 = sum v i^2 centred on the record mean (ex, ey), and C = sum w dL/dpixel.
+                    const float2 q0 = qa[r][(lane & ~3)], q1 = qa[r][(lane & ~3) + 1], q2 = qa[r][(lane & ~3) + 2],
+                                 q3 = qa[r][(lane & ~3) + 3];
+                    float S0, Mx, Mxx, My, Mxy, Myy, C0, C1, C2;
+                    {
+#pragma clang fp contract(fast)
+                        const float ex = ph2_x0 - mrec.x, ey = ph2_y0 - mrec.y;
+                        S0 = (q0.x + q1.x) + (q2.x + q3.x);
+                        const float X1 = fmaf(3.f, q3.x, fmaf(2.f, q2.x, q1.x));  // sum v i
+                        const float X2 = fmaf(9.f, q3.x, fmaf(4.f, q2.x, q1.x));  // sum v i^2
+                        Mx = fmaf(ex, S0, X1);                                      // sum v (x - mx)
+                        Mxx = fmaf(ex, Mx + X1, X2);                                // sum v (x - mx)^2
+                        My = ey * S0;
+                        Myy = ey * My;
+                        Mxy = ey * Mx;
+                        C0 = fmaf(q3.y, dpq[3].x, fmaf(q2.y, dpq[2].x, fmaf(q1.y, dpq[1].x, q0.y * dpq[0].x)));
+                        C1 = fmaf(q3.y, dpq[3].y, fmaf(q2.y, dpq[2].y, fmaf(q1.y, dpq[1].y, q0.y * dpq[0].y)));
+                        C2 = fmaf(q3.y, dpq[3].z, fmaf(q2.y, dpq[2].z, fmaf(q1.y, dpq[1].z, q0.y * dpq[0].z)));
+                    }
+                    // the record's sums over the row's four quads: lane bits 3:2 = (b3, b2) end with quantity
+                    // qsel = b3 + 2 b2 of (Mx, My, Mxx, Mxy) in ca and of (Myy, S0, C0, C1) in cb; C2 everywhere
+                    const float ca = tstep4(tstep8(Mx, My), tstep8(Mxx, Mxy));
+                    const float cb = tstep4(tstep8(Myy, S0), tstep8(C0, C1));
+                    const float c2 = sum4(sum8(C2));
+                    wave_lds_handoff();  // phase-1 writes of the next hand-off must stay behind these reads
+                    if (own) {  // the record's sums into the tile's accumulators (compare-and-swap float adds)
+                        lds_cas_add3(acc + qsel, ca, acc + 4 + qsel, cb, acc + 8, (lane & 12) ? 0.f : c2);
+                    }
+                };
+                hand_off(std::integral_constant<int, 0>{});
+                if (nv > 4) hand_off(std::integral_constant<int, 4>{});
+                if (nv > 8) hand_off(std::integral_constant<int, 8>{});
+                if (nv > 12) hand_off(std::integral_constant<int, 12>{});
+            }
+        };
+        if (any_bg)
+            walk(std::true_type{});
+        else
+            walk(std::false_type{});
+        lds_barrier();
+        if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
+            const float4 pc = s_pc[tid];
+            const float b = s_bo[tid].x;
+            const float o = s_rgb[tid].w;  // the sums are over q = o G dL/dalpha; dL/dopacity = sum G dL/dalpha = S0 / o
+            const float a = -2.f * pc.z, c = -2.f * pc.w;  // exact
+            float* acc = s_acc + kRecUsed * tid;
+            // phase 2 summed the first moments over x - mx, y - my: the reference's dx = mx - x flips them
+            const float m0 = -acc[0], m1 = -acc[1];
+            acc[0] = (a * m0 + b * m1) * -ddelx_dx;
+            acc[1] = (c * m1 + b * m0) * -ddely_dy;
+            acc[2] *= -0.5f;
+            acc[3] *= -0.5f;
+            acc[4] *= -0.5f;
+            acc[5] = o > 0.f ? acc[5] / o : 0.f;  // o = 0: alpha = 0, the record never took a pixel
+            s_u.id[tid] = gid;
+        }
+        lds_barrier();
+        // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,
+        // each inside one 64-B segment of its Gaussian's gradient record.
+        for (int e = tid; e < n * kRecUsed; e += kTilePix) {
+            const int r = e / kRecUsed, q = e - kRecUsed * r;
+            const float a = s_acc[e];
+            if (a != 0.f) atomicAdd(p.grad_rec + (size_t)s_u.id[r] * kGradRec + q, a);
+        }
+    }
+#ifdef GSD_COUNT_WORK
+    count_work(2, n_steps, n_pairs);
+#endif
+}
+
 void launch_render_fwd(const RenderParams& p, hipStream_t s) {
     if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_fwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 }
 void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
+#ifdef GSD_BWD_GROUPS
+    if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd_groups, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+#else
     if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+#endif
 }
 
 }  // namespace gsd

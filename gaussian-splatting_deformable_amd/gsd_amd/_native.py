@@ -7,11 +7,13 @@ code that runs).
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 15
+ABI_VERSION = 16
+CSRC_DIR = os.path.join(_PKG_ROOT, "csrc")
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -65,6 +67,8 @@ class RasterArgs(ctypes.Structure):
 SIGNATURES = {
     "gsd_abi_version": (_i32, []),
     "gsd_last_error": (ctypes.c_char_p, []),
+    "gsd_build_id": (ctypes.c_char_p, []),
+    "gsd_build_flags": (ctypes.c_char_p, []),
     "gsd_geom_buffer_bytes": (_sz, [_i32, _i32, _i32]),
     "gsd_image_buffer_bytes": (_sz, [_i32, _i32]),
     "gsd_backward_scratch_bytes": (_sz, [_i32]),
@@ -144,8 +148,42 @@ class NativeError(RuntimeError):
     pass
 
 
+def source_build_id(csrc: str = CSRC_DIR) -> str:
+    """SHA-256 of the sources a library built from `csrc` carries as gsd_build_id(): csrc/*.hip and *.h in name
+    order, include/gsd_raster.h, csrc/Makefile -- the same bytes, in the same order, as the Makefile's
+    `cat $(ID_SRCS) | sha256sum`."""
+    names = sorted(n for n in os.listdir(csrc) if n.endswith((".hip", ".h")))
+    paths = [os.path.join(csrc, n) for n in names]
+    paths += [os.path.join(csrc, "..", "..", "include", "gsd_raster.h"), os.path.join(csrc, "Makefile")]
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def check_build_id(lib, csrc: str = CSRC_DIR, path: str = LIB_PATH) -> str:
+    """Refuse a library whose gsd_build_id() is not the hash of the sources in `csrc` (a stale or foreign build:
+    the parity and timing claims are about the kernels of this tree).  GSD_SKIP_BUILD_ID=1 lifts the check for
+    A/B experiments that load libraries built from older snapshots (scripts/ab_bench.sh); nothing else sets it."""
+    got = lib.gsd_build_id().decode()
+    if os.environ.get("GSD_SKIP_BUILD_ID") == "1":
+        return got
+    want = source_build_id(csrc)
+    if got != want:
+        raise ImportError(f"gsd: {path} was built from other sources (build id {got[:16]}..., this tree "
+                          f"{want[:16]}...); rebuild it with `make -C gaussian-splatting_deformable_amd/csrc`")
+    return got
+
+
+def build_info() -> dict:
+    """The loaded library's provenance: path, build id (source hash) and extra compiler flags."""
+    lib = load()
+    return {"path": LIB_PATH, "build_id": lib.gsd_build_id().decode(), "flags": lib.gsd_build_flags().decode()}
+
+
 def load():
-    """Load and type the library once; raises if it is absent or ABI-mismatched."""
+    """Load and type the library once; raises if it is absent, ABI-mismatched or built from other sources."""
     global _lib
     if _lib is not None:
         return _lib
@@ -160,6 +198,7 @@ def load():
         fn.argtypes = args
     if lib.gsd_abi_version() != ABI_VERSION:
         raise ImportError(f"gsd: {LIB_PATH} has ABI {lib.gsd_abi_version()}, expected {ABI_VERSION}")
+    check_build_id(lib)
     _lib = lib
     return lib
 

@@ -104,6 +104,22 @@ def save_ply(path: str, pc) -> None:
     write_ply(path, {k: attrs[:, i] for i, k in enumerate(names)})
 
 
+def save_ply_t(path: str, pc, xyz, opacities, rotation) -> None:
+    """GaussianModel.save_ply_t (gaussian_model.py:932-958), what render(..., save_ply=True) writes per frame
+    (gaussian_renderer/__init__.py:165-167): the DEFORMED means and rotations and the ACTIVATED opacities that
+    render() handed the rasterizer, with the raw SH pieces and raw scaling of ``pc``; zero normals; the attribute
+    order of ``attribute_names``."""
+    xyz = xyz.detach().cpu().numpy()
+    f_dc = pc._features_dc.detach().transpose(1, 2).flatten(start_dim=1).contiguous().cpu().numpy()
+    f_rest = pc._features_rest.detach().transpose(1, 2).flatten(start_dim=1).contiguous().cpu().numpy()
+    opac = opacities.detach().cpu().numpy()
+    scale = pc._scaling.detach().cpu().numpy()
+    rot = rotation.detach().cpu().numpy()   # None (compute_cov3D_python) fails here, as upstream
+    attrs = np.concatenate((xyz, np.zeros_like(xyz), f_dc, f_rest, opac, scale, rot), axis=1)
+    names = attribute_names(f_dc.shape[1], f_rest.shape[1], scale.shape[1], rot.shape[1])
+    write_ply(path, {k: attrs[:, i] for i, k in enumerate(names)})
+
+
 def load_ply(path: str, max_sh_degree: int = 3) -> GaussianParams:
     """GaussianModel.load_ply (gaussian_model.py:965-1003) -> raw parameters (CPU float32 tensors)."""
     v = read_ply(path)

@@ -18,10 +18,23 @@ are per-view quantities and must be taken before the reduction; see
 """
 from __future__ import annotations
 
+import datetime
 import os
 
 import torch
 import torch.distributed as dist
+
+# Failure bound of the N > 1 path: every process group (the default one and the gloo signature group) is created
+# with this timeout, so a collective whose peer died or hangs raises on the waiting ranks after at most this long
+# instead of torch's defaults (10 min for RCCL, 30 min for gloo); with RCCL the watchdog then tears the
+# communicator down and the rank exits (TORCH_NCCL_ASYNC_ERROR_HANDLING=1, set unless the caller chose).  A peer
+# that EXITS is seen sooner: gloo's connections close at once, and torch.distributed.run stops every worker when
+# one fails.  GSD_DIST_TIMEOUT_S overrides the 120 s (tests/test_parallel_gloo.py::test_failed_rank_*).
+DIST_TIMEOUT_S = float(os.environ.get("GSD_DIST_TIMEOUT_S", "120"))
+
+
+def dist_timeout() -> datetime.timedelta:
+    return datetime.timedelta(seconds=DIST_TIMEOUT_S)
 
 
 def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
@@ -40,7 +53,8 @@ def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group(backend=backend, timeout=dist_timeout())
         signature_group()   # collective: every rank creates the host-side group at the same point
     return rank, local, world
 
@@ -55,7 +69,8 @@ def signature_group():
     default group itself must call this on every rank before the first data-parallel step."""
     global _SIG_GROUP
     if _SIG_GROUP is None:
-        _SIG_GROUP = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
+        _SIG_GROUP = (dist.group.WORLD if dist.get_backend() == "gloo" else
+                      dist.new_group(backend="gloo", timeout=dist_timeout()))
     return _SIG_GROUP
 
 

@@ -12,6 +12,7 @@ offsets/twists is outside the hot path: any callable
 from __future__ import annotations
 
 import math
+import os
 from types import SimpleNamespace
 
 import torch
@@ -213,7 +214,19 @@ def _time_for(model, tm):
 
 def render(viewpoint_camera, pc, pipe, bg_color, iteration=0, scaling_modifier=1.0, override_color=None,
            save_ply=False, control_time=None):
-    """gaussian_renderer/__init__.py:20-195."""
+    """gaussian_renderer/__init__.py:20-195.  save_ply=True also writes the frame's point cloud the way the reference
+    does (:165-167): test_ply/point_cloud_{int(time * 1000)}.ply under the working directory, with the deformed
+    means and rotations and the activated opacities the rasterizer was given (io.save_ply_t)."""
+    out = _render(viewpoint_camera, pc, pipe, bg_color, iteration, scaling_modifier, override_color, control_time)
+    if save_ply:
+        from .io import save_ply_t
+        t_id = str(int(viewpoint_camera.time * 1000))
+        save_ply_t(os.path.join("test_ply", f"point_cloud_{t_id}.ply"), pc, xyz=out["means3D"],
+                   opacities=out["opacities"], rotation=out["rotations"])
+    return out
+
+
+def _render(viewpoint_camera, pc, pipe, bg_color, iteration, scaling_modifier, override_color, control_time):
     dev = pc.get_xyz.device
     # the reference's zeros_like(xyz, requires_grad=True) + 0 with retain_grad(): a zero tensor whose .grad
     # receives dL/d means2D.  The rasterizer never reads its values, so it is a fresh leaf on a cached zero

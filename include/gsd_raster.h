@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 15
+#define GSD_ABI_VERSION 16
 
 enum {
     GSD_OK = 0,
@@ -157,6 +157,12 @@ typedef struct gsd_raster_args {
 
 int gsd_abi_version(void);
 const char* gsd_last_error(void);
+/* ABI 16, build provenance (no reference counterpart): the SHA-256 (64 hex digits) of the sources this library
+ * was compiled from -- csrc/*.hip and csrc/*.h in name order, this header, csrc/Makefile -- and the extra compiler
+ * flags of the build (HIPFLAGS_EXTRA, "" for the product build).  gsd_amd/_native.py recomputes the hash from its
+ * tree and refuses a library built from other sources. */
+const char* gsd_build_id(void);
+const char* gsd_build_flags(void);
 
 /* State-buffer sizes in bytes (GeometryState / ImageState / BinningState,
  * rasterizer_impl.h:29-73; layouts are private to this library). */

@@ -377,7 +377,8 @@ void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_
                         const float* co = conic_opacity + 4 * g;
                         float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                         if (power > 0.0f) continue;
-                        float alpha = fminf_(0.99f, co[3] * expf(power));
+                        /* CUDA's min(float, float) is fminf: a NaN product gives 0.99 (IEEE minNum) */
+                        float alpha = fminf(0.99f, co[3] * expf(power));
                         if (margin) m_alpha = fminf(m_alpha, fabsf((float)((double)alpha * 255.0 - 1.0)));
                         if (alpha < 1.0f / 255.0f) continue;
                         float test_T = T * (1 - alpha);
@@ -455,7 +456,7 @@ void orc_render_bwd(int P, int W, int H, const uint32_t* ranges, const uint32_t*
                         const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                         if (power > 0.0f) continue;
                         const float G = expf(power);
-                        const float alpha = fminf_(0.99f, co[3] * G);
+                        const float alpha = fminf(0.99f, co[3] * G);  /* minNum, as forward */
                         if (alpha < 1.0f / 255.0f) continue;
                         T = T / (1.f - alpha);
                         const float dchannel_dcolor = alpha * T;

@@ -118,3 +118,35 @@ def test_mlp_training_heads_argument_errors_without_gpu():
     assert rc == 1 and b"weight / bias gradients" in lib.gsd_last_error()
     rc = lib.gsd_deform_mlp_train_backward_heads(0, heads, W, 8, 8, 0, W, W, 0, None)
     assert rc == 1 and b"0 < P" in lib.gsd_last_error()
+
+
+def test_build_id_is_the_hash_of_this_tree():
+    """gsd_build_id() (ABI 16) is the SHA-256 the Makefile took of the sources; load() recomputed it from this
+    tree and accepted the library."""
+    from gsd_amd import _native
+    lib = _native.load()
+    info = _native.build_info()
+    assert info["build_id"] == _native.source_build_id() and len(info["build_id"]) == 64
+    assert info["flags"] == lib.gsd_build_flags().decode()
+
+
+def test_library_built_from_other_sources_is_refused(tmp_path):
+    """A copy of the tree with one source byte changed no longer matches the library: check_build_id raises (the
+    same check load() runs), while the unchanged copy passes."""
+    import shutil
+
+    import pytest
+
+    from gsd_amd import _native
+    lib = _native.load()
+    csrc = tmp_path / "pkg" / "csrc"
+    shutil.copytree(_native.CSRC_DIR, csrc)
+    (tmp_path / "include").mkdir()
+    shutil.copy(HEADER, tmp_path / "include" / "gsd_raster.h")
+    assert _native.check_build_id(lib, csrc=str(csrc)) == _native.source_build_id()
+    src = csrc / "gsd_render.hip"
+    data = bytearray(src.read_bytes())
+    data[100] ^= 0x20
+    src.write_bytes(bytes(data))
+    with pytest.raises(ImportError, match="built from other sources"):
+        _native.check_build_id(lib, csrc=str(csrc))

@@ -238,6 +238,41 @@ def test_backward_low_opacity(oracle_mod):
     assert np.all(got[op < 1.0 / 255.0] == 0.0)
 
 
+@pytest.mark.parametrize("kind", ["negative_zero", "nan"])
+def test_opacities_outside_the_unit_interval(oracle_mod, kind):
+    """The activated API takes opacities as given.  Negative ones give alpha = min(0.99, o G) < 1/255 at
+    every pixel, so they are never composited (forward.cu:343-345; the kernels' threshold t_o = +inf); zero ones
+    likewise; a NaN one composites at alpha = fminf(0.99, NaN) = 0.99 wherever power <= 0 (CUDA's min is IEEE
+    minNum).  Forward bars and backward gradients against the oracle.  With NaN opacities the gradients of the other
+    Gaussians are compared (the NaN Gaussians' own are NaN through dL/dG = o dL/dalpha, backward.cu:538, except
+    dL/dopacity, which the kernel recovers from its sum of o G dL/dalpha and so cannot give for a NaN o)."""
+    P, W, H, deg = 6_000, 320, 240, 3
+    d = scene_inputs(P, W, H, deg, seed=31, device=DEV)
+    op = d["opacities"].clone()
+    if kind == "negative_zero":
+        op[0:600:3] = -op[0:600:3]
+        op[1:600:3] = 0.0
+    else:
+        op[0:600:50] = float("nan")
+    d["opacities"] = op.contiguous()
+    dpix = torch.randn(3, H, W, generator=torch.Generator().manual_seed(32)).mul_(1e-3).to(DEV)
+    o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    fwd = gpu_forward(d)
+    check_forward_against(o, d, fwd)
+    grads = gpu_backward(d, fwd, dpix)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    rows = np.isfinite(op.cpu().numpy().reshape(-1))     # the Gaussians compared
+    for name, gt in zip(names, grads):
+        got = gt.cpu().numpy().reshape(ob[name].shape)[rows]
+        want = ob[name][rows]
+        assert np.isfinite(got).all() and np.isfinite(want).all(), name
+        assert rel_l2(got, want) <= 1e-4, (name, rel_l2(got, want))
+    if kind == "negative_zero":
+        g_op = grads[2].cpu().numpy().reshape(-1)
+        assert np.all(g_op[(op.cpu().numpy().reshape(-1) <= 0)] == 0.0)
+
+
 def test_backward_run_to_run_noise():
     """The backward's gradient sums are float atomics in scheduling order, so two runs on the same inputs differ
     in the last bits; the per-record reductions must not amplify that (a formulation whose centring cancels

@@ -181,3 +181,32 @@ def test_forward_backward_on_a_side_stream_follows_the_current_stream():
         if y.numel():
             assert torch.isfinite(x).all(), i
             assert rel_l2(x.cpu().numpy(), y.numpy()) <= 2e-6, (i, rel_l2(x.cpu().numpy(), y.numpy()))
+
+
+@pytest.mark.parametrize("offsets", [False, True])
+def test_render_save_ply_writes_the_frame(tmp_path, monkeypatch, offsets):
+    """render(..., save_ply=True) (gaussian_renderer/__init__.py:165-167): test_ply/point_cloud_{int(time*1000)}.ply
+    under the working directory holds exactly the means, opacities and rotations render() returned (deformed and
+    activated; the raw-parameter path builds them lazily), the raw scaling and the raw SH pieces."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.io import read_ply
+    from gsd_amd.scene import make_gaussians
+    monkeypatch.chdir(tmp_path)
+    P = 5_000
+    params = make_gaussians(P, 160, 120, seed=8, device=DEV)
+    pc = DeformableGaussians(params, sh_degree=3, offset_model=_FixedOffsets(P, seed=5) if offsets else None)
+    cam = synthetic_camera(160, 120).to(DEV)
+    cam.time = 0.25
+    with torch.no_grad():
+        out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV), save_ply=True)
+    v = read_ply(str(tmp_path / "test_ply" / "point_cloud_250.ply"))
+    col = lambda *ks: np.stack([v[k] for k in ks], 1)  # noqa: E731
+    assert np.array_equal(col("x", "y", "z"), out["means3D"].cpu().numpy())
+    assert np.array_equal(col("opacity"), out["opacities"].cpu().numpy())
+    assert np.array_equal(col("rot_0", "rot_1", "rot_2", "rot_3"), out["rotations"].cpu().numpy())
+    assert np.array_equal(col("scale_0", "scale_1", "scale_2"), pc._scaling.detach().cpu().numpy())
+    assert np.array_equal(col(*[f"f_rest_{3 * 15 - 15 + i}" for i in range(15)]),
+                          pc._features_rest.detach()[:, :, 2].cpu().numpy())
+    if offsets:   # deformed: the file is not the raw parameters
+        assert not np.array_equal(col("x", "y", "z"), pc._xyz.detach().cpu().numpy())

@@ -60,3 +60,27 @@ def test_load_ply_rejects_wrong_sh_degree(tmp_path):
     save_ply(path, _pc(P=8))
     with pytest.raises(ValueError):
         load_ply(path, max_sh_degree=2)
+
+
+def test_save_ply_t_roundtrip(tmp_path):
+    """save_ply_t (gaussian_model.py:932-958): the given deformed means / activated opacities / deformed rotations
+    next to the model's raw SH pieces and raw scaling, in the attribute order of construct_list_of_attributes;
+    read back through read_ply bit for bit."""
+    from gsd_amd.io import attribute_names, read_ply, save_ply_t
+    pc = _pc(P=129, seed=6)
+    g = torch.Generator().manual_seed(1)
+    xyz = pc._xyz + 0.01 * torch.randn(129, 3, generator=g)
+    opac = torch.sigmoid(pc._opacity)
+    rot = torch.nn.functional.normalize(pc._rotation + 0.1 * torch.randn(129, 4, generator=g))
+    path = str(tmp_path / "test_ply" / "point_cloud_250.ply")
+    save_ply_t(path, pc, xyz=xyz, opacities=opac, rotation=rot)
+    v = read_ply(path)
+    assert list(v) == attribute_names()
+    col = lambda *ks: np.stack([v[k] for k in ks], 1)  # noqa: E731
+    assert np.array_equal(col("x", "y", "z"), xyz.detach().numpy())
+    assert np.array_equal(col("nx", "ny", "nz"), np.zeros((129, 3), np.float32))
+    assert np.array_equal(col("opacity"), opac.detach().numpy())
+    assert np.array_equal(col("scale_0", "scale_1", "scale_2"), pc._scaling.detach().numpy())
+    assert np.array_equal(col("rot_0", "rot_1", "rot_2", "rot_3"), rot.detach().numpy())
+    assert np.array_equal(col(*[f"f_rest_{i}" for i in range(15)]), pc._features_rest.detach()[:, :, 0].numpy())
+    assert np.array_equal(col("f_dc_0", "f_dc_1", "f_dc_2"), pc._features_dc.detach()[:, 0, :].numpy())

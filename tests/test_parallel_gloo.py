@@ -8,6 +8,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -586,3 +587,64 @@ def test_eight_rank_sh_view_exchange_matches_sum_of_views(tmp_path):
 
 def test_eight_rank_plain_allreduce_matches_sum_of_views(tmp_path):
     _eight_rank(tmp_path, 0)
+
+
+def _worker_fail(rank, world, port, out_dir, mode):
+    """Three all-reduce steps; rank 2 exits (mode "exit") or hangs ("hang") before its second step.  A surviving
+    rank whose collective raises records the time and exits with status 17."""
+    import sys
+    import time
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), GSD_DIST_TIMEOUT_S="6")
+    from gsd_amd.parallel import FlatGrads, init_from_env
+    r, _, w = init_from_env(backend="gloo")
+    params = [torch.nn.Parameter(torch.zeros(1000)), torch.nn.Parameter(torch.zeros(7, 3))]
+    fg = FlatGrads(params, device="cpu")
+    t0 = None
+    try:
+        for step in range(3):
+            if step == 1 and r == 2:
+                if mode == "exit":
+                    os._exit(3)
+                time.sleep(3600)
+            t0 = time.time()
+            for p in params:
+                p.grad.fill_(1.0)
+            fg.allreduce()
+    except Exception as e:   # the peer's failure, seen by this rank's collective
+        with open(os.path.join(out_dir, f"err{r}.txt"), "w") as f:
+            f.write(f"{time.time() - t0:.3f} {type(e).__name__}: {e}"[:2000])
+        os._exit(17)
+    os._exit(0)
+
+
+@pytest.mark.parametrize("mode", ["exit", "hang"])
+def test_failed_rank_ends_its_peers_within_the_timeout(tmp_path, mode):
+    """Failure bound of the N > 1 path (parallel.DIST_TIMEOUT_S): of four gloo ranks one exits, or hangs, in the
+    middle of the step sequence; the three others must leave their collective with an error and exit non-zero
+    within the timeout (6 s here) plus a margin, instead of waiting in it for torch's default 30 minutes."""
+    import time
+    ctx = mp.get_context("spawn")
+    world, port = 4, _free_port()
+    procs = [ctx.Process(target=_worker_fail, args=(r, world, port, str(tmp_path), mode)) for r in range(world)]
+    t0 = time.time()
+    for p in procs:
+        p.start()
+    try:
+        for r, p in enumerate(procs):
+            if r != 2:
+                p.join(timeout=max(1.0, 60.0 - (time.time() - t0)))
+        for r, p in enumerate(procs):
+            if r == 2:
+                continue
+            assert p.exitcode == 17, (r, p.exitcode)
+            elapsed = float((tmp_path / f"err{r}.txt").read_text().split()[0])
+            assert elapsed <= 6.0 + 10.0, (r, (tmp_path / f"err{r}.txt").read_text())
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+            p.join(timeout=10)
