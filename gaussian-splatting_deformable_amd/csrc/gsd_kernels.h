@@ -420,7 +420,7 @@ void launch_mlp_pack(const MlpPackParams& p, hipStream_t s);
 void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E, float* ET, hipStream_t s);
 void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, float* dx, int accumulate, hipStream_t s);
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s);
-void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s);
+void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s, bool store = true);
 // dW scattered into the reference-shaped weight pieces (dst.W; map/rows as the forward weight), db into dst_b
 void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s);
 void launch_mlp_rows_to_features(int P, int ldp, const MlpHeadsIn& src, float* dst, int dst_rows, hipStream_t s);

@@ -516,7 +516,9 @@ __device__ __forceinline__ f32x16 mfma_x6_part(const Split8& a, const Split8& b,
 //  - the three-term split of the NEXT k-step's B operand, a pair of elements per gap (row blocks 1-4, gap 5);
 // then s_waitcnt vmcnt(the stores and copies issued after k-step s + ks + 1's last copy) and a raw barrier.
 // PREV: the stores of each of the layer before's last two k-steps (0 after layer 0).
-template <int KSE, int KSA, int PREV>
+// ST = false (the evaluation without autograd, k_mlp_fwd_fused<false>): no output stores at all, and the waits count
+// the copies only.
+template <int KSE, int KSA, int PREV, bool ST = true>
 __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsigned char* s_mem, int s, int l,
                                                    int wave, int lane, unsigned voff_h, unsigned voff_b,
                                                    const float (&xe)[4][8], const float (&xt)[2][8],
@@ -544,7 +546,7 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
         const unsigned dst = lds_addr(s_mem) + ((s + kk) & 3) * (24 * 1024);
         const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + ((s + ks) & 3) * (24 * 1024));
         const int k2 = ks >= KSE ? ks - KSE : 0;   // act[k2][r]: row 16 k2 + 8 (r >> 2) + 4 h + (r & 3)
-        const bool stores = ks >= KSE && !(GSD_ABLATE & 4);
+        const bool stores = ST && ks >= KSE && !(GSD_ABLATE & 4);
         Split8 bn = b;
         Split8 a;
         a.hi = sa[lane];
@@ -594,8 +596,8 @@ __device__ __forceinline__ void fused_hidden_layer(const MlpFusedParams& p, unsi
         if constexpr (GSD_ABLATE & 2048) {
             raw_barrier();   // the ds_writes (lgkmcnt) before it; the loads and stores stay in flight
         } else if constexpr (!(GSD_ABLATE & 256)) {
-            wait_vm_u(fused_stores_late(KSE, ks - 2, PREV) + fused_stores(KSE, ks - 1, PREV) +
-                      fused_stores(KSE, ks, PREV) + 12);
+            wait_vm_u((ST ? fused_stores_late(KSE, ks - 2, PREV) + fused_stores(KSE, ks - 1, PREV) +
+                                fused_stores(KSE, ks, PREV) : 0) + 12);
             raw_barrier();
         }
     }
@@ -624,6 +626,10 @@ __device__ __forceinline__ void fused_hidden_epilogue(const float* s_bias, int h
     }
 }
 
+// kStore = false: the evaluation without autograd (the reference's f32 network under torch.no_grad(), render.py:46 ->
+// gaussian_model.py:290-316): the same kernel without the hidden outputs' and ReLU words' stores (8 KB per Gaussian
+// of HBM writes), p.H / p.bits unused -- only the heads are written.
+template <bool kStore>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_mlp_fwd_fused(MlpFusedParams p) {
     __shared__ __attribute__((aligned(16))) unsigned char s_mem[4 * 24 * 1024];
     // the biases in an LDS object of their own: the compiler then knows the ring's copies cannot write them and
@@ -678,21 +684,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
         wait_vm_c<12>();
         raw_barrier();
     }
-    fused_hidden_layer<6, 0, 0>(p, s_mem, 0, 0, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
+    constexpr int PV = kStore ? 8 : 0;
+    fused_hidden_layer<6, 0, 0, kStore>(p, s_mem, 0, 0, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
     fused_hidden_epilogue(s_bias, h, acc, act, bits);
-    fused_hidden_layer<0, 16, 0>(p, s_mem, 6, 1, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
+    fused_hidden_layer<0, 16, 0, kStore>(p, s_mem, 6, 1, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
     fused_hidden_epilogue(s_bias + 256, h, acc, act, bits);
 #pragma unroll 1
     for (int l = 2; l <= 4; ++l) {
-        fused_hidden_layer<0, 16, 8>(p, s_mem, 6 + 16 * (l - 1), l, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
+        fused_hidden_layer<0, 16, PV, kStore>(p, s_mem, 6 + 16 * (l - 1), l, wave, lane, voff_h, voff_b, xe, xt, act,
+                                              bits, acc, R);
         fused_hidden_epilogue(s_bias + 256 * l, h, acc, act, bits);
     }
-    fused_hidden_layer<4, 16, 8>(p, s_mem, 70, 5, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
+    fused_hidden_layer<4, 16, PV, kStore>(p, s_mem, 70, 5, wave, lane, voff_h, voff_b, xe, xt, act, bits, acc, R);
     fused_hidden_epilogue(s_bias + 256 * 5, h, acc, act, bits);
 #pragma unroll 1
     for (int l = 6; l <= 7; ++l) {
-        fused_hidden_layer<0, 16, 8>(p, s_mem, 90 + 16 * (l - 6), l, wave, lane, voff_h, voff_b, xe, xt, act, bits,
-                                     acc, R);
+        fused_hidden_layer<0, 16, PV, kStore>(p, s_mem, 90 + 16 * (l - 6), l, wave, lane, voff_h, voff_b, xe, xt, act,
+                                              bits, acc, R);
         fused_hidden_epilogue(s_bias + 256 * l, h, acc, act, bits);
     }
     // the heads (58 outputs, two row blocks): their own ring over the same LDS, 6 chunks per k-step (two copies per
@@ -723,10 +731,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
         GSD_HEADS_ISSUE(ks + 3);
         const Split8 b = split8(act[ks]);
         const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (8 * 1024));
+        if constexpr (kStore) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            __builtin_nontemporal_store(act[ks][j], H7 + (size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_h);
-        if (ks < 8) __builtin_nontemporal_store((unsigned short)bits[ks < 8 ? ks : 0], B7 + (size_t)(2 * ks) * ldp + voff_b);
+            for (int j = 0; j < 8; ++j)
+                __builtin_nontemporal_store(act[ks][j], H7 + (size_t)(16 * ks + 8 * (j >> 2) + (j & 3)) * ldp + voff_h);
+            if (ks < 8)
+                __builtin_nontemporal_store((unsigned short)bits[ks < 8 ? ks : 0], B7 + (size_t)(2 * ks) * ldp + voff_b);
+        }
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             Split8 a;
@@ -735,8 +746,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
             a.lo = sa[(r * 3 + 2) * 64 + lane];
             ho[r] = mfma_x6(a, b, ho[r]);
         }
-        wait_vm_u(4 + (ks >= 2 ? fused_stores(0, ks - 2, 0) : 0) + (ks >= 1 ? fused_stores(0, ks - 1, 0) : 0) +
-                  fused_stores(0, ks, 0));
+        wait_vm_u(4 + (kStore ? (ks >= 2 ? fused_stores(0, ks - 2, 0) : 0) + (ks >= 1 ? fused_stores(0, ks - 1, 0) : 0) +
+                                    fused_stores(0, ks, 0)
+                              : 0));
         raw_barrier();
     }
 #undef GSD_HEADS_ISSUE
@@ -768,8 +780,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 // once (the weight gradients' operand), its rows stored under the next step's MFMAs; nothing is re-read.  The
 // mask words of all eight steps (16 B per lane each) are loaded at the start: a load issued inside the ring would be
 // waited for by the next k-step's counted wait (the counter retires in order), at HBM latency.  A final two-row-block
-// step multiplies g0 by W0^T's enc(x) rows: the encoding's gradient (layer 5's enc(x) rows are the separate
-// k_mlp_gemm_dma of g5 that adds to it).
+// step multiplies g0 by W0^T's enc(x) rows: the encoding's gradient, to which layer 5's enc(x) rows times g5 add --
+// formed inside the kernel by enc_pass (a ring of its own, just before step 3, while the B operand holds g5).
 
 // global stores of a chain k-step: all eight act rows, three of them (row blocks 5-7) after the k-step's last copy
 __device__ __forceinline__ constexpr int chain_stores(int ks, int prev) { return ks < 0 ? (prev ? 8 : 0) : 8; }
@@ -1286,8 +1298,10 @@ static void launch_gemm_rb(const MlpGemmParams& p, hipStream_t s) {
     }
 }
 
-void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s) {
-    if (p.P > 0) hipLaunchKernelGGL(k_mlp_fwd_fused, dim3(p.ldp / 128), dim3(256), 0, s, p);
+void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s, bool store) {
+    if (p.P <= 0) return;
+    if (store) hipLaunchKernelGGL(k_mlp_fwd_fused<true>, dim3(p.ldp / 128), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_mlp_fwd_fused<false>, dim3(p.ldp / 128), dim3(256), 0, s, p);
 }
 
 void launch_mlp_bwd_chain(const MlpChainParams& p, hipStream_t s) {

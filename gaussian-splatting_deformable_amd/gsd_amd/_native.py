@@ -115,6 +115,9 @@ SIGNATURES = {
                                                   ctypes.POINTER(_vp), _vp]),
     "gsd_deform_mlp_train_backward_heads": (_i32, [_i64, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp, _i32,
                                                    ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i32, _vp]),
+    "gsd_deform_mlp_eval_workspace_bytes": (_sz, [_i64]),
+    "gsd_deform_mlp_eval_forward_heads": (_i32, [_i64, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp,
+                                                 ctypes.POINTER(_vp), _vp]),
     "gsd_work_counters": (_i32, [_i32, ctypes.POINTER(ctypes.c_uint64), _i32]),
     "gsd_timing_enable": (_i32, [_i32]),
     "gsd_timing_collect": (_i32, [_i32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64)]),

@@ -268,6 +268,29 @@ def _train_forward(net: "DirectTemporalNeRF", x: torch.Tensor, ts: torch.Tensor)
     return _MLPTrainF32.apply(x, ts, *ws, *bs)
 
 
+@torch.no_grad()
+def _eval_forward_f32(net: "DirectTemporalNeRF", x: torch.Tensor, ts: torch.Tensor):
+    """The f32 network without autograd (render.py:46 renders under torch.no_grad(), gaussian_model.py:290-316):
+    gsd_deform_mlp_eval_forward_heads -- the training forward's layer-fused BF16x6 kernel without its hidden-output
+    stores, and a workspace of the packed weights and the encoding only (~0.4 KB per Gaussian, freed on return)."""
+    from . import _native
+    from ._C import _ptr, _stream
+    lib = _native.load()
+    P = int(x.shape[0])
+    dev = x.device
+    ws_, bs_ = _param_list(net)
+    wc = [w.detach().contiguous() for w in ws_]
+    bc = [b.detach().contiguous() for b in bs_]
+    xc = x.detach().to(torch.float32).contiguous()
+    tc = ts.detach().to(torch.float32).reshape(-1).expand(P).contiguous()
+    ws = torch.empty(lib.gsd_deform_mlp_eval_workspace_bytes(P), dtype=torch.uint8, device=dev)
+    heads = [torch.empty(P, n, dtype=torch.float32, device=dev) for n in _HEADS]
+    with torch.cuda.device(dev):
+        _native.check(lib.gsd_deform_mlp_eval_forward_heads(P, _ptr(xc), _ptr(tc), _ptr_array(wc), _ptr_array(bc),
+                                                            _ptr(ws), _ptr_array(heads), _stream(dev)))
+    return tuple(heads)
+
+
 def positional_encoding(x: torch.Tensor, n_freqs: int = 10) -> torch.Tensor:
     """[x, sin(x 2^0), cos(x 2^0), ..., sin(x 2^(n-1)), cos(x 2^(n-1))] (gaussian_model.py:33-82, log sampling)."""
     freqs = 2.0 ** torch.linspace(0.0, n_freqs - 1, steps=n_freqs, device=x.device)
@@ -297,16 +320,24 @@ class DirectTemporalNeRF(nn.Module):
     def _reference_arch(self) -> bool:
         return (self.D, self.W, self.n_freqs, self.skips) == (8, 256, 10, (4,))
 
+    def _hip_f32(self, x: torch.Tensor) -> bool:
+        return (self.compute_dtype == torch.float32 and x.device.type == "cuda" and self._reference_arch()
+                and not os.environ.get("GSD_MLP_TORCH") and all(p.dtype == torch.float32 for p in self.parameters())
+                and all(p.device == x.device for p in self.parameters()))
+
+    def _needs_grad(self, x: torch.Tensor) -> bool:
+        return torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
+
     def _use_train_f32(self, x: torch.Tensor) -> bool:
         """The f32 network on a HIP device (the reference's training precision) runs the hand-written training
         path (gsd_mlp_train.hip: BF16x6 on the matrix cores, forward and backward) when a backward can follow --
-        its forward stores every hidden layer for that backward (~10.6 KB per Gaussian), which an evaluation
-        (no_grad, or nothing requiring grad) would allocate for nothing, so that runs on torch's f32 GEMMs.
-        GSD_MLP_TORCH=1 keeps torch."""
-        if not (torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
-            return False
-        return (self.compute_dtype == torch.float32 and x.device.type == "cuda" and self._reference_arch()
-                and not os.environ.get("GSD_MLP_TORCH") and all(p.dtype == torch.float32 for p in self.parameters()))
+        its forward stores every hidden layer and the backward every layer's gradient (~17 KB per Gaussian).  An
+        evaluation (no_grad, or nothing requiring grad) runs the same forward kernel without those stores
+        (_eval_forward_f32).  GSD_MLP_TORCH=1 keeps torch for both."""
+        return self._needs_grad(x) and self._hip_f32(x)
+
+    def _use_eval_f32(self, x: torch.Tensor) -> bool:
+        return not self._needs_grad(x) and self._hip_f32(x)
 
     def _use_fused(self, x: torch.Tensor) -> bool:
         """The fused bf16 kernel (gsd_mlp.hip) serves the bf16 evaluation without autograd on a HIP device, for
@@ -327,6 +358,8 @@ class DirectTemporalNeRF(nn.Module):
             return _fused_forward(self, x, ts)
         if self._use_train_f32(x):
             return _train_forward(self, x, ts)
+        if self._use_eval_f32(x):
+            return _eval_forward_f32(self, x, ts)
         ex = positional_encoding(x, self.n_freqs)
         et = positional_encoding(ts, self.n_freqs)
         dt = self.compute_dtype if self.compute_dtype != torch.float32 else ex.dtype  # f32: the input's own

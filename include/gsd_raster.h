@@ -380,8 +380,8 @@ int gsd_relu_backward_bias(int64_t P, int32_t N, int32_t bf16, const void* grad_
  * (256,319), (256,256) x 2, (3,256), (3,256), (4,256), (48,256) and their biases).  x (P,3), t (P) float32.
  * out (P,58) = [dx 3 | d log-scale 3 | d quaternion 4 | dSH 48] row-major.  workspace:
  * gsd_deform_mlp_train_workspace_bytes(P) bytes; the forward leaves in it what the backward of the same call
- * reads (the encoding and every hidden activation, feature-major: ~10.6 KB per Gaussian).  Replaces the module's
- * forward + autograd backward (torch GEMMs). */
+ * reads (the encoding and every hidden activation and, for the backward's dX chain, every layer's gradient,
+ * feature-major: ~17 KB per Gaussian).  Replaces the module's forward + autograd backward (torch GEMMs). */
 size_t gsd_deform_mlp_train_workspace_bytes(int64_t P);
 int gsd_deform_mlp_train_forward(int64_t P, const float* x, const float* t, const float* const* weights,
                                  const float* const* biases, void* workspace, float* out, void* stream);
@@ -400,6 +400,15 @@ int gsd_deform_mlp_train_forward_heads(int64_t P, const float* x, const float* t
 int gsd_deform_mlp_train_backward_heads(int64_t P, const float* const* grad_heads, const float* const* weights,
                                         void* workspace, float* dx, int32_t dx_accumulate, float* const* d_weights,
                                         float* const* d_biases, int32_t accumulate, void* stream);
+
+/* ABI 16: the same network's float32 EVALUATION without autograd -- the reference evaluates it under torch.no_grad()
+ * when rendering (render.py:46 -> gaussian_renderer/__init__.py:79 -> gaussian_model.py:290-316) -- at the training
+ * path's accuracy (BF16x6), in the training forward's layer-fused kernel without its hidden-output and ReLU-word
+ * stores.  Same arguments as gsd_deform_mlp_train_forward_heads; workspace: gsd_deform_mlp_eval_workspace_bytes(P)
+ * bytes (the packed weights and the encoding, ~0.4 KB per Gaussian), free after the call. */
+size_t gsd_deform_mlp_eval_workspace_bytes(int64_t P);
+int gsd_deform_mlp_eval_forward_heads(int64_t P, const float* x, const float* t, const float* const* weights,
+                                      const float* const* biases, void* workspace, float* const* heads, void* stream);
 
 /* Per-kernel device timing.  While enabled, every kernel this library
  * launches is bracketed by hipEvents on its own stream (a few us of overhead

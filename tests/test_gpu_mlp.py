@@ -286,7 +286,7 @@ def test_train_f32_nan_and_autograd_contracts():
     NaN-preserving, the backward mask passes a NaN's gradient as threshold_backward does): NaN outputs and
     gradients in the same places as the torch f32 path; (2) an in-place parameter update between the forward and
     the backward raises autograd's version error; (3) a second backward raises a clear error; (4) without grad the
-    forward takes torch's path (no 10.6-KB-per-Gaussian workspace)."""
+    forward takes the evaluation kernel (no ~17-KB-per-Gaussian training workspace)."""
     from gsd_amd.deform_mlp import DirectTemporalNeRF
     torch.manual_seed(5)
     net = DirectTemporalNeRF().cuda()
@@ -321,7 +321,7 @@ def test_train_f32_nan_and_autograd_contracts():
         loss.backward()
     with torch.no_grad():
         _, names = _launched(lambda: net2(x, t, 5000))
-    assert "deform_mlp_train_fwd" not in names
+    assert "deform_mlp_train_fwd" not in names and "deform_mlp_eval_fwd" in names
 
 
 def test_train_f32_inplace_gradients_and_unused_heads():
@@ -368,3 +368,76 @@ def test_train_f32_inplace_gradients_and_unused_heads():
     ((outs[0] * w0).sum() + (outs[3] * w3).sum()).backward()
     assert torch.equal(xx.grad, 2 * xa.grad) and all(torch.equal(p.grad, 2 * a) for p, a in zip(params, ga))
     flat.remove_hooks()
+
+
+@pytest.mark.parametrize("P,scale", [(1, 2.0), (77, 2.0), (257, 2.0), (5003, 1.0), (70_001, 1.0)])
+def test_eval_f32_matches_float64_oracle_and_training_forward(P, scale):
+    """The f32 network without autograd (gsd_deform_mlp_eval_forward_heads: the training forward's fused kernel
+    without its hidden-output stores) -- what render.py's torch.no_grad() evaluation runs: the four heads within
+    max(2e-5, 2x torch f32's error) of the float64 restatement, and bit-identical to the training forward's heads
+    (the same kernel arithmetic; only the stores differ)."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    from oracle import deform_mlp_ref
+    torch.manual_seed(60 + P % 5)
+    net = DirectTemporalNeRF()
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(scale)
+    g = torch.Generator().manual_seed(P + 1)
+    x = torch.rand(P, 3, generator=g) * 4 - 2
+    t = torch.full((P, 1), 0.6)
+    sd = {k: v.detach().double() for k, v in net.state_dict().items()}
+    ref = torch.cat(deform_mlp_ref.forward(sd, x.double(), t.double(), 5000), -1)
+    netc = net.cuda()
+    xc, tc = x.cuda(), t.cuda()
+    with torch.no_grad():
+        ev, names = _launched(lambda: netc(xc, tc, 5000))
+        os.environ["GSD_MLP_TORCH"] = "1"
+        try:
+            tor = torch.cat(netc(xc, tc, 5000), -1)
+        finally:
+            os.environ.pop("GSD_MLP_TORCH", None)
+    assert "deform_mlp_eval_fwd" in names and "deform_mlp_train_fwd" not in names
+    ev = torch.cat(ev, -1)
+    scale_ = float(ref.abs().max())
+    e_hip = float((ev.cpu().double() - ref).abs().max()) / scale_
+    e_torch = float((tor.cpu().double() - ref).abs().max()) / scale_
+    assert e_hip <= max(2e-5, 2.0 * e_torch), (e_hip, e_torch)
+    tr = torch.cat(netc(xc.clone().requires_grad_(True), tc, 5000), -1).detach()
+    assert torch.equal(ev, tr)
+
+
+def test_eval_f32_matches_reference_network_fixture():
+    """The evaluation kernel against the reference's own DirectTemporalNeRF run (tests/golden/mlp.npz): the four
+    heads within 2e-5 of their scale."""
+    from conftest import golden
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    g = golden("mlp.npz")
+    names = [str(n) for n in g["names"]]
+    net = DirectTemporalNeRF()
+    net.load_state_dict({n: torch.from_numpy(g["w:" + n]) for n in names})
+    net = net.cuda()
+    heads = ("dx", "dscale", "drot", "dshs")
+    with torch.no_grad():
+        out, launched = _launched(lambda: net(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["t"]).cuda(), 5000))
+    assert "deform_mlp_eval_fwd" in launched
+    want = np.concatenate([g["out:" + k] for k in heads], -1)
+    got = torch.cat(out, -1).cpu().numpy()
+    assert np.abs(got - want).max() <= 2e-5 * np.abs(want).max()
+
+
+def test_train_f32_fallback_kernels():
+    """The comparison paths kept beside the defaults -- the per-layer GEMM forward (GSD_MLP_FWD=gemm), the per-layer
+    dX GEMMs instead of the chain (GSD_MLP_BWD=gemm, which also sizes the workspace without the chain's gradient
+    buffers) and the eight-wave weight gradient (GSD_WGRAD16=0) -- read their switches once per process, so they run
+    here in a child pytest over the float64-oracle, fixture and in-place/unused-heads tests."""
+    import subprocess
+    import sys
+    env = dict(os.environ, GSD_MLP_FWD="gemm", GSD_MLP_BWD="gemm", GSD_WGRAD16="0")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        os.path.join(here, "test_gpu_mlp.py"), "-k",
+                        "train_f32_matches_float64 or train_f32_matches_reference or inplace_gradients"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and "failed" not in r.stdout

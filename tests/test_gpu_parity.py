@@ -4,9 +4,9 @@ Bars (DESIGN.md "Parity"):
   bit-exact   radii, depths, means2D, conic/opacity, rgb, clamp flags, num_rendered,
               ranges, point_list (== the reference's stable sort of |tile|depth| keys)
   tolerance   image and final_T |diff| <= 1e-5 and n_contrib exact at every pixel whose compositing decisions are
-              not borderline in the oracle; at a borderline pixel (some alpha within 1e-6 of 1/255, or some
-              T (1 - alpha) within 3e-5 of 1e-4, relative) a decision may flip -- the flips are counted and
-              reported, and there |diff| <= 1e-2 (image_bar).  Mean |diff| <= 1e-7.  Gradients: per-tensor
+              not borderline in the oracle; at a borderline pixel (some alpha within 3 ulp of 1/255, or some
+              T (1 - alpha) within T_MARGIN of 1e-4, relative) a decision may flip -- the flips are counted and
+              reported, and there |diff| <= FLIP_ABS_CAP (image_bar).  Mean |diff| <= 1e-7.  Gradients: per-tensor
               relative L2 <= 1e-4 (float atomics reorder sums), SE(3) deform vs float64 autograd: rel L2 <= 1e-5.
 """
 from __future__ import annotations
@@ -110,20 +110,26 @@ def check_forward_against(o, d, fwd, colors=None):
     return K
 
 
-# Borderline decisions (the oracle's per-pixel margins, oracle.forward): alpha within ALPHA_MARGIN (relative) of
-# 1/255 -- the HIP kernels decide such alphas on the accurate expf (a band of 3.8e-6 around the threshold, where
-# the hardware exp's few-ulp error could matter), so only the two expf implementations' ulp can still separate
-# them; T (1 - alpha) within T_MARGIN of 1e-4 -- T carries the hardware exp's few-ulp alpha differences of every
-# record before it (up to ~3e-6 relative at T = 1e-4).
-ALPHA_MARGIN = 1e-6
-T_MARGIN = 3e-5
+# Borderline decisions (the oracle's per-pixel margins, oracle.forward).  The HIP kernels decide alpha >= 1/255 as
+# power >= t_o (record_og, gsd_render.hip): the real comparison against t_o = -ln(255 o) rounded to the nearest float,
+# where the oracle rounds o * expf(power).  The two can part only where the oracle's alpha lies within its own rounding
+# of 1/255 (expf's ulp + the product's half ulp) plus t_o's half ulp (up to ~1 relative ulp of alpha): 2.5 ulp, and the
+# flips measured in round 5 sit at 0.5, 1.5 and 2.5 ulp (profiles/round5/parity/).  ALPHA_MARGIN is 3 ulp of 1/255
+# (the relative ulp there is 255 * 2^-31 = 1.19e-7).  T (1 - alpha) within T_MARGIN (relative) of 1e-4: T carries the
+# few-ulp alpha VALUE differences of the hardware exp over every record before it; T_MARGIN is twice the largest
+# relative final_T deviation measured at the configurations' pixels with no borderline alpha.
+ALPHA_MARGIN = 3 * 255 * 2.0 ** -31
+# measured at the alpha-clear pixels of configurations 1-5 (round 5): 6.5e-6, 8.4e-6, 9.2e-6, 1.04e-5, 1.05e-5
+T_MARGIN = 2.1e-5
+# a flip changes one record's share: bounded at twice the largest measured (8.4e-4 at cfg5, round 5)
+FLIP_ABS_CAP = 1.7e-3
 
 
 def image_bar(c, T, nc, o, tag=""):
     """Image / final_T / n_contrib bars against the oracle forward `o`.  Outside the borderline
     pixels: |diff| <= 1e-5 and n_contrib exact.  A pixel whose result differs beyond that must be borderline (a
-    flip); flips are counted and reported (GSD_PARITY_REPORT: a JSONL file to append the counts to), and bounded
-    by 1e-2 (one record's contribution, alpha T c < 1/255 + 1e-4, and the T behind it).  Mean |diff| <= 1e-7."""
+    flip); flips are counted and reported (GSD_PARITY_REPORT: a JSONL file to append the counts to), bounded by
+    FLIP_ABS_CAP and at most a third of the borderline pixels (or 4).  Mean |diff| <= 1e-7."""
     import json
     import os
     c_ref, T_ref, nc_ref = o["color"], o["final_T"], o["n_contrib"]
@@ -132,15 +138,22 @@ def image_bar(c, T, nc, o, tag=""):
     dT = np.abs(T - T_ref)
     nc_bad = nc.astype(np.uint32) != nc_ref
     flips = (dc > 1e-5) | (dT > 1e-5) | nc_bad
+    T_ref64 = np.maximum(np.asarray(T_ref, np.float64), 1e-30)
+    rel_T = np.abs(np.asarray(T, np.float64) - T_ref64) / T_ref64
     stats = dict(tag=tag, pixels=int(dc.size), borderline=int(border.sum()), flips=int(flips.sum()),
                  n_contrib_mismatch=int(nc_bad.sum()),
                  alpha_borderline=int((o["margin_alpha"] < ALPHA_MARGIN).sum()),
-                 max_abs_outside=float(dc[~border].max(initial=0.0)), max_abs_flips=float(dc[flips].max(initial=0.0)))
+                 max_abs_outside=float(dc[~border].max(initial=0.0)), max_abs_flips=float(dc[flips].max(initial=0.0)),
+                 max_rel_T_outside_flips=float(rel_T[~flips].max(initial=0.0)),
+                 max_rel_T_alpha_clear=float(rel_T[~flips & (o["margin_alpha"] >= ALPHA_MARGIN)].max(initial=0.0)),
+                 flip_margins=[[float(a), float(b)] for a, b in zip(o["margin_alpha"][flips], o["margin_T"][flips])])
     if os.environ.get("GSD_PARITY_REPORT"):
         with open(os.environ["GSD_PARITY_REPORT"], "a") as f:
             f.write(json.dumps(stats) + "\n")
     assert not (flips & ~border).any(), ("a decision flipped at a non-borderline pixel", stats)
-    assert dc.max() <= 1e-2 and dT.max() <= 1e-2, stats
+    assert dc.max() <= FLIP_ABS_CAP and dT.max() <= FLIP_ABS_CAP, stats
+    # and they stay rare among the borderline pixels (measured: 11 of 54 at cfg5, 3 of 10 at cfg3, 1 of 302 at cfg4)
+    assert stats["flips"] <= max(4, stats["borderline"] // 3), stats
     assert np.abs(c - c_ref).mean() <= 1e-7 and dT.mean() <= 1e-7, (np.abs(c - c_ref).mean(), dT.mean())
     return stats
 

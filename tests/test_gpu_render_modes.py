@@ -202,9 +202,9 @@ def test_render_save_ply_writes_the_frame(tmp_path, monkeypatch, offsets):
         out = render(cam, pc, default_pipe(), torch.zeros(3, device=DEV), save_ply=True)
     v = read_ply(str(tmp_path / "test_ply" / "point_cloud_250.ply"))
     col = lambda *ks: np.stack([v[k] for k in ks], 1)  # noqa: E731
-    assert np.array_equal(col("x", "y", "z"), out["means3D"].cpu().numpy())
-    assert np.array_equal(col("opacity"), out["opacities"].cpu().numpy())
-    assert np.array_equal(col("rot_0", "rot_1", "rot_2", "rot_3"), out["rotations"].cpu().numpy())
+    assert np.array_equal(col("x", "y", "z"), out["means3D"].detach().cpu().numpy())
+    assert np.array_equal(col("opacity"), out["opacities"].detach().cpu().numpy())
+    assert np.array_equal(col("rot_0", "rot_1", "rot_2", "rot_3"), out["rotations"].detach().cpu().numpy())
     assert np.array_equal(col("scale_0", "scale_1", "scale_2"), pc._scaling.detach().cpu().numpy())
     assert np.array_equal(col(*[f"f_rest_{3 * 15 - 15 + i}" for i in range(15)]),
                           pc._features_rest.detach()[:, :, 2].cpu().numpy())
