@@ -273,39 +273,6 @@ __device__ __forceinline__ float wave_sum8(const float (&c)[8]) {
     return t;
 }
 
-// Float adds into LDS by compare-and-swap.  ds_add_f32 runs at ~3 LDS cycles per LANE on gfx950 (192 cycles per
-// 64-lane instruction per CU, against 4-5 for ds_add_u32 or ds_write_b32: scripts/calib/lds_rate.hip), so a
-// float sum through it costs 40x an integer one.  A read + ds_cmpst_rtn_b32 pair, retried where another lane or
-// wave won the race, measured 13-17 cycles per 64-lane update with 16 waves per CU (39 with every wave on the same
-// addresses).  Three independent updates per lane go out together; a zero addend is skipped.  The order in which
-// concurrent adds land is the scheduler's, as with the atomics.
-__device__ __forceinline__ void lds_cas_add3(float* p0, float v0, float* p1, float v1, float* p2, float v2) {
-    uint32_t* u0 = reinterpret_cast<uint32_t*>(p0);
-    uint32_t* u1 = reinterpret_cast<uint32_t*>(p1);
-    uint32_t* u2 = reinterpret_cast<uint32_t*>(p2);
-    bool d0 = v0 == 0.f, d1 = v1 == 0.f, d2 = v2 == 0.f;
-    uint32_t o0 = d0 ? 0u : *reinterpret_cast<volatile uint32_t*>(u0);
-    uint32_t o1 = d1 ? 0u : *reinterpret_cast<volatile uint32_t*>(u1);
-    uint32_t o2 = d2 ? 0u : *reinterpret_cast<volatile uint32_t*>(u2);
-    while (!(d0 && d1 && d2)) {
-        if (!d0) {
-            const uint32_t q = atomicCAS(u0, o0, __float_as_uint(__uint_as_float(o0) + v0));
-            d0 = q == o0;
-            o0 = q;
-        }
-        if (!d1) {
-            const uint32_t q = atomicCAS(u1, o1, __float_as_uint(__uint_as_float(o1) + v1));
-            d1 = q == o1;
-            o1 = q;
-        }
-        if (!d2) {
-            const uint32_t q = atomicCAS(u2, o2, __float_as_uint(__uint_as_float(o2) + v2));
-            d2 = q == o2;
-            o2 = q;
-        }
-    }
-}
-
 // Capacity guard of a launch queued before num_rendered reached the host (gsd_rasterize_forward): true
 // when the count the tile scan wrote exceeds what the binning buffer holds -- the launch then does nothing
 // and the host re-runs it with a buffer of the right size.  One uniform (scalar) load per workgroup.

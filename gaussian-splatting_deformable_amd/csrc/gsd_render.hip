@@ -401,7 +401,9 @@ __device__ __forceinline__ int row_bcast_i(int v) {
     return __builtin_amdgcn_update_dpp(0, v, 0x150 + U, 0xf, 0xf, true);
 }
 
-__global__ __launch_bounds__(256) void k_render_bwd(RenderBwdParams p) {
+// The round-4 backward (one record list per wave, the 8x8 quadrant, float LDS atomics): kept for A/B against the
+// per-group kernel below (-DGSD_BWD_QUADRANT).
+__global__ __launch_bounds__(256) void k_render_bwd_quadrant(RenderBwdParams p) {
     __shared__ uint32_t s_id[kTilePix];
     // staged records (stage_pc), all at a 16-B stride: one LDS address per record serves the three reads
     __shared__ float4 s_pc[kTilePix];
@@ -666,14 +668,15 @@ __device__ __forceinline__ float tstep4(float a, float b) {
 // alpha < 1/255 at every pixel of the block (the same slack as the exact test: 0.1 % + 0.05 on 2 ln(255 o)).
 // Counted on the cfg4 scene (scripts/sim_bwd_lists.py): the wave then walks 0.708 of the per-quadrant lists' steps
 // (the exact ellipse test per block: 0.682, the alpha box alone: 0.817).
+template <int NB>
 __device__ __forceinline__ void bwd_compact_groups(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
-                                                   const float2* __restrict__ s_bo, uint8_t (*lists)[kTilePix], int n,
+                                                   const float2* __restrict__ s_bo, uint8_t (*lists)[NB], int n,
                                                    float qx0, float qy0, int lane, const int (&t_min)[4],
                                                    int (&cnt)[4]) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) cnt[g] = 0;
 #pragma unroll
-    for (int k = 0; k < kTilePix / 64; ++k) {
+    for (int k = 0; k < NB / 64; ++k) {
         const int t = k * 64 + lane;
         const bool in = t < n;
         const float4 bx = s_box[t];  // slots >= n hold stale values: every test below is masked by `in`
@@ -713,28 +716,37 @@ __device__ __forceinline__ void bwd_compact_groups(const float4* __restrict__ s_
 //   two transposed DPP steps inside the row (tstep8, tstep4: bank-masked moves, no selects) leave each lane two of
 //   the record's nine sums (and the ninth in the lanes with bits 3:2 clear): three LDS adds per lane and hand-off,
 //   as in the quadrant kernel, into the tile's accumulators.
-// LDS: 31.6 KB (the Gaussian ids of a batch wait in registers and go through the hand-off region for the flush), so
-// five workgroups per CU as before.
-// Round 5, measured at cfg4 (scripts/gpu_r5*.sh, profiles/round5/render_bwd/): 3.48M wave steps instead of 4.92M and
-// 0.545 useful lanes instead of 0.386 (GSD_COUNT_WORK), parity green -- but the accumulation bounds it.  Each (row,
-// record) pair now leaves nine sums (12.8M pairs instead of 4.9M (wave, record) pairs), and LDS float atomics cost
-// ~3 LDS cycles per lane on gfx950 (scripts/calib/lds_rate.hip): 0.735 ms with ds_add_f32, 0.489 with the
-// compare-and-swap adds below, 0.38 with plain stores in their place (timing only), against 0.48 for the quadrant
-// kernel.  Not the default (-DGSD_BWD_GROUPS); an accumulation at plain-store cost would make it 20 % faster.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_render_bwd_groups(RenderBwdParams p) {
-    __shared__ float4 s_pc[kTilePix];   // stage_pc: mx, my, -a/2, -c/2
-    __shared__ float2 s_bo[kTilePix];   // b, t_o
-    __shared__ float4 s_rgb[kTilePix];  // r, g, b, o
-    // record t's nine sums at [9 t + q]: an odd pitch, so the per-record accesses of a lane group (the flush's
-    // finishing step, phase 2's adds of consecutive slots) fall in distinct banks, and the flush reads it linearly
-    __shared__ float s_acc[kRecUsed * kTilePix];
-    __shared__ __attribute__((aligned(4))) uint8_t s_list[4][4][kTilePix];  // [wave][group][entry]
+//   The accumulators are doubles: each (row, record) pair leaves its own nine sums (12.8M pairs at cfg4, against
+//   4.9M (wave, record) pairs in the quadrant kernel), and on gfx950 ds_add_f32 costs ~3 LDS cycles per LANE (192 per
+//   64-lane instruction) while ds_add_f64 costs 8 per instruction (scripts/calib/lds_rate.hip).
+// LDS: 24.7 KB at 128-record batches (the Gaussian ids of a batch wait in registers and go through the hand-off
+// region for the flush); five waves per SIMD (the register limit).
+// Round 5, measured at cfg4 (profiles/round5/render_bwd/): 3.57M wave steps instead of 4.92M, 0.532 useful lanes
+// instead of 0.386 (GSD_COUNT_WORK), parity green; 0.398 ms against 0.477 for the quadrant kernel (-DGSD_BWD_QUADRANT).
+// Along the way: ds_add_f32 accumulators 0.735 ms, compare-and-swap float adds 0.489, plain stores in their place
+// (timing only) 0.38.
+// records staged per batch: the double accumulators below take 72 B per record, so 128 keep the workgroup's LDS at
+// 24.6 KB (five workgroups per CU, the register limit)
+constexpr int kGB = 128;
+#ifndef GSD_BWD_GROUPS_WAVES
+#define GSD_BWD_GROUPS_WAVES 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GROUPS_WAVES))) void k_render_bwd(
+    RenderBwdParams p) {
+    __shared__ float4 s_pc[kGB];   // stage_pc: mx, my, -a/2, -c/2
+    __shared__ float2 s_bo[kGB];   // b, t_o
+    __shared__ float4 s_rgb[kGB];  // r, g, b, o
+    // record t's nine sums at [9 t + q], in double: ds_add_f64 costs 8 LDS cycles per 64-lane instruction on gfx950
+    // against 192 for ds_add_f32 (scripts/calib/lds_rate.hip); the odd pitch spreads a lane group's per-record
+    // accesses over the banks, and the flush reads it linearly
+    __shared__ double s_acc[kRecUsed * kGB];
+    __shared__ __attribute__((aligned(4))) uint8_t s_list[4][4][kGB];  // [wave][group][entry]
     // the alpha boxes are read by the compaction only, the hand-off buffer by the walk only, the Gaussian ids by
     // the flush only (barriers apart)
     __shared__ union {
-        float4 box[kTilePix];
+        float4 box[kGB];
         float2 qa[4][kBwdGroup][65];  // per wave: per record and pixel; +1 pad
-        uint32_t id[kTilePix];
+        uint32_t id[kGB];
     } s_u;
     __shared__ int s_tile_lc;
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);  // the forward's 4x4-group lane map
@@ -764,7 +776,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     lds_barrier();
     const int total = min((int)(rg.y - rg.x), s_tile_lc);
     const uint32_t end = rg.x + (uint32_t)total;
-    const int rounds = (total + kTilePix - 1) / kTilePix;
+    const int rounds = (total + kGB - 1) / kGB;
     int toDo = total;
     float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f;
     if (inside) {
@@ -795,11 +807,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     // member where bit 3 is clear, tstep4 where bit 2 is clear)
     const int qsel = ((lane >> 3) & 1) | ((lane >> 1) & 2);
 
-    for (int i = 0; i < rounds; ++i, toDo -= kTilePix) {
+    for (int i = 0; i < rounds; ++i, toDo -= kGB) {
         lds_barrier();
-        const int progress = i * kTilePix + tid;
+        const int progress = i * kGB + tid;
         uint32_t gid = 0;
-        if (progress < total) {  // loaded back to front (backward.cu:466-478)
+        if (tid < kGB && progress < total) {  // loaded back to front (backward.cu:466-478)
             gid = p.point_list[end - progress - 1];
             const RenderRec* r = p.rec + gid;
             const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
@@ -808,16 +820,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q1.y);  // r, g, b, o
             s_u.box[tid] = r->box;
         }
-#pragma unroll
-        for (int q = 0; q < kRecUsed; ++q) s_acc[q * kTilePix + tid] = 0.f;
+        for (int e = tid; e < kRecUsed * kGB; e += kTilePix) s_acc[e] = 0.0;
         lds_barrier();
-        const int n = min(kTilePix, toDo);
-        // slot t of this batch is list position (total - 1 - i*256 - t) counted from the front
-        const int front_base = total - 1 - i * kTilePix;
+        const int n = min(kGB, toDo);
+        // slot t of this batch is list position (total - 1 - i*kGB - t) counted from the front
+        const int front_base = total - 1 - i * kGB;
         int t_min[4], cnt[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) t_min[g] = front_base - glc[g] + 1;
-        bwd_compact_groups(s_u.box, s_pc, s_bo, s_list[tg.wave], n, tg.qx0, tg.qy0, lane, t_min, cnt);
+        bwd_compact_groups<kGB>(s_u.box, s_pc, s_bo, s_list[tg.wave], n, tg.qx0, tg.qy0, lane, t_min, cnt);
         const int m = max(max(cnt[0], cnt[1]), max(cnt[2], cnt[3]));  // the longest list (wave-uniform)
         const int mine = grp == 0 ? cnt[0] : grp == 1 ? cnt[1] : grp == 2 ? cnt[2] : cnt[3];
         // backward.cu:487-488: a pixel replays list position front_base - t only below its last contributor, i.e.
@@ -843,7 +854,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     const bool own = K + r < nvm;
                     const int rs = own ? (int)my_list[j0 + K + r] : 0;
                     const float2 mrec = *reinterpret_cast<const float2*>(&s_pc[rs]);
-                    float* acc = s_acc + kRecUsed * rs;
+                    double* acc = s_acc + kRecUsed * rs;
                     unsigned long long any_m = 0;  // lanes that took any record of the hand-off
                     auto rec = [&](auto uc) {
                         constexpr int U = K + decltype(uc)::value;
@@ -910,8 +921,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     const float cb = tstep4(tstep8(Myy, S0), tstep8(C0, C1));
                     const float c2 = sum4(sum8(C2));
                     wave_lds_handoff();  // phase-1 writes of the next hand-off must stay behind these reads
-                    if (own) {  // the record's sums into the tile's accumulators (compare-and-swap float adds)
-                        lds_cas_add3(acc + qsel, ca, acc + 4 + qsel, cb, acc + 8, (lane & 12) ? 0.f : c2);
+                    if (own) {  // the record's sums into the tile's accumulators (ds_add_f64)
+                        atomicAdd(acc + qsel, (double)ca);
+                        atomicAdd(acc + 4 + qsel, (double)cb);
+                        if (!(lane & 12)) atomicAdd(acc + 8, (double)c2);
                     }
                 };
                 hand_off(std::integral_constant<int, 0>{});
@@ -927,18 +940,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
             const float4 pc = s_pc[tid];
-            const float b = s_bo[tid].x;
+            const double b = s_bo[tid].x;
             const float o = s_rgb[tid].w;  // the sums are over q = o G dL/dalpha; dL/dopacity = sum G dL/dalpha = S0 / o
-            const float a = -2.f * pc.z, c = -2.f * pc.w;  // exact
-            float* acc = s_acc + kRecUsed * tid;
+            const double a = -2.f * pc.z, c = -2.f * pc.w;  // exact
+            double* acc = s_acc + kRecUsed * tid;
             // phase 2 summed the first moments over x - mx, y - my: the reference's dx = mx - x flips them
-            const float m0 = -acc[0], m1 = -acc[1];
-            acc[0] = (a * m0 + b * m1) * -ddelx_dx;
-            acc[1] = (c * m1 + b * m0) * -ddely_dy;
-            acc[2] *= -0.5f;
-            acc[3] *= -0.5f;
-            acc[4] *= -0.5f;
-            acc[5] = o > 0.f ? acc[5] / o : 0.f;  // o = 0: alpha = 0, the record never took a pixel
+            const double m0 = -acc[0], m1 = -acc[1];
+            acc[0] = (a * m0 + b * m1) * -(double)ddelx_dx;
+            acc[1] = (c * m1 + b * m0) * -(double)ddely_dy;
+            acc[2] *= -0.5;
+            acc[3] *= -0.5;
+            acc[4] *= -0.5;
+            acc[5] = o > 0.f ? acc[5] / (double)o : 0.0;  // o = 0: alpha = 0, the record never took a pixel
             s_u.id[tid] = gid;
         }
         lds_barrier();
@@ -946,7 +959,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         // each inside one 64-B segment of its Gaussian's gradient record.
         for (int e = tid; e < n * kRecUsed; e += kTilePix) {
             const int r = e / kRecUsed, q = e - kRecUsed * r;
-            const float a = s_acc[e];
+            const float a = (float)s_acc[e];
             if (a != 0.f) atomicAdd(p.grad_rec + (size_t)s_u.id[r] * kGradRec + q, a);
         }
     }
@@ -959,8 +972,8 @@ void launch_render_fwd(const RenderParams& p, hipStream_t s) {
     if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_fwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 }
 void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
-#ifdef GSD_BWD_GROUPS
-    if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd_groups, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+#ifdef GSD_BWD_QUADRANT
+    if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd_quadrant, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 #else
     if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 #endif

@@ -158,7 +158,7 @@ typedef struct gsd_raster_args {
 int gsd_abi_version(void);
 const char* gsd_last_error(void);
 /* ABI 16, build provenance (no reference counterpart): the SHA-256 (64 hex digits) of the sources this library
- * was compiled from -- csrc/*.hip and csrc/*.h in name order, this header, csrc/Makefile -- and the extra compiler
+ * was compiled from -- the csrc .hip and .h sources in name order, this header, csrc/Makefile -- and the extra compiler
  * flags of the build (HIPFLAGS_EXTRA, "" for the product build).  gsd_amd/_native.py recomputes the hash from its
  * tree and refuses a library built from other sources. */
 const char* gsd_build_id(void);

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Load balance of k_render_bwd's four waves (one 8x8 quadrant each) on the bench workload: per 256-record
+"""Load balance of k_render_bwd_quadrant's four waves (one 8x8 quadrant each) on the bench workload: per 256-record
 batch every wave walks its own compacted list, and the workgroup's barrier after the batch makes the three
 shorter waves wait for the longest.  Counts, from the forward's state (alpha-box test only, the backward's
 exact-ellipse test trims ~11 % more), sum over batches of max-over-waves vs mean-over-waves list length.

@@ -12,6 +12,8 @@
 //       8 float add by compare-and-swap (ds_read_b32 + ds_cmpst_rtn_b32, retried on a lost race), 64 lanes distinct
 //       9 the same, every wave of the workgroup on the same 64 dwords (races between waves)
 //      10 three independent CAS adds per lane in flight together (the kernel's three quantities per hand-off)
+//      11 ds_add_f64, 64 lanes distinct 8-B words          12 ds_add_u64, 64 lanes distinct
+//      13 ds_add_rtn_f32, 64 lanes distinct                14 ds_write_b64, 64 lanes distinct
 template <int MODE>
 __global__ __launch_bounds__(256) void k(float* out, int iters, unsigned long long* clk) {
     __shared__ float s[8192];
@@ -26,6 +28,7 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, unsigned long lo
     else addr = 4u * (wave * 64 + lane);
     const float one = 1.0f;
     const unsigned ione = 1u;
+    float sink = 0.f;
     if (MODE != 2 || lane < 16) {
         for (int it = 0; it < iters; ++it) {
 #pragma unroll
@@ -34,6 +37,14 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, unsigned long lo
                     asm volatile("ds_add_f32 %0, %1" ::"v"(addr), "v"(one) : "memory");
                 if (MODE == 1) asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(one) : "memory");
                 if (MODE == 4) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(ione) : "memory");
+                if (MODE == 11) asm volatile("ds_add_f64 %0, %1" ::"v"(addr * 2), "v"(1.0) : "memory");
+                if (MODE == 12) asm volatile("ds_add_u64 %0, %1" ::"v"(addr * 2), "v"(1ull) : "memory");
+                if (MODE == 13) {
+                    float r;
+                    asm volatile("ds_add_rtn_f32 %0, %1, %2" : "=v"(r) : "v"(addr), "v"(one) : "memory");
+                    sink += r;
+                }
+                if (MODE == 14) asm volatile("ds_write_b64 %0, %1" ::"v"(addr * 2), "v"(1ull) : "memory");
                 if (MODE == 8 || MODE == 9) {
                     unsigned* p = reinterpret_cast<unsigned*>(s) + addr / 4;
                     unsigned old = *reinterpret_cast<volatile unsigned*>(p);
@@ -65,7 +76,7 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, unsigned long lo
         clk[0] = __builtin_amdgcn_s_memtime() - c0;
         clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
     }
-    out[blockIdx.x * 256 + threadIdx.x] = s[threadIdx.x];
+    out[blockIdx.x * 256 + threadIdx.x] = s[threadIdx.x] + sink;
 }
 
 static unsigned long long* g_clk;
@@ -107,6 +118,10 @@ int main() {
         run<8>("CAS float add 64 lanes distinct", out, w, iters);
         run<9>("CAS float add, every wave same 64", out, w, iters);
         run<10>("3 CAS float adds in flight, distinct", out, w, iters);
+        run<11>("ds_add_f64 64 lanes distinct", out, w, iters);
+        run<12>("ds_add_u64 64 lanes distinct", out, w, iters);
+        run<13>("ds_add_rtn_f32 64 lanes distinct", out, w, iters);
+        run<14>("ds_write_b64 64 lanes distinct", out, w, iters);
     }
     return 0;
 }

@@ -11,7 +11,7 @@ sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting_deformable_amd"), ROOT]
 import torch  # noqa: E402
 
 from bench import make_optimizer  # noqa: E402
-from gsd_amd import DeformableGaussians, default_pipe, l1_ssim_loss, render  # noqa: E402
+from gsd_amd import DeformableGaussians, default_pipe, render, training_loss  # noqa: E402
 from gsd_amd.camera import synthetic_camera  # noqa: E402
 from gsd_amd.scene import CONFIGS, make_gaussians  # noqa: E402
 
@@ -25,15 +25,14 @@ pipe = default_pipe()
 with torch.no_grad():
     target = render(cam, pc, pipe, bg)["render"].clone()
 opt = make_optimizer(pc)
-flat = opt.flat
+seed = torch.ones((), device=dev)
 
 
-def step():
+def step():   # bench.py's fused N = 1 step
     out = render(cam, pc, pipe, bg)
-    loss = l1_ssim_loss(out["render"], target, 0.2)
-    loss.backward()
-    flat.allreduce()
-    opt.step(zero_grad=True)
+    loss = training_loss(out["render"], target, out["means3D_offset"], 0.2)
+    with opt.step_in_backward():
+        loss.backward(seed)
 
 
 for _ in range(10):
@@ -46,4 +45,5 @@ for _ in range(50):
 torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(25)
+st.sort_stats("tottime").print_stats(40)
+st.sort_stats("cumulative").print_stats(40)

@@ -36,6 +36,8 @@ def ellipse_min_q(mx, my, a, b, c, x0, x1, y0, y1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=256, help="records staged per batch")
+    ap.add_argument("--chunks", action="store_true", help="also the union-chunked walks")
     a = ap.parse_args()
     from conftest import oracle_kwargs, scene_inputs
     from gsd_amd.scene import CONFIGS
@@ -63,7 +65,7 @@ def main():
     total = np.minimum(ranges[:, 1] - ranges[:, 0], tile_lc)
     keep = pos < total[tile_of]
     tile_of, pos, g = tile_of[keep], pos[keep], pl[keep]
-    batch = (total[tile_of] - 1 - pos) // 256
+    batch = (total[tile_of] - 1 - pos) // a.batch
     co = o["conic_opacity"].astype(np.float64)[g]
     m2 = o["means2D"].astype(np.float64)[g]
     A, B, C, O = co[:, 0], co[:, 1], co[:, 2], co[:, 3]
@@ -154,7 +156,7 @@ def main():
         return steps
 
     C_ = C
-    for Cc in (4, 8, 16, 32):
+    for Cc in ((4, 8, 16, 32) if a.chunks else ()):
         print(f"per-row lists in union chunks of {Cc}: wave steps {count_chunked(Cc)}")
     base = None
     for rw, rh, test in [(8, 8, "exact"), (4, 4, "linear")]:
