@@ -32,8 +32,7 @@
 // MFMAs, 4 the fused forward's activation stores, 8 its MFMAs, 16 the weight-gradient MFMAs, 64 the fused forward's
 // weight copies, 128 the GEMM's copies, 256 the fused forward's per-k-step wait + barrier, 512 five of its six
 // copies per k-step, 2048 the fused forward's weight copies through registers
-// (a load one k-step ahead, then a ds_write; results exact), 4096 k_mlp_wgrad_dma's copies after the first pair, 8192
-// its three-term splits (the hi plane only).  The results are then garbage; the durations say what each part costs.
+// (a load one k-step ahead, then a ds_write; results exact).  The results are then garbage; the durations say what each part costs.
 #ifndef GSD_ABLATE
 #define GSD_ABLATE 0
 #endif
@@ -59,16 +58,6 @@ __device__ __forceinline__ Split8 split8(const float (&v)[8]) {
         s.mid[j] = m;
         s.lo[j] = (__bf16)r2;
     }
-    return s;
-}
-
-// (ablation only, GSD_ABLATE & 8192: the hi plane alone, copied into all three)
-__device__ __forceinline__ Split8 split8_hi(const float (&v)[8]) {
-    Split8 s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s.hi[j] = (__bf16)v[j];
-    s.mid = s.hi;
-    s.lo = s.hi;
     return s;
 }
 
@@ -1232,151 +1221,6 @@ void k_mlp_wgrad(MlpWgradParams p) {
     }
 }
 
-// ---- dW = G X^T with the operands copied by LDS-DMA (round 5; the 256 x 256 layers) ----
-// k_mlp_wgrad stages through registers: its loads have one 16-Gaussian step (~1.6 us) to land, and the split planes
-// it writes to LDS are read again by every wave.  Here the workgroup copies, per 32-Gaussian pair of k-steps, the 32
-// Gaussians of every G and X row -- one 128-B line per row -- global -> LDS with global_load_lds_dwordx4 into one of
-// two slots, a whole pair (two k-steps of MFMAs) ahead; each wave reads its fragments from there as f32 (two
-// ds_read_b128 per fragment) and splits them in registers, as k_mlp_gemm_dma does its activation operand.  A copy
-// instruction moves eight rows: lane L fetches 16-B chunk (L & 7) ^ (L >> 3) of row 8 i + (L >> 3), so LDS holds
-// chunk q of row r at position q ^ (r & 7) and the eight lanes of a b128 read pass (eight consecutive rows, one
-// chunk index) hit eight different bank groups.  The bias gradient's row sums come from the waves holding the G
-// fragments in f32 (tk = 0).  One workgroup per CU (2 x 64 KB of LDS), eight waves of 4 x 2 blocks (two per SIMD).
-// No masking past P: the last pair of the last chunk reads the padded columns [P, ldp), where the backward's gradient
-// rows are exactly zero (the chain kernel and the GEMM path both take the heads' gradients as zero there) and the
-// activation rows finite (the encoding of zeros), so those Gaussians add exact zeros to every sum.
-template <int NRB, int KRB, int TNB, int TKB>
-struct WgradDma {
-    static constexpr int TN = NRB / TNB, TK = KRB / TKB, WAVES = TN * TK;
-    static constexpr int ROWS = 32 * (NRB + KRB);          // G rows, then X rows
-    static constexpr int kCopies = ROWS / 8;               // 1-KB copies per pair (eight 128-B rows each)
-    static constexpr int kPerWave = kCopies / WAVES;
-    static constexpr int kSlot = ROWS * 128;
-    static_assert(TN * TNB == NRB && TK * TKB == KRB && kCopies % WAVES == 0, "wgrad dma tiling");
-    static_assert(2 * kSlot <= 160 * 1024, "two slots of LDS");
-};
-
-// IL: the six products of each block pair issued product-major across the wave's blocks (consecutive MFMAs
-// independent) instead of block by block
-template <int NRB, int KRB, int TNB, int TKB, bool IL, bool WAVES_LAG = true>
-__global__ __launch_bounds__(64 * ((NRB / TNB) * (KRB / TKB))) void k_mlp_wgrad_dma(MlpWgradParams p) {
-    typedef WgradDma<NRB, KRB, TNB, TKB> S;
-    __shared__ __attribute__((aligned(16))) unsigned char s_mem[2 * S::kSlot];
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, c = lane & 31, wave = tid >> 6;
-    const int tn = wave / S::TK, tk = wave % S::TK;
-    const int p_lo = blockIdx.x * p.chunk, p_hi = min(p.P, p_lo + p.chunk);
-    const int npairs = (p_hi - p_lo + 31) / 32;   // >= 1: the launch has no empty chunk
-    // this wave's copies j: rows 8 (wave + WAVES j) + (lane >> 3), 16-B chunk (lane & 7) ^ (lane >> 3) of each
-    // (recomputed per copy: a few integer ops per pair instead of 2 x kPerWave registers held through the loop)
-    auto src = [&](int j, int pm) -> const float* {
-        const int r = 8 * (wave + S::WAVES * j) + (lane >> 3);
-        const int q = (lane & 7) ^ (lane >> 3);
-        const float* base;
-        if (r < 32 * NRB) base = p.G + (size_t)r * p.ldp;
-        else {
-            const int k = r - 32 * NRB;
-            base = k < 32 * p.k_rb0 ? p.X0 + (size_t)k * p.ldp : p.X1 + (size_t)(k - 32 * p.k_rb0) * p.ldp;
-        }
-        return base + pm + 4 * q;   // reads stay below ldp: chunks start on 32-Gaussian boundaries
-    };
-    const unsigned lds0 = lds_addr(s_mem);
-    f32x16 acc[TNB][TKB];
-#pragma unroll
-    for (int i = 0; i < TNB; ++i)
-#pragma unroll
-        for (int j = 0; j < TKB; ++j) acc[i][j] = f32x16{};
-    float bsum[TNB];
-#pragma unroll
-    for (int i = 0; i < TNB; ++i) bsum[i] = 0.f;
-#pragma unroll
-    for (int j = 0; j < S::kPerWave; ++j)
-        dma16_asm(src(j, p_lo), __builtin_amdgcn_readfirstlane(lds0 + (wave + S::WAVES * j) * 1024));
-    Split8 a[TNB], b[TKB];
-    // k-step s of the pair in slot sb -> the wave's split fragments (and, for tk = 0, the bias rows' sums)
-    auto read_split = [&](const unsigned char* sb, int s) {
-        const int q0 = (4 * s + 2 * h) ^ (c & 7);   // position of chunk 4 s + 2 h in rows r = c (mod 8)
-        auto load8 = [&](int r, float (&v)[8]) {
-            const float4* row = reinterpret_cast<const float4*>(sb + r * 128);
-            const float4 x0 = row[q0], x1 = row[q0 ^ 1];
-            v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-        };
-#pragma unroll
-        for (int i = 0; i < TNB; ++i) {
-            float v[8];
-            load8(32 * (TNB * tn + i) + c, v);
-            if (tk == 0) bsum[i] += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-            a[i] = (GSD_ABLATE & 8192) ? split8_hi(v) : split8(v);
-        }
-#pragma unroll
-        for (int j = 0; j < TKB; ++j) {
-            float v[8];
-            load8(32 * NRB + 32 * (TKB * tk + j) + c, v);
-            b[j] = (GSD_ABLATE & 8192) ? split8_hi(v) : split8(v);
-        }
-    };
-    auto mma = [&] {
-        if constexpr (IL && !(GSD_ABLATE & 16)) {
-#define GSD_WG_PART(M)                                                                                          \
-    _Pragma("unroll") for (int i = 0; i < TNB; ++i)                                                             \
-        _Pragma("unroll") for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6_part<M>(a[i], b[j], acc[i][j]);
-            GSD_WG_PART(0) GSD_WG_PART(1) GSD_WG_PART(2) GSD_WG_PART(3) GSD_WG_PART(4) GSD_WG_PART(5)
-#undef GSD_WG_PART
-        } else {
-#pragma unroll
-            for (int i = 0; i < TNB; ++i)
-#pragma unroll
-                for (int j = 0; j < TKB; ++j) acc[i][j] = mfma_x6_abl<GSD_ABLATE & 16>(a[i], b[j], acc[i][j]);
-        }
-    };
-    // The two waves of a SIMD (w and w + 4) take each k-step's phases in opposite orders: the first reads and splits
-    // k-step s, then multiplies it; the second multiplies k-step s - 1 (its fragments held in registers across the
-    // barrier), then reads and splits k-step s -- so one's split VALU runs beside the other's MFMAs instead of both
-    // splitting, then both multiplying.
-    const bool lag = WAVES_LAG && (wave & 4);
-    for (int m = 0; m < npairs; ++m) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's copies of pair m landed ...
-        raw_barrier();                                      // ... every wave's, and every wave is done with pair m - 1
-        if (m + 1 < npairs && !(GSD_ABLATE & 4096)) {      // pair m + 1 into the slot pair m - 1 was read from
-#pragma unroll
-            for (int j = 0; j < S::kPerWave; ++j)
-                dma16_asm(src(j, p_lo + 32 * (m + 1)),
-                          __builtin_amdgcn_readfirstlane(lds0 + ((m + 1) & 1) * S::kSlot + (wave + S::WAVES * j) * 1024));
-        }
-        const unsigned char* sb = s_mem + (m & 1) * S::kSlot;
-        if (!lag) {
-            read_split(sb, 0);
-            mma();
-            read_split(sb, 1);
-            mma();
-        } else {
-            if (m > 0) mma();
-            read_split(sb, 0);
-            mma();
-            read_split(sb, 1);
-        }
-    }
-    if (lag) mma();
-    // partial[chunk][n][k], n = 32 (TNB tn + i) + 8 (q >> 2) + 4 h + (q & 3), k = 32 (TKB tk + j) + c
-    float* out = p.partial + (size_t)blockIdx.x * (32 * NRB) * (32 * KRB);
-#pragma unroll
-    for (int i = 0; i < TNB; ++i)
-#pragma unroll
-        for (int j = 0; j < TKB; ++j)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int n = 32 * (TNB * tn + i) + 8 * (q >> 2) + 4 * h + (q & 3);
-                const int k = 32 * (TKB * tk + j) + c;
-                out[(size_t)n * (32 * KRB) + k] = acc[i][j][q];
-            }
-    if (tk == 0) {   // the bias gradient: row 32 (TNB tn + i) + c's sum over this chunk (its two k-halves combined)
-#pragma unroll
-        for (int i = 0; i < TNB; ++i) {
-            const float t = bsum[i] + __shfl_xor(bsum[i], 32);
-            if (h == 0) p.bias_partial[(size_t)blockIdx.x * (32 * NRB) + 32 * (TNB * tn + i) + c] = t;
-        }
-    }
-}
-
 // dW[n][k] = sum over the chunks of partial[chunk][n][k], in a fixed order (deterministic), scattered into the
 // reference-shaped pieces (padded columns and rows dropped); in the same launch the bias gradient likewise (the first
 // b_blocks workgroups, dispatched first: eight workgroups, each a 489-deep chain of loads, took ~9.5 us in a launch
@@ -1472,25 +1316,18 @@ void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s) {
 
 void launch_mlp_wgrad(const MlpWgradParams& p_in, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s) {
     MlpWgradParams p = p_in;
-    // 256 x 256 by LDS-DMA (k_mlp_wgrad_dma, GSD_WGRAD_DMA=8 etc.; measured slower so far): one workgroup per CU, so the chunk
-    // grows to cover P in one round of 256 workgroups -- never past the caller's chunk count (its partial buffers)
-    static const int dma = [] {   // 8: eight waves of 4 x 2 blocks; 80: the same block by block; 16: sixteen of
-        const char* e = getenv("GSD_WGRAD_DMA");   // 2 x 2; 4: four of 4 x 4; unset / 0: k_mlp_wgrad (A/B)
-        return e ? atoi(e) : 0;
+    // 256 x 256: one workgroup per CU (114 KB of LDS), so the chunk grows to cover P in ONE round of 256 workgroups
+    // (never past the caller's chunk count, which sizes the partial buffers): 0.732 -> 0.708 ms per layer at 1M (no
+    // second, 91 %-full round) and its reduction over 255 partials instead of 489, ~9 us instead of ~24
+    // (profiles/round5/deform_mlp_wgrad/; GSD_WGRAD_ROUND1=0 keeps the 2048-Gaussian chunks)
+    static const bool round1 = [] {
+        const char* e = getenv("GSD_WGRAD_ROUND1");
+        return !(e && strcmp(e, "0") == 0);
     }();
-    const bool use_dma = dma != 0 && p.n_rb == 8 && p.k_rb == 8;
-    if (use_dma) p.chunk = std::max(p.chunk, (int)(((long long)p.P + 256 * 32 - 1) / (256 * 32)) * 32);
+    if (round1 && p.n_rb == 8 && p.k_rb == 8)
+        p.chunk = std::max(p.chunk, (int)(((long long)p.P + 256 * 32 - 1) / (256 * 32)) * 32);
     const int n_chunks = (p.P + p.chunk - 1) / p.chunk;
     const dim3 grid(n_chunks);
-    if (use_dma) {
-#define GSD_WGD(TN, TK, IL) \
-    hipLaunchKernelGGL((k_mlp_wgrad_dma<8, 8, TN, TK, IL>), grid, dim3(64 * WgradDma<8, 8, TN, TK>::WAVES), 0, s, p)
-        if (dma == 16) GSD_WGD(2, 2, true);
-        else if (dma == 4) GSD_WGD(4, 4, true);
-        else if (dma == 80) GSD_WGD(4, 2, false);
-        else GSD_WGD(4, 2, true);
-#undef GSD_WGD
-    } else {
 #define GSD_WGRAD(N, K, TN, TK)                                                                            \
     if (p.n_rb == N && p.k_rb == K)                                                                        \
         hipLaunchKernelGGL((k_mlp_wgrad<N, K, TN, TK>), grid, dim3(64 * WgradShape<N, K, TN, TK>::WAVES), 0, s, p);
@@ -1511,7 +1348,6 @@ void launch_mlp_wgrad(const MlpWgradParams& p_in, const MlpWeightRef& dst, const
     else GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 2, 2, 1) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 3)
     else GSD_WGRAD(2, 8, 1, 2)
 #undef GSD_WGRAD
-    }
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
     const int w_blocks = (int)((nw + 31) / 32), b_blocks = p.skip_bias ? 0 : (32 * p.n_rb + 31) / 32;
     const WgradReduceJob wj{32 * p.n_rb, 32 * p.k_rb, p.k_off, (const float*)p.partial, dst};

@@ -12,5 +12,5 @@ run() {   # name, then env assignments
   local f; f=$(find "$O/prof_$name" -name '*kernel_stats.csv' | head -1)
   echo "== $name"; grep -i "wgrad" "$f" | cut -d, -f1-4
 }
-run dma8 GSD_WGRAD_DMA=8 && run dma80 GSD_WGRAD_DMA=80 && run dma4 GSD_WGRAD_DMA=4 && run dma16 GSD_WGRAD_DMA=16 && \
-run old GSD_WGRAD_DMA=0 && run dma4b GSD_WGRAD_DMA=4 && echo all-done
+run dma8 GSD_WGRAD_DMA=8 && run dma80 GSD_WGRAD_DMA=80 && run dma4 GSD_WGRAD_DMA=4 && run round1 GSD_WGRAD_DMA=0 GSD_WGRAD_ROUND1=1 && \
+run old GSD_WGRAD_DMA=0 && run dma16 GSD_WGRAD_DMA=16 && run round1b GSD_WGRAD_DMA=0 GSD_WGRAD_ROUND1=1 && echo all-done

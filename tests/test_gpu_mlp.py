@@ -254,6 +254,48 @@ def test_train_f32_matches_float64_oracle_like_torch_f32(P, scale):
         assert e_hip <= max(2e-5, 2.0 * e_torch), (name, e_hip, e_torch)
 
 
+def test_train_f32_large_p_weight_gradients_match_torch_f32():
+    """Above 524,288 Gaussians the 256 x 256 weight gradients run in one round of 256 chunks of > 2048 Gaussians
+    (launch_mlp_wgrad, round 5) -- a size the float64-oracle test above cannot reach on the CPU.  Against torch's f32
+    GEMMs at P = 600,001: the four heads and the 24 parameter gradients within 1e-4 of each tensor's scale.  ReLU ties
+    (a pre-activation within f32 rounding of 0 takes different masks in two correct f32 evaluations, moving that
+    Gaussian's whole contribution) are kept out as in test_mlp_training_backward_matches_reference_torch_path: the
+    Gaussians with a pre-activation within 1e-5 of its layer's scale (found in float64) get no upstream gradient.
+    dL/dx is per Gaussian and is covered by the float64-oracle test."""
+    import torch.nn.functional as F
+
+    from gsd_amd.deform_mlp import DirectTemporalNeRF, positional_encoding
+    P = 600_001
+    torch.manual_seed(3)
+    net = DirectTemporalNeRF().cuda()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.rand(P, 3, device="cuda", generator=g) * 4 - 2
+    t = torch.full((P, 1), 0.6, device="cuda")
+    w = [torch.randn(P, n, device="cuda", generator=g) for n in (3, 3, 4, 48)]
+    with torch.no_grad():   # the ReLU ties, from a float64 evaluation of the hidden layers
+        xd, td = x.double(), t.double()
+        ex = positional_encoding(xd)
+        h = torch.cat((ex, positional_encoding(td)), -1)
+        tie = torch.zeros(P, dtype=torch.bool, device="cuda")
+        for i, layer in enumerate(net._time):
+            a = F.linear(h, layer.weight.double(), layer.bias.double())
+            tie |= (a.abs() < 1e-5 * float(a.abs().max())).any(-1)
+            h = F.relu(a)
+            if i in net.skips:
+                h = torch.cat((ex, h), -1)
+        del h, a, ex
+    assert int(tie.sum()) < P // 10
+    w = [wi * (~tie)[:, None] for wi in w]
+    hip = _train_run(net, x, t, w, False)
+    tor = _train_run(net, x, t, w, True)
+    names = ["out", "x"] + [k for k, _ in net.named_parameters()]
+    for name, h_, r in zip(names, [hip[0]] + hip[1], [tor[0]] + tor[1]):
+        if name == "x":
+            continue
+        e = float((h_ - r).abs().max()) / max(float(r.abs().max()), 1e-30)
+        assert e <= 1e-4, (name, e)
+
+
 def test_train_f32_matches_reference_network_fixture():
     """The HIP f32 training path against the reference's own DirectTemporalNeRF run (tests/golden/mlp.npz:
     gaussian_model.py:242-316 with a seeded init, float32 forward + autograd on the CPU): the four heads, dL/dx and
@@ -429,15 +471,16 @@ def test_eval_f32_matches_reference_network_fixture():
 def test_train_f32_fallback_kernels():
     """The comparison paths kept beside the defaults -- the per-layer GEMM forward (GSD_MLP_FWD=gemm), the per-layer
     dX GEMMs instead of the chain (GSD_MLP_BWD=gemm, which also sizes the workspace without the chain's gradient
-    buffers) and the eight-wave weight gradient (GSD_WGRAD16=0) -- read their switches once per process, so they run
-    here in a child pytest over the float64-oracle, fixture and in-place/unused-heads tests."""
+    buffers), the eight-wave weight gradient (GSD_WGRAD16=0) and the 2048-Gaussian chunks at every size
+    (GSD_WGRAD_ROUND1=0) -- read their switches once per process, so they run here in a child pytest over the
+    float64-oracle, fixture, in-place/unused-heads and large-P tests."""
     import subprocess
     import sys
-    env = dict(os.environ, GSD_MLP_FWD="gemm", GSD_MLP_BWD="gemm", GSD_WGRAD16="0")
+    env = dict(os.environ, GSD_MLP_FWD="gemm", GSD_MLP_BWD="gemm", GSD_WGRAD16="0", GSD_WGRAD_ROUND1="0")
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
                         os.path.join(here, "test_gpu_mlp.py"), "-k",
-                        "train_f32_matches_float64 or train_f32_matches_reference or inplace_gradients"],
+                        "train_f32_matches_float64 or train_f32_matches_reference or inplace_gradients or large_p"],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout and "failed" not in r.stdout
