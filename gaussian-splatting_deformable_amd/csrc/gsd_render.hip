@@ -34,6 +34,12 @@
 
 namespace gsd {
 
+// GSD_BWD_ABLATE (k_render_bwd timing-only builds, wrong results): 1 no phase 2, 2 no LDS accumulation, 4 no global
+// flush, 8 no walk
+#ifndef GSD_BWD_ABLATE
+#define GSD_BWD_ABLATE 0
+#endif
+
 #ifdef GSD_COUNT_WORK
 // gsd_work_counters (include/gsd_raster.h): fwd steps, fwd pairs, bwd steps, bwd pairs
 __device__ unsigned long long g_work[4];
@@ -893,6 +899,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                     rec(std::integral_constant<int, 2>{});
                     rec(std::integral_constant<int, 3>{});
                     if (!any_m) return;  // wave-uniform: no pixel took any of these records
+#if GSD_BWD_ABLATE & 1
+                    return;  // timing only: no phase 2
+#endif
                     wave_lds_handoff();
                     // Phase 2 (record-major), as in the quadrant kernel: lane 4 G + r sums its row's record K + r over
                     // the four pixels of its quad, (x0 + i, y0), i = 0..3, from the moments S0 = sum v,
@@ -921,6 +930,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                     const float cb = tstep4(tstep8(Myy, S0), tstep8(C0, C1));
                     const float c2 = sum4(sum8(C2));
                     wave_lds_handoff();  // phase-1 writes of the next hand-off must stay behind these reads
+#if GSD_BWD_ABLATE & 2
+                    if (own && ca == 12345.f && cb == 0.5f && c2 == 0.25f) acc[0] = 1.0;  // timing only: no accumulation
+                    return;
+#endif
                     if (own) {  // the record's sums into the tile's accumulators (ds_add_f64)
                         atomicAdd(acc + qsel, (double)ca);
                         atomicAdd(acc + 4 + qsel, (double)cb);
@@ -933,10 +946,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                 if (nv > 12) hand_off(std::integral_constant<int, 12>{});
             }
         };
+#if !(GSD_BWD_ABLATE & 8)
         if (any_bg)
             walk(std::true_type{});
         else
             walk(std::false_type{});
+#else
+        if (m == 12345 && mine == 7 && t_cut == 3) walk(std::false_type{});  // timing only: no walk
+#endif
         lds_barrier();
         if (tid < n) {  // finish record tid's sums in place: moments -> dL/dmean2D, the constant factors
             const float4 pc = s_pc[tid];
@@ -957,11 +974,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
         lds_barrier();
         // One lane per (record, quantity): a wave-instruction's atomics cover ~7 records' nine-float runs,
         // each inside one 64-B segment of its Gaussian's gradient record.
+#if !(GSD_BWD_ABLATE & 4)
         for (int e = tid; e < n * kRecUsed; e += kTilePix) {
             const int r = e / kRecUsed, q = e - kRecUsed * r;
             const float a = (float)s_acc[e];
             if (a != 0.f) atomicAdd(p.grad_rec + (size_t)s_u.id[r] * kGradRec + q, a);
         }
+#endif
     }
 #ifdef GSD_COUNT_WORK
     count_work(2, n_steps, n_pairs);
