@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--batch", type=int, default=256, help="records staged per batch")
     ap.add_argument("--chunks", action="store_true", help="also the union-chunked walks")
+    ap.add_argument("--fine", action="store_true", help="also 2x2 and 4x2 lane groups")
     a = ap.parse_args()
     from conftest import oracle_kwargs, scene_inputs
     from gsd_amd.scene import CONFIGS
@@ -159,7 +160,8 @@ def main():
     for Cc in ((4, 8, 16, 32) if a.chunks else ()):
         print(f"per-row lists in union chunks of {Cc}: wave steps {count_chunked(Cc)}")
     base = None
-    for rw, rh, test in [(8, 8, "exact"), (4, 4, "linear")]:
+    for rw, rh, test in [(8, 8, "exact"), (4, 4, "linear")] + ([(2, 2, "linear"), (4, 2, "linear"), (2, 2, "exact")]
+                                                              if a.fine else []):
         t0 = time.time()
         s, ls = count(rw, rh, test)
         base = base or s
