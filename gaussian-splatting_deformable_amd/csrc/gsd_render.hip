@@ -406,6 +406,17 @@ template <int U>
 __device__ __forceinline__ int row_bcast_i(int v) {
     return __builtin_amdgcn_update_dpp(0, v, 0x150 + U, 0xf, 0xf, true);
 }
+// acc + (lane U of the row's v) * w as ONE v_fmac_f32_dpp (the broadcast on src0, a fused multiply-add as fmaf):
+// for a v_fmac the compiler puts the broadcast in a v_mov_b32_dpp of its own.  v must not be written by a VALU
+// instruction in the two before it (a DPP source hazard the compiler cannot see inside the asm): the callers pass
+// record fields loaded from LDS at the start of their 16-entry block.
+template <int U>
+__device__ __forceinline__ float fmac_bcast(float v, float w, float acc) {
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(acc)
+        : "v"(v), "v"(w), "n"(U));
+    return acc;
+}
 
 // The round-4 backward (one record list per wave, the 8x8 quadrant, float LDS atomics): kept for A/B against the
 // per-group kernel below (-DGSD_BWD_QUADRANT).
@@ -885,8 +896,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                             const float alpha = fminf(0.99f, og);
                             const float inv1ma = fast_recip(1.f - alpha);
                             T = T * inv1ma;  // backward.cu:503 (T recovered by division)
+#ifndef GSD_BWD_NO_FMAC_DPP
+                            const float cd = fmac_bcast<U>(rrgb.z, dpix2,
+                                                           fmac_bcast<U>(rrgb.y, dpix1, row_bcast<U>(rrgb.x) * dpix0));
+#else
                             const float cd = fmaf(row_bcast<U>(rrgb.z), dpix2,
                                                   fmaf(row_bcast<U>(rrgb.y), dpix1, row_bcast<U>(rrgb.x) * dpix0));
+#endif
                             const float diff = cd - adot;
                             // backward.cu:512-529 (kbg = 0: fmaf(diff, T, -0) is diff * T, bit for bit)
                             const float dL_dalpha = kBg ? fmaf(diff, T, kbg * inv1ma) : diff * T;
