@@ -56,8 +56,9 @@ __device__ __forceinline__ void count_work(int i, unsigned long long steps, unsi
 // 4 is fastest (0.33 ms vs 0.38 at 8: fewer alphas wasted past a pixel's termination; re-measured with the
 // uniform-skip recurrence: 2 / 4 / 8 -> 0.305 / 0.289 / 0.328 ms; with the 4x4 lane groups: 4 / 8 -> 0.252 / 0.280)
 constexpr int kBatch = 4;
-// (forward culling is by the alpha box only: the backward's exact ellipse test costs the forward more than it
-// saves -- 0.306 vs 0.289 ms per 8x8 quadrant, 0.366 vs 0.261 per 4x4 lane group)
+// (forward culling: the exact ellipse test costs the forward more than it saves -- 0.306 vs 0.289 ms per 8x8
+// quadrant, 0.366 vs 0.261 per 4x4 lane group; the backward's linear bound over the 4x4 block on top of the alpha
+// box pays: 0.1994 / 0.1995 ms against 0.2040 / 0.2034 with the box alone, round 5)
 constexpr int kBwdGroup = 4;  // backward: records per pixel-major -> record-major hand-off through LDS
 
 // Does the ellipse {d : Q(d) <= t} around (mx, my) meet the rectangle [x0, x1] x [y0, y1]?
@@ -191,6 +192,52 @@ __device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s
     wave_lds_handoff();
 }
 
+// Backward compaction into one list per 4x4 lane group (the forward's groups, fwd_lane_pixel): lists[g] receives, in
+// increasing slot order, the slots t >= t_min[g] (the group's last-contributor cut) whose alpha box meets group g's
+// block and whose alpha ellipse passes a linear bound over the block: with d the block centre minus the mean and
+// h = 1.5 px the block's half-size, min over the block of Q >= Q(d) - h |grad Q(d)|_1 = Q(d) - 3 (|u| + |v|),
+// (u, v) = (a dx + b dy, b dx + c dy) -- conservative for a positive-definite conic, so a culled record has
+// alpha < 1/255 at every pixel of the block (the same slack as the exact test: 0.1 % + 0.05 on 2 ln(255 o)).
+// Counted on the cfg4 scene (scripts/sim_bwd_lists.py): the wave then walks 0.708 of the per-quadrant lists' steps
+// (the exact ellipse test per block: 0.682, the alpha box alone: 0.817).
+template <int NB>
+__device__ __forceinline__ void bwd_compact_groups(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
+                                                   const float2* __restrict__ s_bo, uint8_t (*lists)[NB], int n,
+                                                   float qx0, float qy0, int lane, const int (&t_min)[4],
+                                                   int (&cnt)[4]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) cnt[g] = 0;
+#pragma unroll
+    for (int k = 0; k < NB / 64; ++k) {
+        const int t = k * 64 + lane;
+        const bool in = t < n;
+        const float4 bx = s_box[t];  // slots >= n hold stale values: every test below is masked by `in`
+        const float4 pc = s_pc[t];
+        const float2 bo = s_bo[t];
+        const float a = -2.f * pc.z, c = -2.f * pc.w, b = bo.x;
+        const float thr = fmaf(-2.002f, bo.y, 0.05f);
+        const bool pd = a > 0.f && c > 0.f && a * c - b * b > 0.f;
+        const float dx0 = (qx0 + 1.5f) - pc.x, dy0 = (qy0 + 1.5f) - pc.y;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float ox = (float)(4 * (g & 1)), oy = (float)(4 * (g >> 1));
+            const float x0 = qx0 + ox, y0 = qy0 + oy;
+            bool hit = in && t >= t_min[g] && bx.y >= x0 && bx.x <= x0 + 3.f && bx.w >= y0 && bx.z <= y0 + 3.f;
+            const float dx = dx0 + ox, dy = dy0 + oy;
+            const float u = a * dx + b * dy, v = b * dx + c * dy;
+            const float q = dx * u + dy * v;
+            const float lb = fmaf(-3.f, fabsf(u) + fabsf(v), q);
+            if (pd && lb > fmaf(1e-6f, q, thr)) hit = false;  // NaN-safe: keeps the record
+            const unsigned long long mask = wave_ballot(hit);
+            if (hit)
+                lists[g][cnt[g] + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0))] = (uint8_t)t;
+            cnt[g] += __popcll(mask);
+        }
+    }
+    wave_lds_handoff();
+}
+
 // forward.cu:330-345 / backward.cu:490-501: the record's alpha at this pixel, shared by both passes so their
 // decisions are identical.  power is evaluated exactly as the reference writes it (no contraction), so it has the
 // reference's bits.  The threshold decision alpha = min(0.99, o exp(power)) >= 1/255 is taken as power >= t_o, with
@@ -314,7 +361,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         __syncthreads();
         const int n = min(kTilePix, toDo);
         int cnt[kFwdGroups];  // the groups' list lengths (scalar)
+#ifndef GSD_FWD_BOX_ONLY
+        // the backward's compaction (alpha box + the linear bound of the ellipse over the 4x4 block), without its
+        // contributor cut: a record it drops has alpha < 1/255 at every pixel of the block, so it is one the
+        // recurrence skips anyway (forward.cu:343-345)
+        {
+            const int t_none[4] = {0, 0, 0, 0};
+            bwd_compact_groups<kTilePix>(s_box, s_pc, s_bo, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane, t_none, cnt);
+        }
+#else
         wave_compact_groups(s_box, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane, cnt);
+#endif
         int m = cnt[0], mine = cnt[0];  // the longest; the calling lane's group's
 #pragma unroll
         for (int g = 1; g < kFwdGroups; ++g) {
@@ -675,52 +732,6 @@ __device__ __forceinline__ float tstep4(float a, float b) {
     const int u = __builtin_amdgcn_update_dpp(__float_as_int(a), __float_as_int(b), 0x124, 0xf, 0xa, false);
     const int v = __builtin_amdgcn_update_dpp(__float_as_int(b), __float_as_int(a), 0x12c, 0xf, 0x5, false);
     return __int_as_float(u) + __int_as_float(v);
-}
-
-// Backward compaction into one list per 4x4 lane group (the forward's groups, fwd_lane_pixel): lists[g] receives, in
-// increasing slot order, the slots t >= t_min[g] (the group's last-contributor cut) whose alpha box meets group g's
-// block and whose alpha ellipse passes a linear bound over the block: with d the block centre minus the mean and
-// h = 1.5 px the block's half-size, min over the block of Q >= Q(d) - h |grad Q(d)|_1 = Q(d) - 3 (|u| + |v|),
-// (u, v) = (a dx + b dy, b dx + c dy) -- conservative for a positive-definite conic, so a culled record has
-// alpha < 1/255 at every pixel of the block (the same slack as the exact test: 0.1 % + 0.05 on 2 ln(255 o)).
-// Counted on the cfg4 scene (scripts/sim_bwd_lists.py): the wave then walks 0.708 of the per-quadrant lists' steps
-// (the exact ellipse test per block: 0.682, the alpha box alone: 0.817).
-template <int NB>
-__device__ __forceinline__ void bwd_compact_groups(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
-                                                   const float2* __restrict__ s_bo, uint8_t (*lists)[NB], int n,
-                                                   float qx0, float qy0, int lane, const int (&t_min)[4],
-                                                   int (&cnt)[4]) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) cnt[g] = 0;
-#pragma unroll
-    for (int k = 0; k < NB / 64; ++k) {
-        const int t = k * 64 + lane;
-        const bool in = t < n;
-        const float4 bx = s_box[t];  // slots >= n hold stale values: every test below is masked by `in`
-        const float4 pc = s_pc[t];
-        const float2 bo = s_bo[t];
-        const float a = -2.f * pc.z, c = -2.f * pc.w, b = bo.x;
-        const float thr = fmaf(-2.002f, bo.y, 0.05f);
-        const bool pd = a > 0.f && c > 0.f && a * c - b * b > 0.f;
-        const float dx0 = (qx0 + 1.5f) - pc.x, dy0 = (qy0 + 1.5f) - pc.y;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float ox = (float)(4 * (g & 1)), oy = (float)(4 * (g >> 1));
-            const float x0 = qx0 + ox, y0 = qy0 + oy;
-            bool hit = in && t >= t_min[g] && bx.y >= x0 && bx.x <= x0 + 3.f && bx.w >= y0 && bx.z <= y0 + 3.f;
-            const float dx = dx0 + ox, dy = dy0 + oy;
-            const float u = a * dx + b * dy, v = b * dx + c * dy;
-            const float q = dx * u + dy * v;
-            const float lb = fmaf(-3.f, fabsf(u) + fabsf(v), q);
-            if (pd && lb > fmaf(1e-6f, q, thr)) hit = false;  // NaN-safe: keeps the record
-            const unsigned long long mask = wave_ballot(hit);
-            if (hit)
-                lists[g][cnt[g] + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0))] = (uint8_t)t;
-            cnt[g] += __popcll(mask);
-        }
-    }
-    wave_lds_handoff();
 }
 
 // Backward with one record list per 4x4 lane group.  The wave's four 16-lane rows are the forward's four 4x4 pixel

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="records staged per batch")
     ap.add_argument("--chunks", action="store_true", help="also the union-chunked walks")
     ap.add_argument("--fine", action="store_true", help="also 2x2 and 4x2 lane groups")
+    ap.add_argument("--balance", action="store_true", help="only: blocks dealt to waves by list length per batch")
     a = ap.parse_args()
     from conftest import oracle_kwargs, scene_inputs
     from gsd_amd.scene import CONFIGS
@@ -156,7 +157,40 @@ def main():
             steps += int(cnt.max(0).sum())
         return steps
 
+    def count_balance():
+        """4x4 linear lists: wave steps with the fixed block -> (wave, row) map against blocks dealt to waves by list
+        length per batch (sorted, four consecutive per wave), and the lower bound sum / 4"""
+        lens = []
+        for blk in range(16):
+            ox, oy = (blk % 4) * 4, (blk // 4) * 4
+            x0, y0 = tx + ox, ty + oy
+            x1, y1 = x0 + 3, y0 + 3
+            hit = (bx1 >= x0) & (bx0 <= x1) & (by1 >= y0) & (by0 <= y1)
+            cx, cy = (x0 + x1) * 0.5, (y0 + y1) * 0.5
+            dx, dy = cx - m2[:, 0], cy - m2[:, 1]
+            u, v = A * dx + B * dy, B * dx + C_ * dy
+            q = dx * u + dy * v
+            hit &= q - 3 * np.abs(u) - 3 * np.abs(v) <= thr * 1.001 + 0.05
+            glc = nct[:, oy:oy + 4, ox:ox + 4].reshape(nct.shape[0], -1).max(1)
+            hit &= pos < glc[tile_of]
+            key = tile_of * nb + batch
+            lens.append(np.bincount(key[hit], minlength=ranges.shape[0] * nb))
+        L = np.stack(lens)  # [16 blocks][tile * nb + batch]; block = 4 * by + bx
+        # the kernel's map: wave w = quadrant (qx, qy), rows = its four 4x4 blocks
+        fixed = 0
+        for wq in range(4):
+            qx, qy = (wq & 1) * 2, (wq >> 1) * 2
+            blks = [(qy + j) * 4 + qx + i for j in range(2) for i in range(2)]
+            fixed += int(L[blks].max(0).sum())
+        Ls = -np.sort(-L, axis=0)
+        dealt = int((Ls[0] + Ls[4] + Ls[8] + Ls[12]).sum())
+        print(f"4x4 linear lists, batch {a.batch}: wave steps fixed map {fixed}, dealt by length {dealt} "
+              f"({dealt / fixed:.3f}), lower bound {int(L.sum()) / 4:.0f} ({L.sum() / 4 / fixed:.3f})")
+
     C_ = C
+    if a.balance:
+        count_balance()
+        return
     for Cc in ((4, 8, 16, 32) if a.chunks else ()):
         print(f"per-row lists in union chunks of {Cc}: wave steps {count_chunked(Cc)}")
     base = None
