@@ -200,14 +200,16 @@ __device__ __forceinline__ void wave_compact_groups(const float4* __restrict__ s
 // alpha < 1/255 at every pixel of the block (the same slack as the exact test: 0.1 % + 0.05 on 2 ln(255 o)).
 // Counted on the cfg4 scene (scripts/sim_bwd_lists.py): the wave then walks 0.708 of the per-quadrant lists' steps
 // (the exact ellipse test per block: 0.682, the alpha box alone: 0.817).
-template <int NB>
+// UNROLL: slots per lane whose loads and tests the compiler may interleave (the forward, at 64 VGPRs, takes them
+// one at a time: unrolled, the extra live values spilled 24 B per lane, ~95 MB of scratch traffic per launch)
+template <int NB, int UNROLL = NB / 64>
 __device__ __forceinline__ void bwd_compact_groups(const float4* __restrict__ s_box, const float4* __restrict__ s_pc,
                                                    const float2* __restrict__ s_bo, uint8_t (*lists)[NB], int n,
                                                    float qx0, float qy0, int lane, const int (&t_min)[4],
                                                    int (&cnt)[4]) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) cnt[g] = 0;
-#pragma unroll
+#pragma unroll UNROLL
     for (int k = 0; k < NB / 64; ++k) {
         const int t = k * 64 + lane;
         const bool in = t < n;
@@ -367,7 +369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         // recurrence skips anyway (forward.cu:343-345)
         {
             const int t_none[4] = {0, 0, 0, 0};
-            bwd_compact_groups<kTilePix>(s_box, s_pc, s_bo, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane, t_none, cnt);
+            bwd_compact_groups<kTilePix, 1>(s_box, s_pc, s_bo, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane, t_none, cnt);
         }
 #else
         wave_compact_groups(s_box, s_list[tg.wave], n, tg.qx0, tg.qy0, tg.lane, cnt);
@@ -823,7 +825,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
     const float bg_dot = p.bg[0] * dpix0 + p.bg[1] * dpix1 + p.bg[2] * dpix2;
     const float kbg = -T_final * bg_dot;
     const bool any_bg = wave_ballot(kbg != 0.f) != 0;  // wave-uniform
-    const float ddelx_dx = (float)(0.5 * p.W), ddely_dy = (float)(0.5 * p.H);
     const float pxf = (float)tg.px, pyf = (float)tg.py;
     const uint8_t* my_list = s_list[tg.wave][grp];
 #ifdef GSD_COUNT_WORK
@@ -990,8 +991,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
             double* acc = s_acc + kRecUsed * tid;
             // phase 2 summed the first moments over x - mx, y - my: the reference's dx = mx - x flips them
             const double m0 = -acc[0], m1 = -acc[1];
-            acc[0] = (a * m0 + b * m1) * -(double)ddelx_dx;
-            acc[1] = (c * m1 + b * m0) * -(double)ddely_dy;
+            // -(double)ddelx_dx, -(double)ddely_dy (= -W/2, -H/2 exactly) rebuilt here from the scalar image size: hoisted
+            // out of the batch loop they were a VGPR pair the register limit spilled (8 B of scratch stored per lane,
+            // reloaded every batch)
+            int wh[2] = {p.W, p.H};
+            asm volatile("" : "+s"(wh[0]), "+s"(wh[1]));
+            acc[0] = (a * m0 + b * m1) * (-0.5 * (double)wh[0]);
+            acc[1] = (c * m1 + b * m0) * (-0.5 * (double)wh[1]);
             acc[2] *= -0.5;
             acc[3] *= -0.5;
             acc[4] *= -0.5;
