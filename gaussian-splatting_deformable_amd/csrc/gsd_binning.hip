@@ -442,10 +442,11 @@ __global__ __launch_bounds__(256) void k_tile_sort(int T, const uint2* __restric
     const int n = (int)(rg.y - rg.x);
     if (n <= 0) return;
     const size_t base = rg.x;
+    static_assert(kSortCap >= 512 && (kSortCap & (kSortCap - 1)) == 0, "a power of two of at least 512");
     if (n <= 512) return sort_tile_regs<2>(keys + base, n, s, point_list + base);
-    if (n <= 1024) return sort_tile_regs<4>(keys + base, n, s, point_list + base);
-    if (n <= 2048) return sort_tile_regs<8>(keys + base, n, s, point_list + base);
-    if (n <= kSortCap) return sort_tile_regs<16>(keys + base, n, s, point_list + base);
+    if constexpr (kSortCap >= 1024) if (n <= 1024) return sort_tile_regs<4>(keys + base, n, s, point_list + base);
+    if constexpr (kSortCap >= 2048) if (n <= 2048) return sort_tile_regs<8>(keys + base, n, s, point_list + base);
+    if constexpr (kSortCap >= 4096) if (n <= 4096) return sort_tile_regs<16>(keys + base, n, s, point_list + base);
     // Large bucket: sort kSortCap chunks in LDS, then merge runs pairwise in
     // global memory (ping-pong keys <-> scratch), the whole workgroup per merge.
     for (int c0 = 0; c0 < n; c0 += kSortCap) {

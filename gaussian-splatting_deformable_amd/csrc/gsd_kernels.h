@@ -455,6 +455,13 @@ constexpr int kHistMaxTiles = 40960;    // 160 KiB of u32 bins; larger grids use
 constexpr int kHistTargetBlocks = 512;  // Gaussian chunks per view
 constexpr int kColSeg = 32;             // histogram rows per column-scan segment
 constexpr int kScanThreads = 1024;
-constexpr int kSortCap = 4096;  // instances sorted in one LDS pass (32 KiB of u64 keys)
+// Instances sorted in one LDS pass (8 B of LDS per key).  Round 5: 2048 instead of 4096 -- the LDS and the
+// 16-key register network of the 4096 class held k_tile_sort at five waves per SIMD with 144 B of scratch per
+// lane; at 2048 it runs eight waves with none (0.0395 -> 0.0367 ms at cfg4, profiles/round5/binning/r5al/), and
+// buckets of 2049-4096 keys take the LDS-chunk + global-merge path of the larger ones.
+#ifndef GSD_SORT_CAP
+#define GSD_SORT_CAP 2048
+#endif
+constexpr int kSortCap = GSD_SORT_CAP;
 
 }  // namespace gsd

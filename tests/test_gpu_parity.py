@@ -337,6 +337,21 @@ def test_dense_tile_merge_path(oracle_mod):
     assert counts.max() > 4096
 
 
+@pytest.mark.parametrize("P,lo,hi", [(700, 512, 1024), (1500, 1024, 2048), (3000, 2048, 4096)])
+def test_dense_tile_sort_classes(oracle_mod, P, lo, hi):
+    """The tile sort's size classes above the 512-key register network: 1024 and 2048 keys in registers, and
+    2049-4096 keys, which take the LDS-chunk + merge path since the LDS cap is 2048 (gsd_kernels.h kSortCap)."""
+    d = scene_inputs(P, 128, 128, 0, seed=6, device=DEV)
+    g = torch.Generator().manual_seed(10)
+    z = torch.rand(P, generator=g) * 4 + 3
+    xy = (torch.rand(P, 2, generator=g) - 0.5) * 0.02 * z[:, None]
+    d["means3D"] = torch.cat([xy, z[:, None]], 1).to(DEV)
+    d["scales"] = torch.full((P, 3), 0.002).to(DEV)
+    o, _ = check_forward(oracle_mod, d)
+    counts = o["ranges"][:, 1].astype(np.int64) - o["ranges"][:, 0]
+    assert lo < counts.max() <= hi
+
+
 def test_binning_buffer_too_small_retries(oracle_mod):
     """The binning buffer is sized from the previous count before the forward knows num_rendered; a short one
     (GSD_NEED_BINNING) is re-allocated and phase 2 re-run -- same results as a well-sized one."""
