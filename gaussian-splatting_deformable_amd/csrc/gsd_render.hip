@@ -721,8 +721,23 @@ __global__ __launch_bounds__(256) void k_render_bwd_quadrant(RenderBwdParams p) 
 // Transposed reduction steps inside a 16-lane row.  DPP bank b is lanes 4b .. 4b + 3 of each row, so a bank mask
 // selects by lane bits 3:2, and a DPP move with a partial bank mask writes only those lanes (the others keep
 // `old`).  row_ror:N gives lane l the value of lane (l - N) mod 16.
-// tstep8: lanes with bit 3 clear return a(l) + a(l ^ 8), lanes with bit 3 set b(l) + b(l ^ 8) -- three VALU ops
-// for a pair of quantities, no lane selects.
+// tstep8: lanes with bit 3 clear return a(l) + a(l ^ 8), lanes with bit 3 set b(l) + b(l ^ 8).  Three VALU ops for
+// a pair of quantities: two full-row DPP adds (row_ror:8) and a select on the lane's bit 3 -- the bank-masked moves
+// of the round-5 first form needed a register copy of the masked move's `old` on top (four ops; GSD_TSTEP_BANKS)
+#ifndef GSD_TSTEP_BANKS
+__device__ __forceinline__ float tstep8(float a, float b) {
+    const float sa = a + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x128, 0xf, 0xf, true));
+    const float sb = b + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(b), 0x128, 0xf, 0xf, true));
+    return (__lane_id() & 8) ? sb : sa;
+}
+// tstep4: lanes with bit 2 clear return a(l) + a(l ^ 4), lanes with bit 2 set b(l) + b(l ^ 4): the partner is
+// l + 4 (row_ror:12) for bit 2 clear and l - 4 (row_ror:4) for bit 2 set.
+__device__ __forceinline__ float tstep4(float a, float b) {
+    const float sa = a + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x12c, 0xf, 0xf, true));
+    const float sb = b + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(b), 0x124, 0xf, 0xf, true));
+    return (__lane_id() & 4) ? sb : sa;
+}
+#else
 __device__ __forceinline__ float tstep8(float a, float b) {
     const int u = __builtin_amdgcn_update_dpp(__float_as_int(a), __float_as_int(b), 0x128, 0xf, 0xc, false);
     const int v = __builtin_amdgcn_update_dpp(__float_as_int(b), __float_as_int(a), 0x128, 0xf, 0x3, false);
@@ -735,6 +750,7 @@ __device__ __forceinline__ float tstep4(float a, float b) {
     const int v = __builtin_amdgcn_update_dpp(__float_as_int(b), __float_as_int(a), 0x12c, 0xf, 0x5, false);
     return __int_as_float(u) + __int_as_float(v);
 }
+#endif
 
 // Backward with one record list per 4x4 lane group.  The wave's four 16-lane rows are the forward's four 4x4 pixel
 // blocks, and each row walks its own list (bwd_compact_groups): a wave step serves four (block, record) pairs, one per
@@ -743,7 +759,7 @@ __device__ __forceinline__ float tstep4(float a, float b) {
 //   (different records in different rows, one LDS read per lane per 16 entries, as in the quadrant kernel);
 // - phase 1 is unchanged: each lane replays its pixel and hands (o G dL/dalpha, alpha T) of four records to LDS;
 // - phase 2: lane 16 g + 4 r' + r sums record r of row g over the four pixels of block row r' (its own quad), then
-//   two transposed DPP steps inside the row (tstep8, tstep4: bank-masked moves, no selects) leave each lane two of
+//   two transposed DPP steps inside the row (tstep8, tstep4: full-row DPP adds and a lane select) leave each lane two of
 //   the record's nine sums (and the ninth in the lanes with bits 3:2 clear): three LDS adds per lane and hand-off,
 //   as in the quadrant kernel, into the tile's accumulators.
 //   The accumulators are doubles: each (row, record) pair leaves its own nine sums (12.8M pairs at cfg4, against
@@ -954,9 +970,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                     }
                     // the record's sums over the row's four quads: lane bits 3:2 = (b3, b2) end with quantity
                     // qsel = b3 + 2 b2 of (Mx, My, Mxx, Mxy) in ca and of (Myy, S0, C0, C1) in cb; C2 everywhere
-                    const float ca = tstep4(tstep8(Mx, My), tstep8(Mxx, Mxy));
-                    const float cb = tstep4(tstep8(Myy, S0), tstep8(C0, C1));
-                    const float c2 = sum4(sum8(C2));
+                    float ca = tstep4(tstep8(Mx, My), tstep8(Mxx, Mxy));
+                    float cb = tstep4(tstep8(Myy, S0), tstep8(C0, C1));
+                    float c2 = sum4(sum8(C2));
+                    // computed here, ahead of the `own` branch: sunk into it, the last adds lost their DPP sources (a
+                    // broadcast stays outside the branch as a v_mov_b32_dpp of its own)
+                    asm volatile("" : "+v"(ca), "+v"(cb), "+v"(c2));
                     wave_lds_handoff();  // phase-1 writes of the next hand-off must stay behind these reads
 #if GSD_BWD_ABLATE & 2
                     if (own && ca == 12345.f && cb == 0.5f && c2 == 0.25f) acc[0] = 1.0;  // timing only: no accumulation
