@@ -1047,7 +1047,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
 // One workgroup per Gaussian chunk computes the whole (32 NRB) x (32 KRB) output, one wave per tile of TNB x TKB
-// blocks of 32 x 32 (four waves, one per SIMD with 512 registers; or eight, two per SIMD, on half-size tiles).  Each 16-Gaussian step, every thread loads 64 B of one or two feature rows (of G or X), splits
+// blocks of 32 x 32 (four waves, one per SIMD with 512 registers; or eight, two per SIMD, on half-size tiles; or
+// twelve / sixteen, with two threads per row, kHalf).  Each 16-Gaussian step, every thread loads 64 B of one or two
+// feature rows (of G or X) -- 32 B of one row with two threads per row --, splits
 // them into the three bf16 planes ONCE and writes them to LDS in the MFMA operand layout; the waves then read their
 // A (G) and B (X) fragments from there: [row][plane * 2 + h] slots of 16 B, 7 slots per row (112 B: the 16 lanes
 // of a b128 read hit 16 distinct bank quads).  Double-buffered: step s + 1 is staged while step s is multiplied.
@@ -1097,7 +1099,9 @@ void k_mlp_wgrad(MlpWgradParams p) {
     float bsum[S::RPT];
 #pragma unroll
     for (int i = 0; i < S::RPT; ++i) {
-        const int r = tid + S::THREADS * i;
+        // (with two threads per row, kHalf below, thread t stages row t / 2)
+        const int r = (S::RPT == 1 && S::THREADS >= 2 * S::ROWS && S::WAVES > 8) ? min(tid >> 1, S::ROWS - 1)
+                                                                                  : tid + S::THREADS * i;
         bsum[i] = 0.f;
         if (r < 32 * NRB) src[i] = p.G + (size_t)r * p.ldp;
         else {
@@ -1111,6 +1115,11 @@ void k_mlp_wgrad(MlpWgradParams p) {
     // (One row per thread only: with more, e.g. layer 5's 576 rows on 256 threads, the pair of steps in registers
     // spills, so those shapes keep one 16-Gaussian segment per row and step, loaded two steps ahead.)
     constexpr bool kWide = S::RPT == 1 && S::WAVES <= 8;
+#ifndef GSD_WGRAD_WHOLE_ROWS
+    constexpr bool kHalf = !kWide && S::RPT == 1 && S::THREADS >= 2 * S::ROWS;
+#else
+    constexpr bool kHalf = false;
+#endif
     constexpr int kWid = kWide ? 32 : 16;
     float raw[S::RPT][kWid];
     auto load_into = [&](float (&dst)[S::RPT][kWid], int p0) {
@@ -1184,6 +1193,47 @@ void k_mlp_wgrad(MlpWgradParams p) {
                 }
             }
         }
+    } else if constexpr (kHalf) {
+        // two threads per row, eight Gaussians each: every wave stages (sixteen waves for 512 rows), instead of half
+        // of them staging whole 16-Gaussian segments while the other half only multiplies
+        const int r = tid >> 1, hv = tid & 1;
+        const bool stager = r < S::ROWS;   // (threads past twice the rows only multiply)
+        const float* row = src[0];
+        float rh[8];
+        auto loadh = [&](int p0) {
+            if (!stager) return;
+            const float4 a = *reinterpret_cast<const float4*>(row + p0 + 8 * hv);
+            const float4 b = *reinterpret_cast<const float4*>(row + p0 + 8 * hv + 4);
+            rh[0] = a.x; rh[1] = a.y; rh[2] = a.z; rh[3] = a.w; rh[4] = b.x; rh[5] = b.y; rh[6] = b.z; rh[7] = b.w;
+        };
+        auto writeh = [&](int p0, int bf) {
+            if (!stager) return;
+            float w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = p0 + 8 * hv + j < p_hi ? rh[j] : 0.f;
+            if (r < 32 * NRB) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum[0] += w[j];
+            }
+            const Split8 sp = split8(w);
+            s_op[bf][r][0 + hv] = sp.hi;
+            s_op[bf][r][2 + hv] = sp.mid;
+            s_op[bf][r][4 + hv] = sp.lo;
+        };
+        int buf = 0;
+        loadh(p_lo);
+        writeh(p_lo, 0);
+        if (p_lo + 16 < p_hi) loadh(p_lo + 16);
+        __syncthreads();
+        for (int pb = p_lo; pb < p_hi; pb += 16, buf ^= 1) {
+            if (pb + 16 < p_hi) {
+                writeh(pb + 16, buf ^ 1);
+                if (pb + 32 < p_hi) loadh(pb + 32);
+            }
+            GSD_WGRAD_MMA(buf);
+            __syncthreads();
+        }
+        bsum[0] += __shfl_xor(bsum[0], 1);   // the row's two halves
     } else {
         int buf = 0;
         load(p_lo);
@@ -1216,8 +1266,13 @@ void k_mlp_wgrad(MlpWgradParams p) {
     }
 #pragma unroll
     for (int i = 0; i < S::RPT; ++i) {   // the bias gradient: the G rows' sums over this chunk
-        const int r = tid + S::THREADS * i;
-        if (r < 32 * NRB) p.bias_partial[(size_t)blockIdx.x * (32 * NRB) + r] = bsum[i];
+        if constexpr (kHalf) {
+            const int r = tid >> 1;
+            if (r < 32 * NRB && !(tid & 1)) p.bias_partial[(size_t)blockIdx.x * (32 * NRB) + r] = bsum[i];
+        } else {
+            const int r = tid + S::THREADS * i;
+            if (r < 32 * NRB) p.bias_partial[(size_t)blockIdx.x * (32 * NRB) + r] = bsum[i];
+        }
     }
 }
 
@@ -1341,12 +1396,22 @@ void launch_mlp_wgrad(const MlpWgradParams& p_in, const MlpWeightRef& dst, const
         const char* e = getenv("GSD_WGRAD16");
         return !(e && strcmp(e, "0") == 0);
     }();
-    // (the narrow shapes with three or four waves per SIMD were slower: 64 x 256 as 16 waves of one block 0.40 ms
-    // against 0.30, 256 x 96 as 12 waves of 2 x 1 blocks 0.45 against 0.43)
+    // (round 4, whole-row staging: the narrow shapes with three or four waves per SIMD were slower -- 64 x 256 as 16
+    // waves of one block 0.40 ms against 0.30, 256 x 96 as 12 waves of 2 x 1 blocks 0.45 against 0.43)
     if (w16 && p.n_rb == 8 && p.k_rb == 8)
         hipLaunchKernelGGL((k_mlp_wgrad<8, 8, 2, 2>), grid, dim3(64 * WgradShape<8, 8, 2, 2>::WAVES), 0, s, p);
+    // Round 5: with two threads staging each row (kHalf in k_mlp_wgrad: every wave stages eight Gaussians of a row
+    // per step, instead of half the waves staging whole 16-Gaussian segments while the rest only multiply), the wide
+    // shapes pay too: 256 x 256 0.715 -> 0.633 ms, 256 x 96 as twelve waves of 2 x 1 blocks 0.445 -> 0.36, 64 x 256 and
+    // 256 x 64 as sixteen waves of one block 0.31 -> 0.295 (profiles/round5/deform_mlp_wgrad/r5aq/);
+    // GSD_WGRAD_NARROW_OLD keeps the round-4 narrow shapes
+#ifndef GSD_WGRAD_NARROW_OLD
+    else GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 2, 1, 1) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 1)
+    else GSD_WGRAD(2, 8, 1, 1)
+#else
     else GSD_WGRAD(8, 8, 4, 2) else GSD_WGRAD(8, 2, 2, 1) else GSD_WGRAD(8, 10, 4, 5) else GSD_WGRAD(8, 3, 2, 3)
     else GSD_WGRAD(2, 8, 1, 2)
+#endif
 #undef GSD_WGRAD
     const long long nw = (long long)(32 * p.n_rb) * (32 * p.k_rb);
     const int w_blocks = (int)((nw + 31) / 32), b_blocks = p.skip_bias ? 0 : (32 * p.n_rb + 31) / 32;

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 5: the 256 x 256 weight gradient: HEAD (build_base/, half the waves stage whole rows), two threads per row
+# (build/), and two threads per row loading both steps of a pair as whole 128-B lines (build_hw/): mlp_ablate.py
+# under rocprofv3, A/B/C x2, then the network tests on build_hw.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; export TMPDIR=/tmp
+OUT=${OUT:-r5ap}; O="gpurun_out/$OUT"; mkdir -p "$O"
+L=gaussian-splatting_deformable_amd
+for rep in 1 2; do
+  for v in build_base build build_hw; do
+    GSD_SKIP_BUILD_ID=1 GSD_HIP_LIB=$L/$v/libgsd_hip.so timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$O/prof_${v}_$rep" -o run -- python scripts/mlp_ablate.py --reps 5 > "$O/ablate_${v}_$rep.log" 2>&1 \
+        || { tail -20 "$O/ablate_${v}_$rep.log"; exit 1; }
+    f=$(find "$O/prof_${v}_$rep" -name '*kernel_stats.csv' | head -1)
+    echo "== $v $rep"; python3 -c "import csv,sys; [print(r[\"Calls\"], r[\"AverageNs\"]) for r in csv.DictReader(open(sys.argv[1])) if \"wgrad<8, 8, 2\" in r[\"Name\"]]" "$f"
+  done
+done
+GSD_SKIP_BUILD_ID=1 GSD_HIP_LIB=$L/build_hw/libgsd_hip.so timeout -k 10 600 python -u -m pytest tests/test_gpu_mlp.py -x -q \
+    -m gpu --timeout 300 --timeout-method thread > "$O/tests_hw.txt" 2>&1 || { tail -30 "$O/tests_hw.txt"; exit 1; }
+tail -2 "$O/tests_hw.txt"
+echo all-done
