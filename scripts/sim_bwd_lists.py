@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--chunks", action="store_true", help="also the union-chunked walks")
     ap.add_argument("--fine", action="store_true", help="also 2x2 and 4x2 lane groups")
     ap.add_argument("--balance", action="store_true", help="only: blocks dealt to waves by list length per batch")
+    ap.add_argument("--linonly", action="store_true", help="also 4x4 groups culled by the linear bound alone (no box)")
     a = ap.parse_args()
     from conftest import oracle_kwargs, scene_inputs
     from gsd_amd.scene import CONFIGS
@@ -97,7 +98,9 @@ def main():
                 hit = (bx1 >= x0) & (bx0 <= x1) & (by1 >= y0) & (by0 <= y1)
                 if test == "exact":
                     hit &= ellipse_min_q(m2[:, 0], m2[:, 1], A, B, C, x0, x1, y0, y1) <= thr * 1.001 + 0.05
-                elif test == "linear":
+                elif test in ("linear", "linonly"):
+                    if test == "linonly":
+                        hit = np.ones_like(hit)
                     cx, cy = (x0 + x1) * 0.5, (y0 + y1) * 0.5
                     dx, dy = cx - m2[:, 0], cy - m2[:, 1]
                     u, v = A * dx + B * dy, B * dx + C * dy
@@ -195,7 +198,7 @@ def main():
         print(f"per-row lists in union chunks of {Cc}: wave steps {count_chunked(Cc)}")
     base = None
     for rw, rh, test in [(8, 8, "exact"), (4, 4, "linear")] + ([(2, 2, "linear"), (4, 2, "linear"), (2, 2, "exact")]
-                                                              if a.fine else []):
+                                                              if a.fine else []) + ([(4, 4, "linonly")] if a.linonly else []):
         t0 = time.time()
         s, ls = count(rw, rh, test)
         base = base or s
