@@ -356,9 +356,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, 0.f);
             s_box[tid] = r->box;
         } else {  // slots past the tile's list: finite zeros (the walk below reads list bytes past a group's end)
-            s_pc[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
-            s_bo[tid] = make_float2(0.f, 0.f);
-            s_rgb[tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+            // (zeros built here from an opaque scalar: a float2 zero hoisted out of the round loop was a VGPR pair
+            // the 64-register limit spilled)
+            int zi = 0;
+            asm volatile("" : "+s"(zi));
+            const float z = __int_as_float(zi);
+            s_pc[tid] = make_float4(z, z, z, z);
+            s_bo[tid] = make_float2(z, z);
+            s_rgb[tid] = make_float4(z, z, z, z);
         }
         __syncthreads();
         const int n = min(kTilePix, toDo);
