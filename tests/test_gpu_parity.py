@@ -188,6 +188,44 @@ def test_backward_matches_oracle(oracle_mod, P, W, H, deg, seed):
         assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
 
 
+@pytest.mark.parametrize("lo,hi", [(5.0, 20.0), (40.0, 200.0)])
+def test_anisotropic_gaussians_forward_and_backward(oracle_mod, lo, hi):
+    """Needle-like Gaussians (one axis lo-hi times the others, random rotations, opacities up to 0.999): their alpha
+    boxes are loose and the linear ellipse bound over each 4x4 block does most of the list culling in both render
+    kernels (bwd_compact_groups).  The forward stays bit-exact and the render kernel's gradients (dL/dmean2D,
+    dL/dcolor, dL/dopacity) and dL/dsh match the oracle at this file's 1e-4.  The 2D covariances are near-singular in
+    float32 here (a c / det up to 2.7e3 at 5-20x, 2.5e5 at 40-200x): the reference's own conic -> cov3D -> scale /
+    rotation chain (backward.cu:144-274, 278-341) amplifies the float-atomic order noise of dL/dconic (measured: the
+    rotation gradient 4.4e-3 from the oracle at 5-20x, 2e-2 for dL/dmean3D at 40-200x).  So the chain's gradients are
+    held to the GPU's own run-to-run difference instead: within 20x of two backward launches' rel L2 (or 1e-4)."""
+    P, W, H, deg, seed = 5_000, 320, 240, 1, 11
+    d = scene_inputs(P, W, H, deg, seed=seed, device=DEV)
+    g = torch.Generator().manual_seed(seed)
+    s = d["scales"].cpu().clone()  # activated scales
+    s[:, 0] *= torch.empty(P).uniform_(lo, hi, generator=g)
+    s[:, 1:] *= 0.4
+    d["scales"] = s.to(DEV)
+    d["opacities"] = torch.empty(d["opacities"].shape).uniform_(0.02, 0.999, generator=g).to(DEV)
+    check_forward(oracle_mod, d)
+    dpix = torch.randn(3, H, W, generator=g).mul_(1e-3).to(DEV)
+    o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
+    fwd = gpu_forward(d)
+    grads = [t.cpu().numpy() for t in gpu_backward(d, fwd, dpix)]
+    again = [t.cpu().numpy() for t in gpu_backward(d, fwd, dpix)]
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    render_level = names[:3] + ["dL_dsh"]
+    for name, gt, g2 in zip(names, grads, again):
+        got = gt.reshape(ob[name].shape)
+        assert np.isfinite(got).all(), name
+        err = rel_l2(got, ob[name])
+        if name in render_level:
+            assert err <= 1e-4, (name, err)
+        else:
+            noise = rel_l2(got, g2.reshape(ob[name].shape))
+            assert err <= max(1e-4, 20 * noise), (name, err, noise)
+
+
 @pytest.mark.parametrize("short_binning", [False, True])
 def test_backward_with_forward_zeroed_scratch(oracle_mod, short_binning):
     """ABI 14 grad_scratch: the forward's compositing kernel zeroes the backward's gradient records (here a
