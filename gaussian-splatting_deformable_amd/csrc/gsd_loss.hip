@@ -57,7 +57,8 @@ struct SsimArgs {
 
 // Stage a 42x42 window of one channel of `a` around the tile, zero outside the image.  Fixed trip
 // counts, fully unrolled: all 12 loads of a thread are in flight before the first LDS store.
-__device__ __forceinline__ void stage(const float* __restrict__ a, float (*sa)[kSsimIn], int H, int W, int ox,
+template <int RS = kSsimIn>
+__device__ __forceinline__ void stage(const float* __restrict__ a, float (*sa)[RS], int H, int W, int ox,
                                       int oy) {
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     constexpr int kRowIt = (kSsimIn + 7) / 8, kColIt = 2;  // 6 x 2 slots of a 8 x 32 thread grid
@@ -229,8 +230,15 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
                                                              const float* __restrict__ gmaps,
                                                              const float* __restrict__ gscale, float sign,
                                                              float* __restrict__ dimg) {
-    __shared__ float sg[3][kSsimIn][kSsimIn];
-    __shared__ float sh[3][kSsimIn][kSsimTile];
+#ifndef GSD_SSIM_BWD_SCALAR_H
+    // rows padded to 44 floats (176 B): the horizontal pass below reads each thread's 16-float window as four
+    // 16-B-aligned ds_read_b128
+    constexpr int kSgStride = 44;
+#else
+    constexpr int kSgStride = kSsimIn;
+#endif
+    __shared__ __attribute__((aligned(16))) float sg[3][kSsimIn][kSgStride];
+    __shared__ __attribute__((aligned(16))) float sh[3][kSsimIn][kSsimTile];
     const int ch = blockIdx.z;
     const int ox = blockIdx.x * kSsimTile, oy = blockIdx.y * kSsimTile;
     const size_t plane = (size_t)p.H * p.W;
@@ -247,8 +255,32 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
         ys[j] = ok ? gt[o] : 0.f;
     }
 #pragma unroll
-    for (int q = 0; q < 3; ++q) stage(gmaps + ((size_t)q * p.C + ch) * plane, sg[q], p.H, p.W, ox, oy);
+    for (int q = 0; q < 3; ++q) stage<kSgStride>(gmaps + ((size_t)q * p.C + ch) * plane, sg[q], p.H, p.W, ox, oy);
     __syncthreads();
+#ifndef GSD_SSIM_BWD_SCALAR_H
+    // horizontal pass, four output columns per thread: the 14-float window from four b128 reads per map instead of
+    // 11 scalar reads per column (the same products and sums in the same order per output)
+    for (int it = threadIdx.x; it < kSsimIn * (kSsimTile / 4); it += kSsimThreads) {
+        const int r = it >> 3, c4 = (it & 7) * 4;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            float v[16];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const float4 f = *reinterpret_cast<const float4*>(&sg[q][r][c4 + 4 * b]);
+                v[4 * b] = f.x; v[4 * b + 1] = f.y; v[4 * b + 2] = f.z; v[4 * b + 3] = f.w;
+            }
+            float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 11; ++k) {
+                const float w = p.w[k];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] += w * v[j + k];
+            }
+            *reinterpret_cast<float4*>(&sh[q][r][c4]) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+#else
     for (int r = threadIdx.x >> 5; r < kSsimIn; r += kSsimThreads / 32) {
         float a = 0.f, cc = 0.f, e = 0.f;
 #pragma unroll
@@ -262,6 +294,7 @@ __global__ __launch_bounds__(kSsimThreads) void k_ssim_bwd(SsimArgs p, const flo
         sh[1][r][c] = cc;
         sh[2][r][c] = e;
     }
+#endif
     __syncthreads();
     const float g = gscale ? sign * gscale[0] : sign;  // d out / d loss (autograd's incoming gradient)
     float acc[3][kSsimRows];
