@@ -632,9 +632,16 @@ if __name__ == "__main__":
         try:
             main()
         except SystemExit as e:   # a rank that stops early must not wait in teardown either
+            if e.code is None:
+                code = 0
+            elif isinstance(e.code, int):
+                code = e.code
+            else:   # sys.exit("message"): print it as the interpreter would, status 1
+                print(e.code, file=sys.stderr)
+                code = 1
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(e.code if isinstance(e.code, int) else 1)
+            os._exit(code)
         except BaseException:
             import traceback
             traceback.print_exc()

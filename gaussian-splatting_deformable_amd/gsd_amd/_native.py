@@ -176,6 +176,12 @@ def check_build_id(lib, csrc: str = CSRC_DIR, path: str = LIB_PATH) -> str:
     if got != want:
         raise ImportError(f"gsd: {path} was built from other sources (build id {got[:16]}..., this tree "
                           f"{want[:16]}...); rebuild it with `make -C gaussian-splatting_deformable_amd/csrc`")
+    # the source hash does not cover HIPFLAGS_EXTRA: a timing-only build (-DGSD_BWD_ABLATE, -DGSD_COUNT_WORK, ...)
+    # of this very tree computes wrong results, so the product path takes only the plain build
+    flags = lib.gsd_build_flags().decode().strip()
+    if flags:
+        raise ImportError(f"gsd: {path} was built with extra flags ({flags!r}); the product path loads only the "
+                          "plain build (experiments set GSD_SKIP_BUILD_ID=1)")
     return got
 
 

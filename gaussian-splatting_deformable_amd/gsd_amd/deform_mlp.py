@@ -351,7 +351,7 @@ class DirectTemporalNeRF(nn.Module):
     def forward(self, x: torch.Tensor, ts: torch.Tensor, iteration: int):
         """-> (dx (P,3), d_scale (P,3), d_rot (P,4), d_sh (P,48)) as in gaussian_model.py:290-316."""
         P = x.shape[0]
-        if iteration < self.zero_before:
+        if iteration < self.zero_before or P == 0:   # the HIP paths take P >= 1; an empty set has empty heads
             z = x.new_zeros
             return z(P, 3), z(P, 3), z(P, 4), z(P, 48)
         if self._use_fused(x):

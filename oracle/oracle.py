@@ -194,11 +194,6 @@ def backward(fwd, dL_dpix, means3D, *, shs=None, colors_precomp=None, scales=Non
     L = lib()
     means3D = _f32(means3D).reshape(-1, 3)
     P = means3D.shape[0]
-    M = fwd["M"]
-    shs_a, shs_p = _opt(shs)
-    sc_a, sc_p = _opt(scales)
-    ro_a, ro_p = _opt(rotations)
-    cp_a, _ = _opt(cov3D_precomp)
     col_a, _ = _opt(colors_precomp)
     bg = _f32(bg).reshape(3)
     feats = col_a.reshape(P, 3) if col_a is not None else fwd["rgb"]
@@ -210,6 +205,32 @@ def backward(fwd, dL_dpix, means3D, *, shs=None, colors_precomp=None, scales=Non
     L.orc_render_bwd(P, W, H, fwd["ranges"], np.ascontiguousarray(fwd["point_list"]), bg, fwd["means2D"],
                      fwd["conic_opacity"], np.ascontiguousarray(feats), fwd["final_T"].reshape(-1),
                      fwd["n_contrib"].reshape(-1), dpix, dmean2D, dconic, dopac, dcolor)
+    pre = preprocess_backward(fwd, dmean2D, dconic, dcolor, means3D, shs=shs, scales=scales, rotations=rotations,
+                              cov3D_precomp=cov3D_precomp, viewmatrix=viewmatrix, projmatrix=projmatrix,
+                              campos=campos, W=W, H=H, tanfovx=tanfovx, tanfovy=tanfovy, sh_degree=sh_degree,
+                              scale_modifier=scale_modifier)
+    return dict(dL_dmeans2D=dmean2D, dL_dcolors=dcolor, dL_dopacity=dopac, dL_dconic=dconic, **pre)
+
+
+def preprocess_backward(fwd, dL_dmean2D, dL_dconic, dL_dcolor, means3D, *, shs=None, scales=None, rotations=None,
+                        cov3D_precomp=None, viewmatrix, projmatrix, campos, W, H, tanfovx, tanfovy, sh_degree,
+                        scale_modifier=1.0, **_):
+    """The per-Gaussian half of the reference backward alone (computeCov2DCUDA + preprocessCUDA bwd,
+    backward.cu:144-396, rasterizer_impl.cu:405-434) from given render-level gradients: dL/dmean2D (P,3),
+    dL/dconic in the reference's float4 layout (P,4: .x, .y with the 1/2 factor of backward.cu:550, .w) and
+    dL/dcolor (P,3).  Fed with a HIP run's own render gradients it checks the HIP preprocess backward's chain
+    without the render kernel's float-atomic order noise in its input."""
+    L = lib()
+    means3D = _f32(means3D).reshape(-1, 3)
+    P = means3D.shape[0]
+    M = fwd["M"]
+    _, shs_p = _opt(shs)
+    _, sc_p = _opt(scales)
+    _, ro_p = _opt(rotations)
+    cp_a, _ = _opt(cov3D_precomp)
+    dmean2D = np.ascontiguousarray(_f32(dL_dmean2D).reshape(P, 3))
+    dconic = np.ascontiguousarray(_f32(dL_dconic).reshape(P, 4))
+    dcolor = np.ascontiguousarray(_f32(dL_dcolor).reshape(P, 3))
     dmean3D = np.zeros((P, 3), np.float32)
     dcov3D = np.zeros((P, 6), np.float32)
     dsh = np.zeros((P, max(M, 0), 3), np.float32)
@@ -220,5 +241,4 @@ def backward(fwd, dL_dpix, means3D, *, shs=None, colors_precomp=None, scales=Non
                          float(scale_modifier), np.ascontiguousarray(cov_used), _f32(viewmatrix).reshape(16),
                          _f32(projmatrix).reshape(16), int(W), int(H), float(tanfovx), float(tanfovy),
                          _f32(campos).reshape(3), dmean2D, dconic, dcolor, dmean3D, dcov3D, dsh, dscale, drot)
-    return dict(dL_dmeans2D=dmean2D, dL_dcolors=dcolor, dL_dopacity=dopac, dL_dmeans3D=dmean3D,
-                dL_dcov3D=dcov3D, dL_dsh=dsh, dL_dscales=dscale, dL_drotations=drot, dL_dconic=dconic)
+    return dict(dL_dmeans3D=dmean3D, dL_dcov3D=dcov3D, dL_dsh=dsh, dL_dscales=dscale, dL_drotations=drot)

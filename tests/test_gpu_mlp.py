@@ -449,6 +449,19 @@ def test_eval_f32_matches_float64_oracle_and_training_forward(P, scale):
     assert torch.equal(ev, tr)
 
 
+def test_empty_point_set_gives_empty_heads():
+    """P = 0 (an empty point set, which the torch path always handled): empty heads of the right widths, with and
+    without autograd, and no native call that would reject P <= 0."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF
+    net = DirectTemporalNeRF().cuda()
+    x, t = torch.zeros(0, 3, device="cuda"), torch.zeros(0, 1, device="cuda")
+    with torch.no_grad():
+        outs = net(x, t, 5000)
+    assert [tuple(o.shape) for o in outs] == [(0, 3), (0, 3), (0, 4), (0, 48)]
+    outs = net(x.clone().requires_grad_(True), t, 5000)
+    assert [tuple(o.shape) for o in outs] == [(0, 3), (0, 3), (0, 4), (0, 48)]
+
+
 def test_eval_f32_matches_reference_network_fixture():
     """The evaluation kernel against the reference's own DirectTemporalNeRF run (tests/golden/mlp.npz): the four
     heads within 2e-5 of their scale."""

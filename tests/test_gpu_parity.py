@@ -47,7 +47,7 @@ def poison_allocator(nbytes=256 << 20):
     del t
 
 
-def gpu_backward(d, fwd, dpix, *, colors=None, cov3D=None, scale_modifier=1.0):
+def gpu_backward(d, fwd, dpix, *, colors=None, cov3D=None, scale_modifier=1.0, scratch=None):
     from gsd_amd import _C
     poison_allocator()
     num_rendered, color, radii, geom, binning, img = fwd
@@ -57,7 +57,7 @@ def gpu_backward(d, fwd, dpix, *, colors=None, cov3D=None, scale_modifier=1.0):
     return _C.rasterize_gaussians_backward(d["bg"], d["means3D"], radii, empty if colors is None else colors, scales,
                                            rots, scale_modifier, empty if cov3D is None else cov3D, d["viewmatrix"],
                                            d["projmatrix"], d["tanfovx"], d["tanfovy"], dpix, shs, d["sh_degree"],
-                                           d["campos"], geom, num_rendered, binning, img, False)
+                                           d["campos"], geom, num_rendered, binning, img, False, scratch=scratch)
 
 
 def oracle_fwd_bwd(oracle_mod, d, dpix=None, *, colors=None, cov3D=None, scale_modifier=1.0):
@@ -188,16 +188,24 @@ def test_backward_matches_oracle(oracle_mod, P, W, H, deg, seed):
         assert rel_l2(got, ob[name]) <= 1e-4, (name, rel_l2(got, ob[name]))
 
 
+# the per-Gaussian gradient record (gsd_kernels.h GradRecField): dL/dmean2D x, y; dL/dconic a, b, c; dL/dopacity;
+# dL/dcolor r, g, b -- 16 floats per Gaussian in the backward's scratch
+_REC_FLOATS = 16
+
+
 @pytest.mark.parametrize("lo,hi", [(5.0, 20.0), (40.0, 200.0)])
 def test_anisotropic_gaussians_forward_and_backward(oracle_mod, lo, hi):
     """Needle-like Gaussians (one axis lo-hi times the others, random rotations, opacities up to 0.999): their alpha
     boxes are loose and the linear ellipse bound over each 4x4 block does most of the list culling in both render
-    kernels (bwd_compact_groups).  The forward stays bit-exact and the render kernel's gradients (dL/dmean2D,
-    dL/dcolor, dL/dopacity) and dL/dsh match the oracle at this file's 1e-4.  The 2D covariances are near-singular in
-    float32 here (a c / det up to 2.7e3 at 5-20x, 2.5e5 at 40-200x): the reference's own conic -> cov3D -> scale /
-    rotation chain (backward.cu:144-274, 278-341) amplifies the float-atomic order noise of dL/dconic (measured: the
-    rotation gradient 4.4e-3 from the oracle at 5-20x, 2e-2 for dL/dmean3D at 40-200x).  So the chain's gradients are
-    held to the GPU's own run-to-run difference instead: within 20x of two backward launches' rel L2 (or 1e-4)."""
+    kernels (bwd_compact_groups).  The forward stays bit-exact; the render kernel's gradients (dL/dmean2D, dL/dconic
+    read from the backward's gradient records, dL/dcolor, dL/dopacity) and dL/dsh match the oracle at this file's
+    1e-4.  The 2D covariances are near-singular in float32 (a c / det up to 2.7e3 at 5-20x, 2.5e5 at 40-200x), so the
+    reference's own conic -> cov3D -> scale / rotation chain (backward.cu:144-274, 278-341) amplifies the last-bit
+    differences of dL/dconic (float-atomic order) into the 1e-3..1e-2 range for dL/dmeans3D, dL/dcov3D, dL/dscales
+    and dL/drotations.  That chain is pinned on its own instead: the oracle's preprocess backward
+    (oracle.preprocess_backward, backward.cu:144-396) fed with the HIP run's own render-level gradients must give
+    the HIP's four chain gradients within rel L2 1e-5; against the full oracle they stay under a fixed 5e-2."""
+    from gsd_amd import _C
     P, W, H, deg, seed = 5_000, 320, 240, 1, 11
     d = scene_inputs(P, W, H, deg, seed=seed, device=DEV)
     g = torch.Generator().manual_seed(seed)
@@ -210,20 +218,37 @@ def test_anisotropic_gaussians_forward_and_backward(oracle_mod, lo, hi):
     dpix = torch.randn(3, H, W, generator=g).mul_(1e-3).to(DEV)
     o, ob = oracle_fwd_bwd(oracle_mod, d, dpix)
     fwd = gpu_forward(d)
-    grads = [t.cpu().numpy() for t in gpu_backward(d, fwd, dpix)]
-    again = [t.cpu().numpy() for t in gpu_backward(d, fwd, dpix)]
+    scratch = torch.zeros(_C.backward_scratch_bytes(P), dtype=torch.uint8, device=DEV)
+    assert scratch.data_ptr() % 128 == 0   # the library aligns the records to 128 B: offset 0 here
+    grads = [t.cpu().numpy() for t in gpu_backward(d, fwd, dpix, scratch=scratch)]
+    torch.cuda.synchronize()
+    rec = scratch[: 4 * _REC_FLOATS * P].view(torch.float32).view(P, _REC_FLOATS).cpu().numpy()
+    vis = (fwd[2].cpu().numpy() > 0)[:, None]
+    dmean2D = np.where(vis, np.concatenate([rec[:, 0:2], np.zeros((P, 1), np.float32)], 1), 0).astype(np.float32)
+    dconic = np.where(vis, np.stack([rec[:, 2], rec[:, 3], np.zeros(P, np.float32), rec[:, 4]], 1), 0)
+    dconic = dconic.astype(np.float32)
+    dcolor = np.where(vis, rec[:, 6:9], 0).astype(np.float32)
     names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
              "dL_drotations"]
-    render_level = names[:3] + ["dL_dsh"]
-    for name, gt, g2 in zip(names, grads, again):
-        got = gt.reshape(ob[name].shape)
-        assert np.isfinite(got).all(), name
-        err = rel_l2(got, ob[name])
-        if name in render_level:
-            assert err <= 1e-4, (name, err)
-        else:
-            noise = rel_l2(got, g2.reshape(ob[name].shape))
-            assert err <= max(1e-4, 20 * noise), (name, err, noise)
+    got = {n: gt.reshape(ob[n].shape) for n, gt in zip(names, grads)}
+    # the records are what the API returned, and the render-level gradients match the oracle's
+    np.testing.assert_array_equal(got["dL_dmeans2D"], dmean2D)
+    np.testing.assert_array_equal(got["dL_dcolors"], dcolor)
+    assert rel_l2(dconic, ob["dL_dconic"]) <= 1e-4, ("dL_dconic", rel_l2(dconic, ob["dL_dconic"]))
+    for n in ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dsh"]:
+        assert np.isfinite(got[n]).all(), n
+        assert rel_l2(got[n], ob[n]) <= 1e-4, (n, rel_l2(got[n], ob[n]))
+    kw = oracle_kwargs(d)
+    pre = oracle_mod.preprocess_backward(o, dmean2D, dconic, dcolor, d["means3D"].cpu().numpy(), shs=kw["shs"],
+                                         scales=kw["scales"], rotations=kw["rotations"],
+                                         viewmatrix=kw["viewmatrix"], projmatrix=kw["projmatrix"],
+                                         campos=kw["campos"], W=W, H=H, tanfovx=kw["tanfovx"],
+                                         tanfovy=kw["tanfovy"], sh_degree=deg)
+    for n in ["dL_dmeans3D", "dL_dcov3D", "dL_dscales", "dL_drotations"]:
+        assert np.isfinite(got[n]).all(), n
+        e_chain = rel_l2(got[n], pre[n])
+        assert e_chain <= 1e-5, (n, "vs the oracle chain on the HIP's records", e_chain)
+        assert rel_l2(got[n], ob[n]) <= 5e-2, (n, "vs the full oracle", rel_l2(got[n], ob[n]))
 
 
 @pytest.mark.parametrize("short_binning", [False, True])

@@ -464,7 +464,7 @@ def test_step_in_backward_with_offset_network():
     the network is stepped on leaving the block -- all equal to backward() + step."""
     from gsd_amd.deform_mlp import DirectTemporalNeRF
     res = []
-    for fused in (True, False):
+    for fused in (True, False, False, False):   # one fused run, three unfused runs for the noise figure
         torch.manual_seed(0)
         net = DirectTemporalNeRF().to(DEV)
         with torch.no_grad():
@@ -474,14 +474,16 @@ def test_step_in_backward_with_offset_network():
     assert res[0][2] == res[1][2]
     # Bars: the Gaussians' parameters and moments 1e-4 (the rasterizer's float-atomic order, ~1e-6 relative per
     # gradient, is all that differs).  The network's gradients are sums over the 6,000 Gaussians that mostly cancel
-    # (layer-0 weight gradients ~1e-9 from terms ~1e-6), which amplifies that same noise by up to ~1e3: its moments
-    # get 2e-3 (a run at round 5's close measured 2.3e-4 on one of them), its parameters the Gaussians' 1e-4.
-    n_gauss = 6
+    # (layer-0 weight gradients ~1e-9 from terms ~1e-6), which amplifies that same noise by up to ~1e3.  So each
+    # tensor's bar is measured: 20x the largest rel L2 between the three unfused runs (the same float-atomic order
+    # noise, with no fusion in it), with the Gaussians' 1e-4 as the floor.
     n_params = len(res[0][0])
-    tensors = list(zip(res[0][0] + res[0][1], res[1][0] + res[1][1]))
-    for k, (x, y) in enumerate(tensors):
-        net_moment = k >= n_params and (k - n_params) // 2 >= n_gauss
-        assert rel_l2(x, y) <= (2e-3 if net_moment else 1e-4), (k, rel_l2(x, y))
+    flat = [r[0] + r[1] for r in res]
+    for k in range(len(flat[0])):
+        noise = max(rel_l2(flat[i][k], flat[j][k]) for i, j in ((1, 2), (1, 3), (2, 3)))
+        bar = max(1e-4, 20.0 * noise)
+        err = rel_l2(flat[0][k], flat[1][k])
+        assert err <= bar, (k, "moment" if k >= n_params else "param", err, noise)
 
 
 def test_step_in_backward_rejects_second_producer():
