@@ -71,9 +71,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_GINST = 1024 * 0.5 * 2.4
 
 
-def algorithmic_bytes(P, V, K, W, H, C):
+# Adam's per-Gaussian parameter floats (xyz 3, f_dc 3, f_rest 45, opacity 1, scaling 3, rotation 4) and its bytes per
+# float when fused into the preprocess backward: param, exp_avg, exp_avg_sq each read and written (the gradient is
+# formed in registers, never stored)
+ADAM_FLOATS_PER_G = 59
+FUSED_ADAM_BYTES_PER_FLOAT = 24
+
+
+def algorithmic_bytes(P, V, K, W, H, C, adam_fused=False):
     """Per-launch algorithmic HBM bytes of each kernel (DESIGN.md 'Roofline');
-    P Gaussians, V visible, K instances, C = (D+1)^2 SH coefficients."""
+    P Gaussians, V visible, K instances, C = (D+1)^2 SH coefficients.  adam_fused: the bench step at N = 1, where
+    the preprocess backward carries the Adam step (gsd_adam_epilogue) -- its bytes are then Adam's 24 B per
+    parameter float over all P (the parameter reads serve the backward's own inputs: means, scales, rotations,
+    opacities, SH), plus radii 4, the gradient record 48, the clamp flags 1 read and dL/dmean2D 12 written per
+    Gaussian; no gradient of a parameter is stored."""
     T = ((W + 15) // 16) * ((H + 15) // 16)
     npix = W * H
     return {
@@ -84,7 +95,8 @@ def algorithmic_bytes(P, V, K, W, H, C):
         "tile_sort": 8 * T + 8 * K + 4 * K,
         "render_fwd": 8 * T + 44 * K + 20 * npix,
         "render_bwd": 8 * T + 44 * K + 20 * npix + 44 * V,
-        "preprocess_bwd": 4 * P + (85 + 12 * C) * V + (64 + 12 * C) * V,
+        "preprocess_bwd": (FUSED_ADAM_BYTES_PER_FLOAT * ADAM_FLOATS_PER_G * P + (4 + 48 + 1 + 12) * P if adam_fused
+                           else 4 * P + (85 + 12 * C) * V + (64 + 12 * C) * V),
         "l1_ssim": 3 * npix * (8 + 12),         # img, gt in; window adjoints out
         "l1_ssim_bwd": 3 * npix * (12 + 8 + 4),  # adjoints, img, gt in; dL/dimg out
         "adam": 32 * P * (3 + 3 + 45 + 1 + 3 + 4),
@@ -147,6 +159,35 @@ def work_counts(kernel, workload):
         if d.get("_workload") == workload and kernel in d:
             return dict(d[kernel], source=os.path.relpath(f, ROOT))
     return None
+
+
+# the kernels behind each C-ABI timing slot (gsd_capi.hip kKernelNames), by their PMC short names (pmc_traffic.py)
+TIMING_SLOT_KERNELS = {
+    "preprocess_fwd": ["preprocess_fwd"], "tile_hist": ["tile_hist", "colscan_partial", "colscan_final"],
+    "tile_scan": ["tile_scan"], "scatter_keys": ["scatter_hist"], "tile_sort": ["tile_sort"],
+    "render_fwd": ["render_fwd"], "render_bwd": ["render_bwd"],
+    "preprocess_bwd": ["preprocess_bwd_sh_adam", "preprocess_bwd"], "l1_ssim": ["ssim_fwd", "loss_sum"],
+    "l1_ssim_bwd": ["ssim_bwd"], "densify_stats": ["densify_stats"],
+}
+
+
+def kernels_vs_hbm(per_kernel, ab, workload):
+    """Every timed slot of the step against HBM: algorithmic bytes / live launch time vs 8 TB/s, and -- where a
+    committed PMC summary of the bench step itself (workload "cfgN-step", rocprofv3 --pmc over bench.py) holds every
+    kernel of the slot -- the measured bytes and their ratio to the algorithmic ones."""
+    out = {}
+    for k, ms in per_kernel.items():
+        if k not in ab or ms <= 0:
+            continue
+        gbs = ab[k] / (ms * 1e-3) / 1e9
+        e = {"algorithmic_bytes": int(ab[k]), "gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        trs = [pmc_traffic(n, workload) for n in TIMING_SLOT_KERNELS.get(k, [k])]
+        if trs and all(t is not None and t.get("hbm_bytes") is not None for t in trs):
+            e["traffic"] = int(sum(t["hbm_bytes"] for t in trs))
+            e["traffic_over_algorithmic"] = round(e["traffic"] / max(ab[k], 1), 3)
+            e["traffic_source"] = trs[0]["source"]
+        out[k] = e
+    return out
 
 
 def roofline(kernel, ms, nbytes, workload):
@@ -344,7 +385,7 @@ def main():
     from gsd_amd import _C as gsdC
     from gsd_amd._native import kernel_times
     from gsd_amd.camera import synthetic_camera
-    from gsd_amd.parallel import init_from_env
+    from gsd_amd.parallel import dp_active, init_from_env
     from gsd_amd.scene import CONFIGS, make_gaussians
 
     rank, local, world = init_from_env()
@@ -571,12 +612,17 @@ def main():
         per_kernel = {k: tot / max(n, 1) for k, (tot, n) in kt.items()}
         dom = max(kt, key=lambda k: kt[k][0]) if kt else None
         roof = None
+        adam_fused = FUSED_STEP and net is None and world == 1 and not dp_active()
+        kernel_hbm = kernels_vs_hbm(per_kernel, algorithmic_bytes(int(pc._xyz.shape[0]), V, K, W, H,
+                                                                  (min(D, 3) + 1) ** 2, adam_fused=adam_fused),
+                                    f"cfg{args.config}-step")
         if dom in mfma_flops(1):   # the deformation network's training call (--with-mlp): the matrix cores
             roof = mfma_roofline(dom, per_kernel[dom], mfma_flops(int(pc._xyz.shape[0]))[dom],
                                  f"cfg{args.config}+mlp")
         elif dom:
             # the kernel-timing pass's scene: V and K of its last view, P of that view (no densification in it)
-            nbytes = algorithmic_bytes(int(pc._xyz.shape[0]), V, K, W, H, (min(D, 3) + 1) ** 2).get(dom)
+            nbytes = algorithmic_bytes(int(pc._xyz.shape[0]), V, K, W, H, (min(D, 3) + 1) ** 2,
+                                       adam_fused=adam_fused).get(dom)
             if nbytes:
                 roof = roofline(dom, per_kernel[dom], nbytes, f"cfg{args.config}")
         cpu = None
@@ -614,6 +660,7 @@ def main():
             "fwd_bwd_ms_per_view": round(fwd_bwd_ms, 4),
             "fwd_bwd_ms_per_view_host_synced": round(fwd_bwd_synced_ms, 4),
             "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+            "kernels_hbm": kernel_hbm,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

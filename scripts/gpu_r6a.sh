@@ -18,7 +18,7 @@ fi
 pick() { for c in "$@"; do grep -qw "$c" "$O/counters.txt" && printf '%s ' "$c"; done; }
 S1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"
 S2="$(pick SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC)GRBM_GUI_ACTIVE"
-S3="$(pick SQ_INSTS_VMEM SQ_INSTS_FLAT SQ_ACTIVE_INST_FLAT SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_EXP)GRBM_GUI_ACTIVE"
+S3="$(pick SQ_INSTS_VMEM SQ_INSTS_FLAT SQ_ACTIVE_INST_FLAT SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_TRANS_F32 SQ_THREAD_CYCLES_VALU SQ_LEVEL_WAVES)GRBM_GUI_ACTIVE"
 echo "S2=$S2"; echo "S3=$S3"
 PMC_OUT="$O/stall_cfg4" KREGEX=render PROF_ARGS="--config 4 --iters 3" PMC_PASSES="$S1;$S2;$S3" bash scripts/gpu_pmc.sh || exit 1
 # the bench step's kernels (bench.py itself after --, no wrapper): traffic and VALU / stall figures per kernel
