@@ -557,6 +557,17 @@ def main():
         ts.sort()
         return ts[len(ts) // 2]
 
+    # GSD_BENCH_STEP_ONLY=1 (profiling: rocprofv3 --pmc over this script): only the warmup and the timed steps, so
+    # every launch the counters see is a bench step's; the line then carries no fwd+bwd or per-kernel figures
+    if os.environ.get("GSD_BENCH_STEP_ONLY") == "1":
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": round(world * args.steps / elapsed, 3), "unit": "views/s",
+                              "n_gpus": world, "steps": args.steps, "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+                              "step_only": True}), flush=True)
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     fwd_bwd_ms = fwd_bwd(True)
     fwd_bwd_synced_ms = fwd_bwd(False)
 
@@ -600,7 +611,8 @@ def main():
     # per-kernel device times: a separate pass of full steps with the C-ABI's hipEvent timing on
     restore()
     kernel_times(enable=True, reset=True)
-    for _ in range(min(20, max(5, args.steps))):
+    n_timing_steps = min(20, max(5, args.steps))
+    for _ in range(n_timing_steps):
         out = step()
     torch.cuda.synchronize()
     kt = kernel_times(enable=False, reset=True)
@@ -660,6 +672,7 @@ def main():
             "fwd_bwd_ms_per_view": round(fwd_bwd_ms, 4),
             "fwd_bwd_ms_per_view_host_synced": round(fwd_bwd_synced_ms, 4),
             "kernels_ms": {k: round(v, 4) for k, v in per_kernel.items()},
+            "kernel_launches_per_step": {k: round(n / n_timing_steps, 2) for k, (tot, n) in kt.items()},
             "kernels_hbm": kernel_hbm,
             "roofline": roof,
             "cpu_baseline": cpu,
