@@ -276,24 +276,17 @@ __device__ __forceinline__ float record_og(float4 pc, float2 bt, float pxf, floa
 #endif
 }
 
-// A float constant held in an SGPR: the VALU op that reads it keeps its 4-byte VOP2 encoding (an SGPR is a legal
-// src0) instead of carrying a 32-bit literal (8 bytes).  The 8-byte forms -- literal, VOP3, DPP -- cost ~4.5 cycles
-// per wave64 instruction against ~3 for the 4-byte ones at the render kernels' occupancy
-// (scripts/calib/valu_cost.hip, profiles/round6/).  Materialised once per kernel, ahead of the loops.
-__device__ __forceinline__ float sgpr_const(float v) {
-    int i = __float_as_int(v);
-    asm volatile("" : "+s"(i));
-    return __int_as_float(i);
-}
-
-// 1/d from v_rcp_f32 (1 ulp) plus one Newton step: ~0.5 ulp in 3 VALU ops instead of the ~10 of the
-// correctly rounded division sequence.
+// 1/d from v_rcp_f32 (1 ulp) -- the backward's T recovery (backward.cu:503) -- instead of the ~10 VALU ops of the
+// correctly rounded division.  Round 6: without the Newton step that took it to ~0.5 ulp (-DGSD_NEWTON_RCP restores
+// it): k_render_bwd is VALU-issue bound (profiles/round6/stall_cfg4/), and the two FMAs per (pixel, record) step cost
+// 2.4 % of it (0.3813 / 0.3788 / 0.3759 ms against 0.3885 / 0.3901 / 0.3849, profiles/round6/render_ab/); the
+// gradients stay inside the parity bars (rel L2 1e-4, tests/test_gpu_parity.py).
 __device__ __forceinline__ float fast_recip(float d) {
     float r = __builtin_amdgcn_rcpf(d);
-#ifdef GSD_BARE_RCP
-    return r;
-#else
+#ifdef GSD_NEWTON_RCP
     return fmaf(fmaf(-d, r, 1.0f), r, r);
+#else
+    return r;
 #endif
 }
 
@@ -337,7 +330,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             p.zero_rec[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (over_capacity(p.k_guard, p.k_cap)) return;
-    const float k099 = sgpr_const(0.99f);  // forward.cu:343's clamp
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);
     // `done` (the pixel has saturated, or lies outside the image) as the wave's lane mask: the per-record
     // decisions below are lane masks combined on the scalar unit and used as select masks
@@ -396,10 +388,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             m = max(m, cnt[g]);
             mine = tg.lane / (64 / kFwdGroups) == g ? cnt[g] : mine;
         }
-        // the list index of the lane's last taken record in this round (-1: none): a select on a scalar per taken
-        // step, turned into the contributor count once per round below -- instead of forming the count
-        // (i * 256 + slot + 1, an 8-byte SDWA add) at every taken step
-        int lc_idx = -1;
         for (int j0 = 0; j0 < m; j0 += kBatch) {
             if (done_m == ~0ull) break;  // every pixel of this wave has saturated
             // branch-free alphas of kBatch records (independent: the exps overlap) ...
@@ -423,7 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 in_m[u] = wave_ballot(j0 + u < mine);
 #endif
                 slot[u] = (int)((w4 >> (8 * u)) & 0xffu);
-                a[u] = fminf(k099, record_og(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u]));
+                a[u] = fminf(0.99f, record_og(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u]));
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
             // One wave-uniform branch per record (skipped when no lane takes it), the lane decisions as selects:
@@ -457,11 +445,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 C1 = fmaf(c.y, wgt, C1);
                 C2 = fmaf(c.z, wgt, C2);
                 T = take ? test_T : T;
-                lc_idx = take ? j0 + u : lc_idx;
+                last_contributor = take ? (uint32_t)(i * kTilePix + slot[u] + 1) : last_contributor;
             }
         }
-        // forward.cu:359: the 1-based list position of the last composited record
-        if (lc_idx >= 0) last_contributor = (uint32_t)(i * kTilePix + (int)list[lc_idx] + 1);
     }
 #ifdef GSD_COUNT_WORK
     count_work(0, n_steps, n_pairs);
@@ -820,7 +806,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
     const TileGeom tg = tile_geom(p.num_tiles, p.grid_x, p.W, p.H, true);  // the forward's 4x4-group lane map
     const int tid = threadIdx.x;
     const int lane = tg.lane, u16 = lane & 15, grp = lane >> 4;
-    const float k099 = sgpr_const(0.99f);  // backward.cu:499's clamp
     const uint2 rg = p.ranges[tg.tile];
     const int pid = p.W * tg.py + tg.px;
     const int plane = p.H * p.W;
@@ -944,7 +929,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
 #pragma clang fp contract(fast)
                             const bool valid = __builtin_amdgcn_inverse_ballot_w64(valid_m);
                             const float og = valid ? OG : 0.f;
-                            const float alpha = fminf(k099, og);
+                            const float alpha = fminf(0.99f, og);
                             const float inv1ma = fast_recip(1.f - alpha);
                             T = T * inv1ma;  // backward.cu:503 (T recovered by division)
 #ifndef GSD_BWD_NO_FMAC_DPP

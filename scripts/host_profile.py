@@ -15,10 +15,11 @@ from gsd_amd import DeformableGaussians, default_pipe, render, training_loss  # 
 from gsd_amd.camera import synthetic_camera  # noqa: E402
 from gsd_amd.scene import CONFIGS, make_gaussians  # noqa: E402
 
-cfg = CONFIGS[4]
+CFG = int(sys.argv[1]) if len(sys.argv) > 1 else 4   # python scripts/host_profile.py [config]
+cfg = CONFIGS[CFG]
 P, W, H, D = cfg["P"], cfg["W"], cfg["H"], cfg["sh_degree"]
 dev = torch.device("cuda:0")
-pc = DeformableGaussians(make_gaussians(P, W, H, seed=4).to(dev), sh_degree=D)
+pc = DeformableGaussians(make_gaussians(P, W, H, seed=CFG).to(dev), sh_degree=D)
 cam = synthetic_camera(W, H).to(dev)
 bg = torch.zeros(3, device=dev)
 pipe = default_pipe()
@@ -38,6 +39,8 @@ def step():   # bench.py's fused N = 1 step
 for _ in range(10):
     step()
 torch.cuda.synchronize()
+import time  # noqa: E402
+T0 = time.perf_counter()
 pr = cProfile.Profile()
 pr.enable()
 for _ in range(50):
@@ -45,5 +48,6 @@ for _ in range(50):
 torch.cuda.synchronize()
 pr.disable()
 st = pstats.Stats(pr)
+print("host+device per step under cProfile: %.3f ms" % (1e3 * (time.perf_counter() - T0) / 50))
 st.sort_stats("tottime").print_stats(40)
 st.sort_stats("cumulative").print_stats(40)
