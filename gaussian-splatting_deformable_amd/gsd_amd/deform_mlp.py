@@ -376,3 +376,118 @@ class DirectTemporalNeRF(nn.Module):
         b = torch.cat([m.bias for m in heads], dim=0)
         o = _Linear.apply(h, W, b, False).float()
         return tuple(t.contiguous() for t in o.split([m.out_features for m in heads], dim=-1))
+
+
+class DirectTemporalNeRF_se3(nn.Module):
+    """The reference's SE(3) twist producer ``DirectTemporalNeRF_se3`` (scene/gaussian_model.py:99-173; dormant in the
+    reference's training loop): an 8-layer, 256-wide ReLU MLP on the raw point and time (no positional
+    encoding: ``input_ch`` 3 + ``input_ch_time`` 1), the point re-injected after layer 4 (``cat([x, h])``), and two
+    linear heads w (3) and v (3).  ``forward`` returns what the reference returns: the (P, 4, 4) transform
+    ``exp_se3([w, v] / |w|, |w|)`` (rigid_body.py:86-93) -- the identity where |w| = 0 instead of the reference's NaN
+     -- or ``zeros_like(x[:, :4])`` before iteration 3000 (:168-171).  ``twist`` returns the raw (P, 6) [w, v]
+    that ``render()``'s SE(3) mode takes (``DeformableGaussians(..., deform="se3", twist_model=net.twist)``): the
+    fused HIP exp-map (gsd_deform.hip) normalises it with the same |w| guard and moves means and rotations.
+
+    Parameter names and shapes are the reference's (``_time.{0..7}``, ``_w``, ``_v``), so its state dicts load as
+    they are.  In float32 on a HIP device the network runs on DirectTemporalNeRF's training kernels
+    (gsd_mlp_train.hip, BF16x6): this architecture IS that one with structurally zero weights -- the raw point is
+    channels 0-2 of the positional encoding and the raw time channel 63 of the layer-0 input, the skip layer's
+    re-injected point columns 0-2 of its encoding block, and w / v the first two heads (dx, d log-scale) with the
+    other heads zero.  Zero weights contribute exact zeros to every f32 accumulation, so the kernels compute this
+    network's values; the padded weights are built from the parameters by differentiable concatenation, so autograd
+    hands the real entries' gradients back to the parameters and drops the structural zeros'."""
+
+    def __init__(self, D: int = 8, W: int = 256, input_ch: int = 3, input_ch_time: int = 1, skips=(4,),
+                 zero_before: int = 3000):
+        super().__init__()
+        self.D, self.W, self.skips = D, W, tuple(skips)
+        self.input_ch, self.input_ch_time = input_ch, input_ch_time
+        self.zero_before = zero_before
+        layers = [nn.Linear(input_ch + input_ch_time, W)]
+        for i in range(D - 1):
+            layers.append(nn.Linear(W + (input_ch if i in self.skips else 0), W))
+        self._time = nn.ModuleList(layers)
+        self._w = nn.Linear(W, 3)
+        self._v = nn.Linear(W, 3)
+
+    def _hip_f32(self, x: torch.Tensor) -> bool:
+        return ((self.D, self.W, self.skips, self.input_ch, self.input_ch_time) == (8, 256, (4,), 3, 1)
+                and x.device.type == "cuda" and not os.environ.get("GSD_MLP_TORCH")
+                and all(p.dtype == torch.float32 and p.device == x.device for p in self.parameters()))
+
+    def _padded(self):
+        """The twelve weights and biases of the reference-architecture network (DirectTemporalNeRF's C-ABI order)
+        that computes this one: see the class docstring."""
+        W = self.W
+        hid = list(self._time)
+        z = lambda r, c, like: like.new_zeros(r, c)  # noqa: E731
+        w0 = hid[0].weight   # (W, 4): x 0-2, t 3
+        ws = [torch.cat([w0[:, :3], z(W, 60, w0), w0[:, 3:4], z(W, 20, w0)], 1)]
+        for i in range(1, self.D):
+            w = hid[i].weight
+            if (i - 1) in self.skips:   # cat([x, h]): x into the encoding block's first three columns
+                w = torch.cat([w[:, :3], z(W, 60, w), w[:, 3:]], 1)
+            ws.append(w)
+        ref = self._w.weight
+        ws += [self._w.weight, self._v.weight, z(4, W, ref), z(48, W, ref)]
+        bs = [m.bias for m in hid] + [self._w.bias, self._v.bias, ref.new_zeros(4), ref.new_zeros(48)]
+        return ws, bs
+
+    def query_time(self, x: torch.Tensor, ts: torch.Tensor):
+        """gaussian_model.py:142-150 -> (w, v), each (P, 3)."""
+        if self._hip_f32(x) and x.shape[0] > 0:
+            ws, bs = self._padded()
+            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+                heads = _MLPTrainF32.apply(x, ts, *ws, *bs)
+            else:
+                with torch.no_grad():
+                    heads = _MLPTrainF32.apply(x, ts, *[w.detach() for w in ws], *[b.detach() for b in bs])
+            return heads[0], heads[1]
+        h = torch.cat([x, ts.to(x.dtype).expand(x.shape[0], 1)], dim=-1)
+        for i, layer in enumerate(self._time):
+            h = torch.relu(layer(h))
+            if i in self.skips:
+                h = torch.cat([x, h], dim=-1)
+        return self._w(h), self._v(h)
+
+    def twist(self, x: torch.Tensor, ts: torch.Tensor, iteration: int) -> torch.Tensor:
+        """(P, 6) raw [w, v] for render()'s SE(3) mode; zeros (the identity motion) before iteration 3000."""
+        if iteration < self.zero_before:
+            return x.new_zeros(x.shape[0], 6)
+        w, v = self.query_time(x, ts)
+        return torch.cat([w, v], dim=-1)
+
+    def forward(self, x: torch.Tensor, ts: torch.Tensor, iteration: int) -> torch.Tensor:
+        """gaussian_model.py:153-173: the (P, 4, 4) transform, or before iteration 3000 the reference's
+        ``torch.zeros_like(input_pts[:, :4])`` -- (P, 3) zeros for (P, 3) points, as written."""
+        if iteration < self.zero_before:
+            return torch.zeros_like(x[:, :4])
+        w, v = self.query_time(x, ts)
+        return se3_transform(torch.cat([w, v], dim=-1))
+
+
+def se3_transform(twist: torch.Tensor) -> torch.Tensor:
+    """(P, 6) raw [w, v] -> (P, 4, 4) exp_se3 of the unit screw axis [w, v] / |w| by the angle |w|
+    (rigid_body.py:61-65, 86-93, gaussian_model.py:161-165): R = I + sin t W + (1 - cos t) W^2,
+    p = (t I + (1 - cos t) W + (t - sin t) W^2) v / t, W = skew(w / t); the identity where t = 0."""
+    w, v = twist[:, :3], twist[:, 3:]
+    th = torch.linalg.vector_norm(w, dim=-1)
+    safe = torch.where(th > 0, th, torch.ones_like(th))
+    wn, vn = w / safe[:, None], v / safe[:, None]
+    Z = torch.zeros_like(th)
+    Wm = torch.stack([torch.stack([Z, -wn[:, 2], wn[:, 1]], -1), torch.stack([wn[:, 2], Z, -wn[:, 0]], -1),
+                      torch.stack([-wn[:, 1], wn[:, 0], Z], -1)], -2)
+    W2 = Wm @ Wm
+    s, c = torch.sin(th)[:, None, None], torch.cos(th)[:, None, None]
+    eye = torch.eye(3, dtype=twist.dtype, device=twist.device).expand(twist.shape[0], 3, 3)
+    R = eye + s * Wm + (1.0 - c) * W2
+    t = th[:, None, None]
+    p = ((t * eye + (1.0 - c) * Wm + (t - s) * W2) @ vn[:, :, None])[..., 0]
+    on = (th > 0)[:, None, None]
+    R = torch.where(on, R, eye)
+    p = torch.where(on[..., 0], p, torch.zeros_like(p))
+    T = torch.zeros(twist.shape[0], 4, 4, dtype=twist.dtype, device=twist.device)
+    T[:, :3, :3] = R
+    T[:, :3, 3] = p
+    T[:, 3, 3] = 1.0
+    return T

@@ -154,3 +154,80 @@ def test_fused_mlp_packing_emulated():
         dm._PERM16 = saved
     bad = torch.as_tensor(_emulate_fused_mlp(f2, b2, x.numpy(), t.numpy()))
     assert float((bad - ref).abs().max() / ref.abs().max()) > 0.1
+
+
+# ---- DirectTemporalNeRF_se3 (scene/gaussian_model.py:99-173) against the reference's own run (tests/golden/mlp_se3.npz)
+def se3net_weights(named_params, seed=82):
+    """The fixture's weights, regenerated as tests/golden/make_golden.py:se3net_weights draws them."""
+    import math
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in named_params:
+            fan_in = p.shape[1] if p.dim() == 2 else p.shape[0]
+            if name.endswith("bias"):
+                fan_in = 256
+            p.copy_((torch.rand(p.shape, generator=g) * 2.0 - 1.0) / math.sqrt(fan_in))
+
+
+def se3net_from_fixture(device="cpu"):
+    from conftest import golden
+    from gsd_amd.deform_mlp import DirectTemporalNeRF_se3
+    g = golden("mlp_se3.npz")
+    net = DirectTemporalNeRF_se3()
+    se3net_weights(list(net.named_parameters()))
+    return net.to(device), g
+
+
+def _rel(a, b):
+    a, b = torch.as_tensor(a).detach().double(), torch.as_tensor(b).detach().double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def test_se3net_parameter_names_are_the_references():
+    from gsd_amd.deform_mlp import DirectTemporalNeRF_se3
+    sd = DirectTemporalNeRF_se3().state_dict()
+    assert list(sd)[:2] == ["_time.0.weight", "_time.0.bias"] and list(sd)[-4:] == ["_w.weight", "_w.bias",
+                                                                                    "_v.weight", "_v.bias"]
+    assert sd["_time.0.weight"].shape == (256, 4) and sd["_time.5.weight"].shape == (256, 259)
+
+
+def test_se3net_matches_reference_fixture_cpu():
+    """The torch path (CPU): query_time's w / v, the transform, the zeros before 3000 and the autograd gradients of
+    the moved points against the reference's DirectTemporalNeRF_se3 run."""
+    net, g = se3net_from_fixture()
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    t = torch.from_numpy(g["t"])
+    w, v = net.query_time(x, t)
+    assert _rel(w, g["w"]) <= 1e-5 and _rel(v, g["v"]) <= 1e-5
+    T = net(x, t, 5000)
+    assert float((T.detach() - torch.from_numpy(g["T"])).abs().max()) <= 1e-6
+    z = net(x.detach(), t, 2000)
+    assert z.shape == g["zero2000"].shape and not z.any()
+    moved = (T @ torch.cat([x, torch.ones_like(x[:, :1])], 1)[..., None])[:, :3, 0]
+    assert float((moved.detach() - torch.from_numpy(g["moved"])).abs().max()) <= 1e-6
+    params = dict(net.named_parameters())
+    names = [str(n) for n in g["names"]]
+    grads = torch.autograd.grad((moved * torch.from_numpy(g["upstream"])).sum(), [x] + [params[n] for n in names])
+    assert _rel(grads[0], g["grad:x"]) <= 1e-4
+    for n, gr in zip(names, grads[1:]):
+        assert _rel(gr, g["grad:" + n]) <= 1e-4, n
+
+
+def test_se3net_padded_weights_compute_the_same_network_cpu():
+    """The structurally-zero embedding into DirectTemporalNeRF's layout (what the HIP kernels take), evaluated by
+    the reference architecture's torch restatement on [enc(x), enc(t)]: the same w / v."""
+    from gsd_amd.deform_mlp import positional_encoding
+    net, g = se3net_from_fixture()
+    ws, bs = net._padded()
+    assert [tuple(w.shape) for w in ws] == [(256, 84)] + [(256, 256)] * 4 + [(256, 319)] + [(256, 256)] * 2 + \
+        [(3, 256), (3, 256), (4, 256), (48, 256)]
+    x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["t"])
+    ex = positional_encoding(x, 10)
+    h = torch.cat([ex, positional_encoding(t, 10)], -1)
+    for i in range(8):
+        h = torch.relu(h @ ws[i].t() + bs[i])
+        if i == 4:
+            h = torch.cat([ex, h], -1)
+    w = h @ ws[8].t() + bs[8]
+    v = h @ ws[9].t() + bs[9]
+    assert _rel(w, g["w"]) <= 1e-5 and _rel(v, g["v"]) <= 1e-5

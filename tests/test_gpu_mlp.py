@@ -497,3 +497,50 @@ def test_train_f32_fallback_kernels():
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout and "failed" not in r.stdout
+
+
+def test_se3net_hip_path_matches_reference_fixture():
+    """DirectTemporalNeRF_se3 on the HIP training kernels (its weights embedded, structurally zero elsewhere, in
+    DirectTemporalNeRF's layout) and the fused HIP exp-map (se3_deform): w / v, the moved means and the gradients
+    of the reference's weighted sum of them (x and the parameters, through the kernels' backward) against the
+    reference's own run (tests/golden/mlp_se3.npz)."""
+    from test_deform_mlp import _rel, se3net_from_fixture
+    from gsd_amd._native import kernel_times
+    from gsd_amd.deform import se3_deform
+    net, g = se3net_from_fixture("cuda")
+    x = torch.from_numpy(g["x"]).cuda().requires_grad_(True)
+    t = torch.from_numpy(g["t"]).cuda()
+    kernel_times(enable=True, reset=True)
+    tw = net.twist(x, t, 5000)
+    moved, _ = se3_deform(tw, x)
+    names = [str(n) for n in g["names"]]
+    params = dict(net.named_parameters())
+    grads = torch.autograd.grad((moved * torch.from_numpy(g["upstream"]).cuda()).sum(), [x] + [params[n] for n in names])
+    torch.cuda.synchronize()
+    kt = kernel_times(enable=False, reset=True)
+    assert "deform_mlp_train_fwd" in kt and "deform_mlp_train_bwd" in kt and "se3_fwd" in kt, sorted(kt)
+    assert _rel(tw[:, :3].cpu(), g["w"]) <= 2e-5 and _rel(tw[:, 3:].cpu(), g["v"]) <= 2e-5
+    assert float((moved.detach().cpu() - torch.from_numpy(g["moved"])).abs().max()) <= 2e-6
+    assert _rel(grads[0].cpu(), g["grad:x"]) <= 1e-4
+    for n, gr in zip(names, grads[1:]):
+        assert _rel(gr.cpu(), g["grad:" + n]) <= 1e-4, n
+    assert not net(x.detach(), t, 2000).any()
+
+
+def test_se3net_drives_render_se3_mode():
+    """render() in the SE(3) mode with the network as its twist producer (twist_model=net.twist): the frame renders
+    and a loss on it reaches every layer of the network through the rasterizer, the exp-map and the kernels."""
+    from gsd_amd import DeformableGaussians, default_pipe, render
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.deform_mlp import DirectTemporalNeRF_se3
+    from gsd_amd.scene import make_gaussians
+    torch.manual_seed(5)
+    net = DirectTemporalNeRF_se3().cuda()
+    P, W, H = 4000, 160, 128
+    pc = DeformableGaussians(make_gaussians(P, W, H, seed=3).to("cuda"), sh_degree=3, deform="se3",
+                             twist_model=net.twist)
+    cam = synthetic_camera(W, H).to("cuda")
+    out = render(cam, pc, default_pipe(), torch.zeros(3, device="cuda"), iteration=5000)
+    assert out["means3D_offset"].abs().max() > 0
+    out["render"].square().sum().backward()
+    assert all(p.grad is not None and p.grad.abs().sum() > 0 for p in net.parameters())
