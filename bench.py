@@ -430,7 +430,25 @@ def main():
     # step; identical semantics)
     seed = torch.ones((), device=dev)
 
+    # The step as one native call (gsd_amd.train_step.FusedTrainStep: the drop-in path's kernels with the same
+    # arguments, its argument structures built once) where it applies -- one rank, no offsets / SE(3) -- so the host
+    # does not pace small views; GSD_TRAIN_STEP=0 times the drop-in API path (render + training_loss +
+    # step_in_backward + add_densification_stats) instead.  Both are timed below (value: the former).
+    fused_step = None
+    if FUSED_STEP and world == 1 and net is None and not se3 and os.environ.get("GSD_TRAIN_STEP", "1") != "0":
+        from gsd_amd.train_step import FusedTrainStep
+        fused_step = FusedTrainStep(pc, opt, cam, target, bg, 0.2, densifier=dens)
+
     def step():
+        if fused_step is not None:
+            out = fused_step()
+            nstep[0] += 1
+            if densify_every and nstep[0] % densify_every == 0:
+                dens.densify_and_prune(0.0002, 0.005, 10.0, None)
+            return out
+        return dropin_step()
+
+    def dropin_step():
         out = render(cam, pc, pipe, bg, iteration)
         # train.py:323-332 + :529, lambda_dssim = 0.2: the offset-norm term is 0 (and skipped) when nothing moves
         # the means (configurations 2, 4, 5); in the SE(3) mode (1, 3) it is the moved distance's mean norm
@@ -533,6 +551,37 @@ def main():
                 dist.all_reduce(lo, op=dist.ReduceOp.MIN)
                 dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             replicas = bool(int(lo.item()) == int(hi.item()))
+    # GSD_BENCH_STEP_ONLY=1 (profiling: rocprofv3 --pmc over this script): only the warmup and the timed steps, so
+    # every launch the counters see is a bench step's; the line then carries no fwd+bwd or per-kernel figures
+    if os.environ.get("GSD_BENCH_STEP_ONLY") == "1":
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": round(world * args.steps / elapsed, 3), "unit": "views/s",
+                              "n_gpus": world, "steps": args.steps, "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+                              "step_only": True}), flush=True)
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    # the drop-in API's step (render + training_loss + step_in_backward + add_densification_stats, what a user of
+    # the reference's interface runs) over the same number of steps, for comparison with the one-call step above
+    dropin = None
+    if fused_step is not None:
+        restore()
+        for _ in range(3):
+            dropin_step()
+        restore()
+        torch.cuda.synchronize()
+        if no_gc:
+            gc.disable()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            dropin_step()
+        torch.cuda.synchronize()
+        dropin_s = time.perf_counter() - t1
+        if no_gc:
+            gc.enable()
+        dropin = {"ms_per_step": round(1000.0 * dropin_s / args.steps, 4),
+                  "views_per_s": round(args.steps / dropin_s, 3)}
     restore()
     # fwd+bwd ms/view: render + loss + backward of one view (no optimizer / collective),
     # hipEvents on the current stream, median over >= 100 views, two ways:
@@ -557,17 +606,6 @@ def main():
         ts.sort()
         return ts[len(ts) // 2]
 
-    # GSD_BENCH_STEP_ONLY=1 (profiling: rocprofv3 --pmc over this script): only the warmup and the timed steps, so
-    # every launch the counters see is a bench step's; the line then carries no fwd+bwd or per-kernel figures
-    if os.environ.get("GSD_BENCH_STEP_ONLY") == "1":
-        if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": round(world * args.steps / elapsed, 3), "unit": "views/s",
-                              "n_gpus": world, "steps": args.steps, "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
-                              "step_only": True}), flush=True)
-        if dist.is_initialized():
-            dist.barrier()
-            dist.destroy_process_group()
-        return
     fwd_bwd_ms = fwd_bwd(True)
     fwd_bwd_synced_ms = fwd_bwd(False)
 
@@ -677,6 +715,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        res["step_path"] = "gsd_train_step (one native call)" if fused_step is not None else "drop-in API"
+        if dropin is not None:
+            res["dropin_api_step"] = dropin
         if exchange is not None:
             res["exchange"] = exchange
         if replicas is not None:

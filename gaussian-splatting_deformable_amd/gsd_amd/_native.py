@@ -12,7 +12,7 @@ import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GSD_HIP_LIB", os.path.join(_PKG_ROOT, "build", "libgsd_hip.so"))
-ABI_VERSION = 16
+ABI_VERSION = 17
 CSRC_DIR = os.path.join(_PKG_ROOT, "csrc")
 
 _vp = ctypes.c_void_p
@@ -63,6 +63,18 @@ class RasterArgs(ctypes.Structure):
     ]
 
 
+class TrainStepArgs(ctypes.Structure):
+    """Mirror of ``gsd_train_step_args`` (include/gsd_raster.h, ABI 17)."""
+
+    _fields_ = [
+        ("raster", RasterArgs), ("geom_buffer", _vp), ("image_buffer", _vp), ("binning_buffer", _vp),
+        ("binning_bytes", _sz), ("radii", _vp), ("out_color", _vp), ("gt", _vp), ("lambda_dssim", _f32),
+        ("loss_out3", _vp), ("loss_workspace", _vp), ("dL_dimg", _vp), ("grad_seed", _vp), ("dL_dmeans2D", _vp),
+        ("dL_dcolors", _vp), ("scratch", _vp), ("grad_accum", _vp), ("grad_accum_3vec", _vp), ("denom", _vp),
+        ("max_radii2D", _vp),
+    ]
+
+
 # name -> (restype, argtypes); every symbol include/gsd_raster.h declares
 SIGNATURES = {
     "gsd_abi_version": (_i32, []),
@@ -100,6 +112,7 @@ SIGNATURES = {
                                 ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32, _vp,
                                 _i64, _i64, _vp]),
     "gsd_densify_stats": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsd_train_step": (_i32, [ctypes.POINTER(TrainStepArgs), ctypes.POINTER(_i64), _vp]),
     "gsd_knn_workspace_bytes": (_sz, [_i32]),
     "gsd_knn_mean_dist2": (_i32, [_i32, _vp, _vp, _vp, _vp]),
     "gsd_deform_mlp_fragments": (_i32, []),

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GSD_ABI_VERSION 16
+#define GSD_ABI_VERSION 17
 
 enum {
     GSD_OK = 0,
@@ -336,6 +336,45 @@ int gsd_adam_step_ex(int64_t n, float* param, float* grad, float* exp_avg, float
                      const int64_t* group_begin, const float* group_lr, const int64_t* group_step, double beta1,
                      double beta2, double eps, int32_t zero_grad, const float* addend, int64_t addend_begin,
                      int64_t addend_end, void* stream);
+
+/* One training step of the reference's loop for one view, as ONE call (ABI 17; no reference counterpart -- the
+ * reference's step is train.py:138-683's Python sequence render() -> loss -> backward() -> optimizer.step() ->
+ * add_densification_stats, each a pybind / autograd hop):
+ *   gsd_rasterize_forward(raster)                       (both phases, one num_rendered read-back)
+ *   gsd_l1_ssim + gsd_l1_ssim_backward                  (0.8 L1 + 0.2 (1 - SSIM), train.py:529; d loss / d image
+ *                                                        scaled by *grad_seed, NULL = 1)
+ *   gsd_rasterize_backward(raster)                      (raster.adam: the Adam step fused where it applies;
+ *                                                        dL/dmeans2D and dL/dcolors written, the parameter
+ *                                                        gradients to raster.activation / raster.sh_split sinks)
+ *   gsd_densify_stats                                   (skipped when grad_accum is NULL)
+ * -- the same kernels with the same arguments as the per-op calls, so the same results.  The raster args serve
+ * both passes (the forward ignores the backward-only fields: sinks, adam).  GSD_NEED_BINNING: binning_bytes was
+ * short -- phase 1 ran, *num_rendered is set, nothing else was done and no state was modified (the caller grows
+ * the buffer to gsd_binning_buffer_bytes(*num_rendered) and calls again).  raster.grad_scratch must equal
+ * scratch (the forward zeroes it for the backward). */
+typedef struct gsd_train_step_args {
+    gsd_raster_args raster;
+    void* geom_buffer;          /* gsd_geom_buffer_bytes(P, W, H) */
+    void* image_buffer;         /* gsd_image_buffer_bytes(W, H) */
+    void* binning_buffer;       /* binning_bytes */
+    size_t binning_bytes;
+    int32_t* radii;             /* (P) out */
+    float* out_color;           /* (3,H,W) out: the rendered image */
+    const float* gt;            /* (3,H,W) the view's ground truth */
+    float lambda_dssim;
+    float* loss_out3;           /* (3) device out: {loss, L1, SSIM} */
+    void* loss_workspace;       /* gsd_l1_ssim_workspace_bytes(3, H, W) */
+    float* dL_dimg;             /* (3,H,W) device scratch: d loss / d image */
+    const float* grad_seed;     /* one device float (autograd's seed gradient), or NULL = 1 */
+    float* dL_dmeans2D;         /* (P,3) out: the viewspace_points gradient */
+    float* dL_dcolors;          /* (P,3) out */
+    void* scratch;              /* gsd_backward_scratch_bytes(P) */
+    float* grad_accum;          /* densification statistics (gsd_densify_stats), or NULL: skipped */
+    float* grad_accum_3vec;
+    float* denom;
+    float* max_radii2D;
+} gsd_train_step_args;
+int gsd_train_step(const gsd_train_step_args* args, int64_t* num_rendered, void* stream);
 
 /* Per-view densification statistics (train.py:613-616, scene/gaussian_model.py:1252-1257): for every
  * Gaussian with radii > 0, max_radii2D = max(max_radii2D, radii); grad_accum_3vec += viewspace_grad;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 6: the one-call training step (gsd_train_step / FusedTrainStep): equality with the drop-in step, then the
+# bench lines of configurations 2, 4 and 5 with it (each line also times the drop-in API step).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; export TMPDIR=/tmp
+OUT=${OUT:-r6f}; O="gpurun_out/$OUT"; mkdir -p "$O"
+timeout -k 10 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+    tests/test_gpu_train.py -k "fused_train_step" > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+tail -4 "$O/tests.log"
+for c in 2 4 5; do
+  timeout -k 10 400 python bench.py --config $c --steps 100 --warmup 10 --cpu-baseline off > "$O/bench_cfg$c.log" 2>&1 \
+      || { tail -20 "$O/bench_cfg$c.log"; exit 1; }
+  grep '^{"metric"' "$O/bench_cfg$c.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('cfg$c', d['value'], d['ms_per_step'], d.get('step_path'), d.get('dropin_api_step'), round(sum(d['kernels_ms'].values()),4))"
+done
+echo all-done

@@ -736,3 +736,75 @@ def test_densify_and_prune_matches_reference_gaussian_model_fixture(monkeypatch)
 
     _densify_fixture_run(golden("densify.npz"), make, step, stats, densify, lambda m: m.dens.reset_opacity(),
                          snapshot, dict(param=1e-5, m=1e-6, v=1e-9, stat=1e-6))
+
+
+def _train_run(fused_step, steps=4, P=30_000, W=320, H=240, densify_at=None):
+    """`steps` training steps (render + 0.8 L1 + 0.2 (1 - SSIM) + backward + Adam + densification statistics) of
+    one view through the drop-in API (render, training_loss, FusedAdam.step_in_backward, GaussianDensifier) or
+    through FusedTrainStep -> parameters, moments, statistics, the last image and loss."""
+    from bench import make_optimizer
+    from gsd_amd import DeformableGaussians, default_pipe, render, training_loss
+    from gsd_amd.camera import synthetic_camera
+    from gsd_amd.densify import GaussianDensifier
+    from gsd_amd.scene import make_gaussians
+    from gsd_amd.train_step import FusedTrainStep
+    pc = DeformableGaussians(make_gaussians(P, W, H, seed=9).to(DEV), sh_degree=3)
+    cam = synthetic_camera(W, H).to(DEV)
+    bg = torch.zeros(3, device=DEV)
+    gt = torch.rand(3, H, W, generator=torch.Generator().manual_seed(4)).to(DEV)
+    opt = make_optimizer(pc)
+    dens = GaussianDensifier(pc, opt)
+    seed = torch.ones((), device=DEV)
+    fs = FusedTrainStep(pc, opt, cam, gt, bg, 0.2, densifier=dens) if fused_step else None
+    img = loss = None
+    for i in range(steps):
+        if fs is not None:
+            out = fs()
+            img, loss = out["render"].clone(), fs.loss()
+        else:
+            out = render(cam, pc, default_pipe(), bg)
+            lo = training_loss(out["render"], gt, out["means3D_offset"], 0.2)
+            with opt.step_in_backward():
+                lo.backward(seed)
+            dens.add_densification_stats(out["viewspace_points"], out["radii"])
+            img, loss = out["render"].detach().clone(), float(lo)
+        if densify_at is not None and i == densify_at:
+            dens.densify_and_prune(0.0002, 0.005, 10.0, None)
+    stats = [dens.xyz_gradient_accum, dens.xyz_gradient_accum_3vec, dens.denom, dens.max_radii2D]
+    return ([p.detach().clone() for p in opt._params], [opt.exp_avg.clone(), opt.exp_avg_sq.clone()],
+            [s.clone() for s in stats], list(opt.steps), img, loss)
+
+
+@pytest.mark.parametrize("densify_at", [None, 1])
+def test_fused_train_step_equals_dropin_step(densify_at):
+    """FusedTrainStep (one gsd_train_step call per step) against the drop-in API's step: the same parameters,
+    Adam moments, step counts and densification statistics after several steps (the float-atomic order of the
+    rasterizer's gradient sums is all that differs, rel L2 1e-5), the same image and loss on the last step; with
+    a densify_and_prune in between (new slabs: the fused step rebuilds its structures)."""
+    a = _train_run(True, densify_at=densify_at)
+    b = _train_run(False, densify_at=densify_at)
+    assert a[3] == b[3]
+    for x, y in zip(a[0] + a[1] + a[2], b[0] + b[1] + b[2]):
+        assert x.shape == y.shape
+        assert rel_l2(x, y) <= 1e-5, rel_l2(x, y)
+    assert float((a[4] - b[4]).abs().max()) <= 1e-5
+    assert abs(a[5] - b[5]) <= 1e-6 * max(1.0, abs(b[5]))
+
+
+def test_fused_train_step_grows_its_binning_buffer():
+    """A short binning buffer (a guess of 1 instance) is grown and the step redone without a state change: the
+    result equals the drop-in path's."""
+    from gsd_amd import train_step
+    orig = train_step.FusedTrainStep._build
+
+    def tiny(self):
+        self._k_guess = 1
+        orig(self)
+    train_step.FusedTrainStep._build = tiny
+    try:
+        a = _train_run(True, steps=2)
+    finally:
+        train_step.FusedTrainStep._build = orig
+    b = _train_run(False, steps=2)
+    for x, y in zip(a[0] + a[1], b[0] + b[1]):
+        assert rel_l2(x, y) <= 1e-5
