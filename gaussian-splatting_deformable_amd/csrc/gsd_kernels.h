@@ -151,6 +151,9 @@ struct PreprocessBwdParams {
     float* dL_drotations;
     int adam_on;           // fused Adam epilogue (any of its sinks set)
     AdamEpiDev adam;
+    // the view's densification statistics (gsd_densify_stats, train.py:613-616) folded into the geometry half,
+    // which holds dL/dmean2D and radii in registers; NULL: not here (gsd_train_step sets them)
+    float *dens_accum, *dens_accum3, *dens_denom, *dens_max_radii;
 };
 
 struct BinParams {

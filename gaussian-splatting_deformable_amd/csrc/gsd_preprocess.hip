@@ -891,7 +891,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams& p,
     // Every per-Gaussian load is issued up front, before the visibility test: a Gaussian the backward skips
     // (radii == 0, backward.cu:359-360) is computed like the others and its outputs are replaced by the zeros
     // torch::zeros holds -- one latency instead of two, and no divergent branch.
-    const bool vis = p.radii[idx] > 0;
+    const int rad = p.radii[idx];
+    const bool vis = rad > 0;
     const float3 m = make_float3(p.means3D[3 * idx], p.means3D[3 * idx + 1], p.means3D[3 * idx + 2]);
     const float4* rec4 = reinterpret_cast<const float4*>(p.grad_rec + (size_t)idx * kGradRec);
     const float4 r0 = rec4[0], r1 = rec4[1], r2 = rec4[2];
@@ -923,6 +924,15 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdParams& p,
         p.dL_dmean2D[3 * idx] = z(r0.x);
         p.dL_dmean2D[3 * idx + 1] = z(r0.y);
         p.dL_dmean2D[3 * idx + 2] = 0.f;
+    }
+    if (p.dens_accum && vis) {  // gsd_densify_stats for this view, the same float operations (gsd_densify.hip)
+        const float gx = r0.x, gy = r0.y;
+        p.dens_max_radii[idx] = fmaxf(p.dens_max_radii[idx], (float)rad);
+        p.dens_accum3[3 * idx] += gx;
+        p.dens_accum3[3 * idx + 1] += gy;
+        p.dens_accum3[3 * idx + 2] += 0.f;  // dL/dmean2D.z, stored as 0 above
+        p.dens_accum[idx] += sqrtf(gx * gx + gy * gy);
+        p.dens_denom[idx] += 1.0f;
     }
     if (p.dL_dopacity) p.dL_dopacity[idx] = z(r1.y);
     if (p.dL_dcolor) {

@@ -346,7 +346,9 @@ int gsd_adam_step_ex(int64_t n, float* param, float* grad, float* exp_avg, float
  *   gsd_rasterize_backward(raster)                      (raster.adam: the Adam step fused where it applies;
  *                                                        dL/dmeans2D and dL/dcolors written, the parameter
  *                                                        gradients to raster.activation / raster.sh_split sinks)
- *   gsd_densify_stats                                   (skipped when grad_accum is NULL)
+ *   the densification statistics of gsd_densify_stats   (skipped when grad_accum is NULL; folded into the
+ *                                                        backward's per-Gaussian pass, which holds dL/dmean2D and
+ *                                                        radii in registers -- the same float operations)
  * -- the same kernels with the same arguments as the per-op calls, so the same results.  The raster args serve
  * both passes (the forward ignores the backward-only fields: sinks, adam).  GSD_NEED_BINNING: binning_bytes was
  * short -- phase 1 ran, *num_rendered is set, nothing else was done and no state was modified (the caller grows

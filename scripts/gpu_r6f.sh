@@ -5,11 +5,23 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; export TMPDIR=/tmp
 OUT=${OUT:-r6f}; O="gpurun_out/$OUT"; mkdir -p "$O"
 timeout -k 10 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread \
-    tests/test_gpu_train.py -k "fused_train_step" > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+    tests/test_gpu_train.py tests/test_gpu_mlp.py -k "fused_train_step or se3net or empty_point" > "$O/tests.log" 2>&1 \
+    || { tail -40 "$O/tests.log"; exit 1; }
 tail -4 "$O/tests.log"
 for c in 2 4 5; do
   timeout -k 10 400 python bench.py --config $c --steps 100 --warmup 10 --cpu-baseline off > "$O/bench_cfg$c.log" 2>&1 \
       || { tail -20 "$O/bench_cfg$c.log"; exit 1; }
   grep '^{"metric"' "$O/bench_cfg$c.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('cfg$c', d['value'], d['ms_per_step'], d.get('step_path'), d.get('dropin_api_step'), round(sum(d['kernels_ms'].values()),4))"
 done
+# do the flips and the T deviation collapse under expf?  The five configuration parity tests on the
+# -DGSD_PRECISE_EXP build, their flip report committed
+# (a failing assertion here is a result, not a fault: only a crash or time limit, rc > 1, ends the script)
+GSD_SKIP_BUILD_ID=1 GSD_HIP_LIB=gaussian-splatting_deformable_amd/build_precise/libgsd_hip.so \
+  GSD_PARITY_REPORT="$O/parity_flips_precise_exp.jsonl" timeout -k 10 600 python -u -m pytest -q -p no:cacheprovider \
+  --timeout 300 --timeout-method thread tests/test_gpu_configs.py -k "full_view or chain" > "$O/precise.log" 2>&1
+rc=$?; tail -3 "$O/precise.log"; [ $rc -gt 1 ] && exit $rc
+GSD_PARITY_REPORT="$O/parity_flips_product.jsonl" timeout -k 10 600 python -u -m pytest -x -q -p no:cacheprovider \
+  --timeout 300 --timeout-method thread tests/test_gpu_configs.py -k "full_view or chain" > "$O/product.log" 2>&1 \
+  || { tail -30 "$O/product.log"; exit 1; }
+tail -2 "$O/product.log"
 echo all-done
