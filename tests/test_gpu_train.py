@@ -748,6 +748,7 @@ def _train_run(fused_step, steps=4, P=30_000, W=320, H=240, densify_at=None):
     from gsd_amd.densify import GaussianDensifier
     from gsd_amd.scene import make_gaussians
     from gsd_amd.train_step import FusedTrainStep
+    torch.manual_seed(123)   # densify_and_prune's split samples come from the global generators
     pc = DeformableGaussians(make_gaussians(P, W, H, seed=9).to(DEV), sh_degree=3)
     cam = synthetic_camera(W, H).to(DEV)
     bg = torch.zeros(3, device=DEV)
@@ -767,7 +768,7 @@ def _train_run(fused_step, steps=4, P=30_000, W=320, H=240, densify_at=None):
             with opt.step_in_backward():
                 lo.backward(seed)
             dens.add_densification_stats(out["viewspace_points"], out["radii"])
-            img, loss = out["render"].detach().clone(), float(lo)
+            img, loss = out["render"].detach().clone(), float(lo.detach())
         if densify_at is not None and i == densify_at:
             dens.densify_and_prune(0.0002, 0.005, 10.0, None)
     stats = [dens.xyz_gradient_accum, dens.xyz_gradient_accum_3vec, dens.denom, dens.max_radii2D]
