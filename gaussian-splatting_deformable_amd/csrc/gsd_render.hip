@@ -262,14 +262,28 @@ __device__ __forceinline__ float4 stage_pc(float2 xy, float4 co) {
 // Returns o G = exp(power - t_o) / 255 (alpha before the 0.99 clamp); `keep` is false where power > 0 (skipped)
 // and `over` false where power < t_o (alpha < 1/255) -- the callers fold both into their take / valid masks; a NaN
 // power passes both, as in the reference (alpha = fminf(0.99, NaN) = 0.99).
-__device__ __forceinline__ float record_og(float4 pc, float2 bt, float pxf, float pyf, bool& keep, bool& over) {
+// GSD_REFERENCE_ALPHA (parity experiments only): alpha as the oracle restates forward.cu:343-345 --
+// o * expf(power), skipped when min(0.99, alpha) < 1/255 -- with the opacity `o` the callers then pass; the default
+// build decides power >= t_o and forms exp(power - t_o) / 255 (below).
+#ifdef GSD_REFERENCE_ALPHA
+#define GSD_REF_O(x) (x)
+#else
+#define GSD_REF_O(x) 0.f
+#endif
+__device__ __forceinline__ float record_og(float4 pc, float2 bt, float pxf, float pyf, bool& keep, bool& over,
+                                           float o = 0.f) {
     const float dx = pc.x - pxf;
     const float dy = pc.y - pyf;
     const float power = (pc.z * dx * dx + pc.w * dy * dy) - bt.x * dx * dy;
     const float d = power - bt.y;  // its sign is exact: a float difference is 0 only for equal operands
     keep = !(power > 0.0f);
     over = !(d < 0.0f);
-#ifdef GSD_PRECISE_EXP
+#if defined(GSD_REFERENCE_ALPHA)
+    (void)o;
+    const float og = o * expf(power);
+    over = !(fminf(0.99f, og) < 1.0f / 255.0f);
+    return og;
+#elif defined(GSD_PRECISE_EXP)
     return expf(d) * (1.0f / 255.0f);
 #else
     return __builtin_amdgcn_exp2f(fmaf(d, kLog2e, -kLog2_255));
@@ -356,7 +370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
             s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
             s_bo[tid] = make_float2(q0.w, q2.y);  // b, t_o
-            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, 0.f);
+            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q1.y);  // r, g, b, o (o read by GSD_REFERENCE_ALPHA only)
             s_box[tid] = r->box;
         } else {  // slots past the tile's list: finite zeros (the walk below reads list bytes past a group's end)
             // (zeros built here from an opaque scalar: a float2 zero hoisted out of the round loop was a VGPR pair
@@ -411,7 +425,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 in_m[u] = wave_ballot(j0 + u < mine);
 #endif
                 slot[u] = (int)((w4 >> (8 * u)) & 0xffu);
-                a[u] = fminf(0.99f, record_og(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u]));
+                a[u] = fminf(0.99f, record_og(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u],
+                                              GSD_REF_O(s_rgb[slot[u]].w)));
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
             // One wave-uniform branch per record (skipped when no lane takes it), the lane decisions as selects:
@@ -915,7 +930,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                                                       row_bcast<U>(rpc.w));
                         const float2 bo = make_float2(row_bcast<U>(rbo.x), row_bcast<U>(rbo.y));
                         bool keep, over;
-                        const float OG = record_og(pc, bo, pxf, pyf, keep, over);  // alpha before the 0.99 clamp
+                        const float OG = record_og(pc, bo, pxf, pyf, keep, over,
+                                                   GSD_REF_O(row_bcast<U>(rrgb.w)));  // alpha before the 0.99 clamp
                         // backward.cu:487-488 (list position below the pixel's last contributor; INT_MIN past the
                         // row's list), :490-501
                         const unsigned long long valid_m =
