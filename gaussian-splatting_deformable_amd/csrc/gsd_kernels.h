@@ -191,6 +191,7 @@ struct RenderParams {
     uint32_t k_cap;
     float4* zero_rec;         // optional: the backward's gradient records, zeroed by this launch (n16 float4s)
     long long zero_n16;
+    int ref_alpha;            // gsd_raster_args.alpha_mode (ABI 17): 1 = the reference's alpha expression
 };
 
 struct RenderBwdParams {
@@ -203,6 +204,7 @@ struct RenderBwdParams {
     const uint32_t* n_contrib;
     const float* dL_dpix;
     float* grad_rec;    // (P, kGradRec), zeroed before the launch
+    int ref_alpha;      // as RenderParams.ref_alpha (the forward's mode)
 };
 
 struct ActivateParams {

@@ -262,28 +262,27 @@ __device__ __forceinline__ float4 stage_pc(float2 xy, float4 co) {
 // Returns o G = exp(power - t_o) / 255 (alpha before the 0.99 clamp); `keep` is false where power > 0 (skipped)
 // and `over` false where power < t_o (alpha < 1/255) -- the callers fold both into their take / valid masks; a NaN
 // power passes both, as in the reference (alpha = fminf(0.99, NaN) = 0.99).
-// GSD_REFERENCE_ALPHA (parity experiments only): alpha as the oracle restates forward.cu:343-345 --
-// o * expf(power), skipped when min(0.99, alpha) < 1/255 -- with the opacity `o` the callers then pass; the default
-// build decides power >= t_o and forms exp(power - t_o) / 255 (below).
-#ifdef GSD_REFERENCE_ALPHA
-#define GSD_REF_O(x) (x)
-#else
-#define GSD_REF_O(x) 0.f
-#endif
+// kRef (gsd_raster_args.alpha_mode = GSD_ALPHA_REFERENCE, ABI 17): alpha exactly as forward.cu:343-345 writes it --
+// o * expf(power) (the correctly rounded-ish library exp), skipped when min(0.99, alpha) < 1/255 -- with the
+// record's opacity `o`.  Measured (profiles/round6/parity/): the oracle's decisions and final_T then agree to 1.9e-6
+// relative (1.05e-5 in the default mode) and one flip remains over the five configurations (11 at cfg5 by default,
+// and as many with expf in the default formula: the deviation is the formula's rounding, not the hardware exp);
+// it costs render_fwd +26 % and render_bwd +18 %.
+template <bool kRef = false>
 __device__ __forceinline__ float record_og(float4 pc, float2 bt, float pxf, float pyf, bool& keep, bool& over,
                                            float o = 0.f) {
     const float dx = pc.x - pxf;
     const float dy = pc.y - pyf;
     const float power = (pc.z * dx * dx + pc.w * dy * dy) - bt.x * dx * dy;
-    const float d = power - bt.y;  // its sign is exact: a float difference is 0 only for equal operands
     keep = !(power > 0.0f);
+    if (kRef) {
+        const float og = o * expf(power);
+        over = !(fminf(0.99f, og) < 1.0f / 255.0f);
+        return og;
+    }
+    const float d = power - bt.y;  // its sign is exact: a float difference is 0 only for equal operands
     over = !(d < 0.0f);
-#if defined(GSD_REFERENCE_ALPHA)
-    (void)o;
-    const float og = o * expf(power);
-    over = !(fminf(0.99f, og) < 1.0f / 255.0f);
-    return og;
-#elif defined(GSD_PRECISE_EXP)
+#ifdef GSD_PRECISE_EXP
     return expf(d) * (1.0f / 255.0f);
 #else
     return __builtin_amdgcn_exp2f(fmaf(d, kLog2e, -kLog2_255));
@@ -327,6 +326,7 @@ __device__ __forceinline__ TileGeom tile_geom(int num_tiles, int grid_x, int W, 
     return g;
 }
 
+template <bool kRef>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_fwd(RenderParams p) {
     // staged records (stage_pc); (b, o) at an 8-B stride keeps the LDS at 8 workgroups per CU
     __shared__ float4 s_pc[kTilePix];
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             const float4 q0 = r->q0, q1 = r->q1, q2 = r->q2;
             s_pc[tid] = stage_pc(make_float2(q0.x, q0.y), make_float4(q0.z, q0.w, q1.x, q1.y));
             s_bo[tid] = make_float2(q0.w, q2.y);  // b, t_o
-            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q1.y);  // r, g, b, o (o read by GSD_REFERENCE_ALPHA only)
+            s_rgb[tid] = make_float4(q1.z, q1.w, q2.x, q1.y);  // r, g, b, o (o read by the reference alpha mode)
             s_box[tid] = r->box;
         } else {  // slots past the tile's list: finite zeros (the walk below reads list bytes past a group's end)
             // (zeros built here from an opaque scalar: a float2 zero hoisted out of the round loop was a VGPR pair
@@ -425,8 +425,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
                 in_m[u] = wave_ballot(j0 + u < mine);
 #endif
                 slot[u] = (int)((w4 >> (8 * u)) & 0xffu);
-                a[u] = fminf(0.99f, record_og(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u],
-                                              GSD_REF_O(s_rgb[slot[u]].w)));
+                a[u] = fminf(0.99f, record_og<kRef>(s_pc[slot[u]], s_bo[slot[u]], pxf, pyf, keep[u], over[u],
+                                                    kRef ? s_rgb[slot[u]].w : 0.f));
             }
             // ... then the sequential front-to-back recurrence (forward.cu:325-362)
             // One wave-uniform branch per record (skipped when no lane takes it), the lane decisions as selects:
@@ -800,6 +800,7 @@ constexpr int kGB = 128;
 #ifndef GSD_BWD_GROUPS_WAVES
 #define GSD_BWD_GROUPS_WAVES 5
 #endif
+template <bool kRef>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GROUPS_WAVES))) void k_render_bwd(
     RenderBwdParams p) {
     __shared__ float4 s_pc[kGB];   // stage_pc: mx, my, -a/2, -c/2
@@ -930,8 +931,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
                                                       row_bcast<U>(rpc.w));
                         const float2 bo = make_float2(row_bcast<U>(rbo.x), row_bcast<U>(rbo.y));
                         bool keep, over;
-                        const float OG = record_og(pc, bo, pxf, pyf, keep, over,
-                                                   GSD_REF_O(row_bcast<U>(rrgb.w)));  // alpha before the 0.99 clamp
+                        const float OG = record_og<kRef>(pc, bo, pxf, pyf, keep, over,
+                                                         kRef ? row_bcast<U>(rrgb.w) : 0.f);  // before the 0.99 clamp
                         // backward.cu:487-488 (list position below the pixel's last contributor; INT_MIN past the
                         // row's list), :490-501
                         const unsigned long long valid_m =
@@ -1064,13 +1065,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSD_BWD_GRO
 }
 
 void launch_render_fwd(const RenderParams& p, hipStream_t s) {
-    if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_fwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+    if (p.num_tiles <= 0) return;
+    if (p.ref_alpha)
+        hipLaunchKernelGGL(k_render_fwd<true>, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_render_fwd<false>, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 }
 void launch_render_bwd(const RenderBwdParams& p, hipStream_t s) {
 #ifdef GSD_BWD_QUADRANT
     if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd_quadrant, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 #else
-    if (p.num_tiles > 0) hipLaunchKernelGGL(k_render_bwd, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+    if (p.num_tiles <= 0) return;
+    if (p.ref_alpha)
+        hipLaunchKernelGGL(k_render_bwd<true>, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_render_bwd<false>, dim3(p.num_tiles), dim3(kTilePix), 0, s, p);
 #endif
 }
 

@@ -10,6 +10,7 @@ legacy default stream and the *current* device -- rasterize_points.cu:71).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -153,8 +154,27 @@ class _Args:
             cov3D_precomp=_ptr(self.cov3D).value, viewmatrix=_ptr(self.view).value,
             projmatrix=_ptr(self.proj).value, campos=_ptr(self.campos).value,
             sh_split=None if sh_split is None else ctypes.addressof(sh_split.c),
-            activation=None if activation is None else ctypes.addressof(activation))
+            activation=None if activation is None else ctypes.addressof(activation), alpha_mode=_ALPHA_MODE[0])
         self.activation = activation
+
+
+# gsd_raster_args.alpha_mode (ABI 17): "fast" (the default: alpha >= 1/255 decided as power >= t_o, the value from the
+# hardware exp) or "reference" (forward.cu:343-345 as written, min(0.99, o * expf(power)) < 1/255: the oracle's
+# decisions and final_T to ~2e-6, ~20 % slower compositing).  GSD_ALPHA_MODE=reference selects it at
+# import; a backward must run in its forward's mode.
+_ALPHA_MODES = {"fast": 0, "reference": 1}
+_ALPHA_MODE = [_ALPHA_MODES[os.environ.get("GSD_ALPHA_MODE", "fast")]]
+
+
+def set_alpha_mode(mode: str) -> None:
+    """Select how the compositing kernels evaluate alpha: "fast" or "reference" (see above)."""
+    if mode not in _ALPHA_MODES:
+        raise ValueError(f"alpha mode must be one of {sorted(_ALPHA_MODES)}, got {mode!r}")
+    _ALPHA_MODE[0] = _ALPHA_MODES[mode]
+
+
+def alpha_mode() -> str:
+    return "reference" if _ALPHA_MODE[0] else "fast"
 
 
 _K_GUESS = {}   # device -> last num_rendered

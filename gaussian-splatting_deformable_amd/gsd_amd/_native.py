@@ -60,6 +60,7 @@ class RasterArgs(ctypes.Structure):
         ("background", _vp), ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp),
         ("scales", _vp), ("rotations", _vp), ("cov3D_precomp", _vp), ("viewmatrix", _vp), ("projmatrix", _vp),
         ("campos", _vp), ("sh_split", _vp), ("activation", _vp), ("adam", _vp), ("grad_scratch", _vp),
+        ("alpha_mode", _i32),
     ]
 
 

@@ -24,7 +24,7 @@ import math
 
 import torch
 
-from . import _native
+from . import _C, _native
 from ._C import _dev_mat, _ptr, _stream
 from .parallel import dp_active
 from .renderer import ZeroOffsets
@@ -146,6 +146,7 @@ class FusedTrainStep:
 
     def _camera(self):
         cam, r = self.cam, self.args.raster
+        r.alpha_mode = _C._ALPHA_MODE[0]
         r.tan_fovx = math.tan(cam.FoVx * 0.5)
         r.tan_fovy = math.tan(cam.FoVy * 0.5)
         # held for the call: the contiguous (cached) copies of the camera's matrices
@@ -177,7 +178,6 @@ class FusedTrainStep:
             steps[i] += 1
         opt._bump(i for _, i in self._sinks)   # in-place updates through raw pointers: advance the versions
         self._k_guess = int(K.value)
-        from . import _C
         _C.last_forward.update(P=self.P, W=self.W, H=self.H, num_rendered=self._k_guess)
         return {"render": self.color, "radii": self.radii, "viewspace_grad": self.dmeans2D,
                 "num_rendered": self._k_guess}

@@ -153,7 +153,14 @@ typedef struct gsd_raster_args {
                                    backward's `scratch` argument, that scratch is taken as zeroed by the forward
                                    that was given it and is not cleared again (pass it to ONE backward only);
                                    NULL or any other value: the backward zeroes its scratch itself. */
+    int32_t alpha_mode;         /* ABI 17: GSD_ALPHA_FAST (0, default) decides alpha >= 1/255 as power >= t_o (the
+                                   exact real comparison) and forms alpha = exp(power - t_o) / 255 with the hardware
+                                   exp; GSD_ALPHA_REFERENCE (1) evaluates forward.cu:343-345 as written,
+                                   min(0.99, o * expf(power)) < 1/255 -- the oracle's decisions and final_T to ~2e-6
+                                   (DESIGN.md 4), ~20 % slower compositing.  A backward must use its forward's mode. */
 } gsd_raster_args;
+
+enum { GSD_ALPHA_FAST = 0, GSD_ALPHA_REFERENCE = 1 };
 
 int gsd_abi_version(void);
 const char* gsd_last_error(void);
