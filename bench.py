@@ -89,7 +89,9 @@ def algorithmic_bytes(P, V, K, W, H, C, adam_fused=False):
     npix = W * H
     return {
         "preprocess_fwd": 44 * P + 12 * C * V + 4 * P + 81 * V,   # 64-B render record per visible Gaussian
-        "tile_hist": 4 * P + 8 * V,
+        # + the per-chunk tile histograms (B = 512 chunks x T u32): written by the histogram pass, read and
+        # rewritten as chunk offsets by the column scans (gsd_binning.hip)
+        "tile_hist": 4 * P + 8 * V + 4 * 4 * 512 * T,
         "tile_scan": 16 * T,
         "scatter_keys": 4 * P + 12 * V + 8 * K,
         "tile_sort": 8 * T + 8 * K + 4 * K,

@@ -66,12 +66,18 @@ class FusedTrainStep:
     # ---- structures ----
     def _state_key(self):
         ps = [getattr(self.pc, a) for _, a in _SLOTS]
-        key = tuple(p.data_ptr() for p in ps) + (int(self.pc._xyz.shape[0]), self.opt.exp_avg.data_ptr(),
+        return tuple(p.data_ptr() for p in ps) + (int(self.pc._xyz.shape[0]), self.opt.exp_avg.data_ptr(),
                                                   self.opt.exp_avg_sq.data_ptr())
-        if self.dens is not None:
-            key += (self.dens.xyz_gradient_accum.data_ptr(), self.dens.denom.data_ptr(),
-                    self.dens.max_radii2D.data_ptr())
-        return key
+
+    def _stats(self):
+        """The densifier's statistics buffers (re-read every call: its reset replaces them without a new P)."""
+        a, d = self.args, self.dens
+        if d is None:
+            return
+        if d.xyz_gradient_accum.shape[0] != self.P:
+            raise RuntimeError("FusedTrainStep: the densifier's statistics do not match the Gaussians")
+        a.grad_accum, a.grad_accum_3vec = d.xyz_gradient_accum.data_ptr(), d.xyz_gradient_accum_3vec.data_ptr()
+        a.denom, a.max_radii2D = d.denom.data_ptr(), d.max_radii2D.data_ptr()
 
     def _build(self):
         lib = _native.load()
@@ -123,11 +129,6 @@ class FusedTrainStep:
             grad_seed=self._seed.data_ptr(), dL_dmeans2D=self.dmeans2D.data_ptr(),
             dL_dcolors=self.dcolors.data_ptr(), scratch=self.scratch.data_ptr())
         self.args.binning_buffer, self.args.binning_bytes = self.binning.data_ptr(), self.binning.numel()
-        if self.dens is not None:
-            d = self.dens
-            self.args.grad_accum, self.args.grad_accum_3vec = d.xyz_gradient_accum.data_ptr(), \
-                d.xyz_gradient_accum_3vec.data_ptr()
-            self.args.denom, self.args.max_radii2D = d.denom.data_ptr(), d.max_radii2D.data_ptr()
         r = self.args.raster
         r.P, r.D, r.M, r.width, r.height = P, int(pc.active_sh_degree), 1 + int(ps["rest"].shape[1]), W, H
         r.scale_modifier = self.scaling_modifier
@@ -159,6 +160,7 @@ class FusedTrainStep:
     def __call__(self):
         if self._key != self._state_key():
             self._build()
+        self._stats()
         self._camera()
         opt, lib = self.opt, _native.load()
         steps = opt.steps
