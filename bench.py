@@ -495,17 +495,20 @@ def main():
         opt.flat.invalidate()   # as a fresh optimizer: no gradients yet
 
     gc.collect()   # before the warmup, so the device is busy again when the timed steps start
+    restore_first = os.environ.get("GSD_BENCH_RESTORE_FIRST") == "1"   # diagnostics: no restore after the warmup
     for _ in range(args.warmup):
         step()
     if densify_every:
         # one densification in the warmup as well: PyTorch loads each elementwise kernel's code object on its
         # first launch (~0.1 s over densify_and_prune's ops on a fresh process), a one-time cost, not a step's
         dens.densify_and_prune(0.0002, 0.005, 10.0, None)
-    restore()
+    if not restore_first:
+        restore()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     step_ev = [] if os.environ.get("GSD_BENCH_STEP_TIMES") else None   # diagnostics: per-step device times
+    step_host = []
     # Python's cyclic garbage collector off inside the timed steps (as timeit does): a collection pass stalls the
     # host, which paces the device through the per-step num_rendered read-back (+0.15 ms on one step of every
     # ~10 at 1M Gaussians).  The collection is done before the warmup: a pause of the host here, with the device
@@ -518,9 +521,11 @@ def main():
         if step_ev is not None:
             step_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             step_ev[-1][0].record()
+            th = time.perf_counter()
         out = step()
         if step_ev is not None:
             step_ev[-1][1].record()
+            step_host.append(1000.0 * (time.perf_counter() - th))
         if i == 0:
             K_start = int(gsdC.last_forward.get("num_rendered", 0))  # host value, already read by the forward
     torch.cuda.synchronize()
@@ -528,6 +533,7 @@ def main():
         gc.enable()
     if step_ev is not None and rank == 0:
         print("step ms:", " ".join("%.3f" % a.elapsed_time(b) for a, b in step_ev), file=sys.stderr)
+        print("host ms:", " ".join("%.3f" % h for h in step_host), file=sys.stderr)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

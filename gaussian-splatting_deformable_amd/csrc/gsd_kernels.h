@@ -330,6 +330,10 @@ struct MlpPackParams {
     // layer's accumulators (k_mlp_fwd_fused); natural order below it
     int perm_from;
     int m_off;             // transpose: A row m is W^T row m + m_off (layer 5's h rows for the backward chain)
+    // m16: fragments of v_mfma_f32_16x16x32_bf16 (k_mlp_fwd_fused16): (K / 32) x (M / 16) x 3 x 64 of 16 B, lane l
+    // holding row 16 rb + (l & 15) and columns 32 ks + 8 (l >> 4) + j (natural) or 32 ks + 16 (j >> 2) + 4 (l >> 4) +
+    // (j & 3) (k-steps >= perm_from: the 16 x 16 accumulator order)
+    int m16;
 };
 struct MlpPackBatch {   // up to 12 packs in one launch
     MlpPackParams job[12];
@@ -383,6 +387,9 @@ struct MlpChainParams {
     float* dE;
 };
 void launch_mlp_bwd_chain(const MlpChainParams& p, hipStream_t s);
+// the same chain at two waves per SIMD, 16 Gaussians per wave (k_mlp_bwd_chain16: every W^T packed with m16; reads
+// the ReLU words either forward writes)
+void launch_mlp_bwd_chain16(const MlpChainParams& p, hipStream_t s);
 enum { kMlpFwdRelu = 0, kMlpFwdHeads = 1, kMlpBwdMask = 2 };
 struct MlpGemmParams {
     int P, ldp;                     // Gaussians; row stride of the feature-major matrices (P rounded up to 256)
@@ -426,6 +433,8 @@ void launch_mlp_encode(int P, int ldp, const float* x, const float* t, float* E,
 void launch_mlp_encode_bwd(int P, int ldp, const float* E, const float* dE, float* dx, int accumulate, hipStream_t s);
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s);
 void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s, bool store = true);
+// the same forward at two waves per SIMD, 16 Gaussians per wave (weights packed with m16; the same outputs)
+void launch_mlp_fwd_fused16(const MlpFusedParams& p, hipStream_t s, bool store = true);
 // dW scattered into the reference-shaped weight pieces (dst.W; map/rows as the forward weight), db into dst_b
 void launch_mlp_wgrad(const MlpWgradParams& p, const MlpWeightRef& dst, const MlpWeightRef& dst_b, hipStream_t s);
 void launch_mlp_rows_to_features(int P, int ldp, const MlpHeadsIn& src, float* dst, int dst_rows, hipStream_t s);

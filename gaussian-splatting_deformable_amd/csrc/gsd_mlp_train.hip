@@ -105,15 +105,22 @@ __global__ __launch_bounds__(256) void k_mlp_pack_multi(MlpPackBatch b) {
     if ((int)blockIdx.y < b.n) mlp_pack_one(b.job[blockIdx.y], blockIdx.x * 256 + threadIdx.x);
 }
 __device__ __forceinline__ void mlp_pack_one(const MlpPackParams& p, int t) {
-    const int RB = p.M / 32, KS = p.K / 16;
+    const int RW = p.m16 ? 16 : 32, KW = p.m16 ? 32 : 16;   // fragment rows and k-step depth
+    const int RB = p.M / RW, KS = p.K / KW;
     if (t >= KS * RB * 64) return;
     const int lane = t & 63, rb = (t >> 6) % RB, ks = (t >> 6) / RB;
-    const int m = 32 * rb + (lane & 31);
+    const int m = RW * rb + (lane & (RW - 1));
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int h = lane >> 5;
-        const int k = 16 * ks + (ks >= p.perm_from ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j);
+        int k;
+        if (p.m16) {
+            const int q = lane >> 4;
+            k = 32 * ks + (ks >= p.perm_from ? 16 * (j >> 2) + 4 * q + (j & 3) : 8 * q + j);
+        } else {
+            const int h = lane >> 5;
+            k = 16 * ks + (ks >= p.perm_from ? 8 * (j >> 2) + 4 * h + (j & 3) : 8 * h + j);
+        }
         // forward: A = W, rows m = output features, columns k = (padded) input features; backward: A = W^T
         const float* e = p.transpose ? mlp_elem(p.w, k, mlp_col(p.w.map, m + p.m_off))
                                      : mlp_elem(p.w, m, mlp_col(p.w.map, k));
@@ -770,6 +777,305 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     }
 }
 
+// ---- the layer-fused forward at two waves per SIMD (k_mlp_fwd_fused16) ----
+// k_mlp_fwd_fused holds 32 Gaussians per wave in ~450 registers: one wave per SIMD, so the issue of every weight copy
+// and activation store stalls that wave's MFMA stream (the ablations of DESIGN.md §7: the MFMA work and the copy /
+// store issue add up).  Here a wave holds 16 Gaussians on v_mfma_f32_16x16x32_bf16 -- 16 row blocks of 16 output
+// rows, k-steps of 32 -- in 64 accumulator and 64 activation registers, so the workgroup's eight waves run two per
+// SIMD and one wave's copies, stores and splits issue while the other's MFMAs run.  The weight fragments are read
+// from LDS twice as often per MAC (a 16 x 32 fragment per 16 x 16 output block): 128 B/clk of the array's 256 for
+// ds_read_b128.  The ring: three 48-KB slots (k-step t + 2 copied while t is multiplied), the biases beside it.
+// Operand maps (lane l: q = l >> 4, c = l & 15, the Gaussian):
+//   A fragment: row 16 rb + c, columns 32 ks + kcol(q, j), j = 0..7 (k_mlp_pack m16: natural kcol 8 q + j, or the
+//               accumulator order 16 (j >> 2) + 4 q + (j & 3))
+//   B operand:  element j of k-step ks = input feature 32 ks + kcol(q, j) of Gaussian c
+//   C:          acc[rb][i] = output row 16 rb + 4 q + i
+// so row blocks 2 s and 2 s + 1 of a layer's output are the next layer's k-step s with no lane movement.  The hidden
+// outputs and ReLU words go to HBM in the layouts k_mlp_fwd_fused writes (the backward reads them unchanged).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kF16Step = 16 * 3 * 64;   // bf16x8 per hidden k-step (48 KB)
+constexpr int kF16Slot = 48 * 1024;
+
+template <int M>
+__device__ __forceinline__ f32x4 mfma16_part(const Split8& a, const Split8& b, f32x4 acc) {
+    if constexpr (M == 0) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, acc, 0, 0, 0);
+    if constexpr (M == 1) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.mid, acc, 0, 0, 0);
+    if constexpr (M == 2) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, acc, 0, 0, 0);
+    if constexpr (M == 3) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.hi, acc, 0, 0, 0);
+    if constexpr (M == 4) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.mid, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, acc, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16_x6(const Split8& a, const Split8& b, f32x4 acc) {
+    acc = mfma16_part<0>(a, b, acc);
+    acc = mfma16_part<1>(a, b, acc);
+    acc = mfma16_part<2>(a, b, acc);
+    acc = mfma16_part<3>(a, b, acc);
+    acc = mfma16_part<4>(a, b, acc);
+    return mfma16_part<5>(a, b, acc);
+}
+
+// nontemporal row stores through a buffer descriptor built from wave-uniform values (the base: a k-step's first
+// row), the lane's part a 32-bit offset: no 64-bit address per store held in registers.  v: element (row, g) with
+// `row` rows (uniform) past base and `voff` = (its row within the group) * ldp + g (per lane), in elements.
+__device__ __forceinline__ void store_row_nt(float v, const float* base, unsigned voff, int row_elems) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, -1, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)(4 * voff), 4 * row_elems, 2);
+}
+__device__ __forceinline__ void store_row(float v, const float* base, unsigned voff, int row_elems) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, -1, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)(4 * voff), 4 * row_elems, 0);
+}
+__device__ __forceinline__ float load_row(const float* base, unsigned voff, int row_elems) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, -1, 0x00020000);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4 * voff), 4 * row_elems, 0));
+}
+__device__ __forceinline__ void store_word_nt(unsigned w, const unsigned short* base, unsigned voff) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(base), 0, -1, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w, r, (int)(2 * voff), 0, 2);
+}
+
+// dma16_asm with a wave-uniform base (SGPRs) and the lane's 32-bit byte offset: no 64-bit address per copy in
+// registers (the chunk's offset folds into the base)
+__device__ __forceinline__ void dma16_sa(const void* sbase, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
+                 : "memory");
+}
+
+// global stores a k-step issues, all after its weight copies: 8 activation rows and a ReLU word (the k-steps fed by
+// the layer before); ks < 0: the layer before's last k-step (prev)
+__device__ __forceinline__ constexpr int f16_stores(int kse, int ks, int prev) {
+    return ks < 0 ? prev : (ks < kse ? 0 : 9);
+}
+
+// One hidden layer (KSE encoding k-steps: enc(x) 0-1, then enc(t); then KSA activation k-steps), fully unrolled.  s:
+// the layer's first global k-step (ring slot (s + ks) % 3).  Per k-step: 16 row blocks x 6 MFMAs, and in their gaps
+// the next row block's fragments (LDS), k-step s + ks + 2's six copies per wave (row blocks 0-5), the previous layer's
+// eight output rows this k-step consumes and its ReLU word (row blocks 6-14), the next B operand's split (1-4); then
+// a counted vmcnt (k-step s + ks + 1 landed) and a raw barrier.
+template <int KSE, int KSA, int PREV, bool ST>
+__device__ __forceinline__ void fused16_layer(const MlpFusedParams& p, unsigned char* s_mem, int s, int l, int wave,
+                                              int lane, unsigned voff_dma, unsigned voff_h, unsigned voff_b, bool bit_lane,
+                                              const float (&xe)[2][8], const float (&xt)[8], const float (&act)[8][8],
+                                              const unsigned (&bits)[8], f32x4 (&acc)[16]) {
+    constexpr int KS = KSE + KSA;
+    constexpr int kStepB = kF16Step * 16;   // bytes per k-step
+    const char* fc = reinterpret_cast<const char*>(p.frags[l]);
+    const char* fn = l < 7 ? reinterpret_cast<const char*>(p.frags[l + 1]) : fc + (KS - 1) * kStepB;
+    const int ldp = p.ldp;
+    float* Hp = KSA ? p.H[l - 1] : nullptr;
+    unsigned short* Bp = KSA ? p.bits[l - 1] : nullptr;
+    const int s3 = s % 3;
+    const unsigned base = lds_addr(s_mem);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = f32x4{};
+    auto operand = [&](int ks) -> const float(&)[8] {
+        if (ks < KSE) return ks < 2 ? xe[ks < 2 ? ks : 0] : xt;
+        return act[ks >= KSE ? ks - KSE : 0];
+    };
+    auto slot = [&](int k) -> unsigned {   // k: a compile-time offset from s
+        int t = s3 + k % 3;
+        t = t >= 3 ? t - 3 : t;
+        return (unsigned)t * kF16Slot;
+    };
+    Split8 b = split8(operand(0));
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int kk = ks + 2;
+        const char* f = kk < KS ? fc + kk * kStepB : (l < 7 ? fn + (kk - KS) * kStepB : fn);
+        const unsigned dst = base + slot(kk);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + slot(ks));
+        const int k2 = ks >= KSE ? ks - KSE : 0;
+        const bool stores = ST && ks >= KSE;
+        Split8 bn = b;
+        Split8 a;
+        a.hi = sa[lane];
+        a.mid = sa[64 + lane];
+        a.lo = sa[128 + lane];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            Split8 an = a;
+            if (r + 1 < 16) {
+                an.hi = sa[((r + 1) * 3) * 64 + lane];
+                an.mid = sa[((r + 1) * 3 + 1) * 64 + lane];
+                an.lo = sa[((r + 1) * 3 + 2) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<0>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<1>(a, b, acc[r]);
+            if (r < 6)   // chunk wave + 8 r: bytes 8192 r + 16 tid of the k-step
+                dma16_sa(f + 8192 * r, voff_dma, __builtin_amdgcn_readfirstlane(dst + (wave + 8 * r) * 1024));
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<2>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<3>(a, b, acc[r]);
+            if (stores && r >= 6 && r < 14) {
+                const int e = r - 6;   // act[k2][e]: row 32 k2 + 16 (e >> 2) + 4 q + (e & 3)
+                store_row_nt(act[k2][e < 8 ? e : 0], Hp + (size_t)(32 * k2) * ldp, voff_h,
+                             (16 * (e >> 2) + (e & 3)) * ldp);
+            }
+            if (stores && r == 14 && bit_lane) store_word_nt(bits[k2], Bp + (size_t)(2 * k2) * ldp, voff_b);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<4>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<5>(a, b, acc[r]);
+            if (r >= 1 && r <= 4 && ks + 1 < KS) split_pair(operand(ks + 1 < KS ? ks + 1 : 0), r - 1, bn);
+            __builtin_amdgcn_sched_barrier(0);
+            a = an;
+        }
+        b = bn;
+        wait_vm_u(f16_stores(KSE, ks - 1, PREV) + 6 + f16_stores(KSE, ks, PREV));
+        raw_barrier();
+    }
+}
+
+// bias (LDS) + ReLU into the next layer's B operand (k-step rb32 = row blocks 2 rb32, 2 rb32 + 1) and the ReLU words
+// in k_mlp_fwd_fused's layout (word 2 rb32 + h, bit 4 q4 + i = row 32 rb32 + 8 q4 + 4 h + i): lane (q, c) holds
+// half of word 2 rb32 + (q & 1), lane (q ^ 2, c) the other half
+__device__ __forceinline__ void fused16_epilogue(const float* s_bias, int q, const f32x4 (&acc)[16],
+                                                 float (&act)[8][8], unsigned (&bits)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        unsigned w = 0;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const float4 b4 = *reinterpret_cast<const float4*>(s_bias + 16 * (2 * k + a) + 4 * q);
+            const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float y = relu_nan(acc[2 * k + a][i] + bq[i]);
+                act[k][4 * a + i] = y;
+                w |= (!(y <= 0.f) ? 1u : 0u) << (8 * a + i);
+            }
+        }
+        w <<= 4 * (q >> 1);
+        bits[k] = w | (unsigned)__shfl_xor((int)w, 32);
+    }
+}
+
+template <bool kStore>
+__global__ __launch_bounds__(512) void k_mlp_fwd_fused16(MlpFusedParams p) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[3 * kF16Slot];
+    __shared__ __attribute__((aligned(16))) float s_bias[8 * 256 + 64];
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, c = lane & 15, wave = tid >> 6;
+    const int g = blockIdx.x * 128 + wave * 16 + c;   // < ldp (the grid covers ldp / 128 workgroups)
+    const int ldp = p.ldp;
+    const unsigned voff_h = (unsigned)(4 * q) * (unsigned)ldp + (unsigned)g;      // row 4 q of a layer's output
+    const unsigned voff_b = (unsigned)(q & 1) * (unsigned)ldp + (unsigned)g;      // ReLU word of half q & 1
+    const bool bit_lane = q < 2;
+    const unsigned voff_dma = 16u * (unsigned)tid;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_bias[512 * i + tid] = p.bias[(512 * i + tid) >> 8][(512 * i + tid) & 255];
+    if (tid < 64) s_bias[2048 + tid] = p.bias_heads[tid];
+    float xe[2][8], xt[8];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xe[ks][j] = p.E[(size_t)(32 * ks + 8 * q + j) * ldp + g];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xt[j] = p.ET[(size_t)(8 * q + j) * ldp + g];
+    __builtin_amdgcn_s_waitcnt(0xf70);   // plain loads done before the first copy (as k_mlp_fwd_fused)
+    __syncthreads();
+    {
+        const char* f0 = reinterpret_cast<const char*>(p.frags[0]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                dma16_sa(f0 + k * (kF16Step * 16) + 8192 * i, voff_dma,
+                         __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + k * kF16Slot + (wave + 8 * i) * 1024));
+    }
+    wait_vm_c<6>();
+    raw_barrier();
+    float act[8][8];
+    unsigned bits[8];
+    f32x4 acc[16];
+    constexpr int PV = kStore ? 9 : 0;
+    fused16_layer<3, 0, 0, kStore>(p, s_mem, 0, 0, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt, act, bits, acc);
+    fused16_epilogue(s_bias, q, acc, act, bits);
+    fused16_layer<0, 8, 0, kStore>(p, s_mem, 3, 1, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt, act, bits, acc);
+    fused16_epilogue(s_bias + 256, q, acc, act, bits);
+#pragma unroll 1
+    for (int l = 2; l <= 4; ++l) {
+        fused16_layer<0, 8, PV, kStore>(p, s_mem, 3 + 8 * (l - 1), l, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt,
+                                        act, bits, acc);
+        fused16_epilogue(s_bias + 256 * l, q, acc, act, bits);
+    }
+    fused16_layer<2, 8, PV, kStore>(p, s_mem, 35, 5, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt, act, bits, acc);
+    fused16_epilogue(s_bias + 256 * 5, q, acc, act, bits);
+#pragma unroll 1
+    for (int l = 6; l <= 7; ++l) {
+        fused16_layer<0, 8, PV, kStore>(p, s_mem, 45 + 8 * (l - 6), l, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt,
+                                        act, bits, acc);
+        fused16_epilogue(s_bias + 256 * l, q, acc, act, bits);
+    }
+    // the heads (58 outputs, four row blocks of 16, eight k-steps): their own ring of four 16-KB slots over the same
+    // LDS, 12 chunks per k-step (two copies per wave; waves 4-7 re-copy chunk 0 into the slot's padding); layer 7's
+    // output and ReLU words ride under their MFMAs
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    const char* fh = reinterpret_cast<const char*>(p.frags[8]);
+    // chunk wave: bytes 16 tid of the k-step; chunk wave + 8: 8192 + 16 tid for waves 0-3, chunk 0 (16 lane) again
+    // for waves 4-7
+    const unsigned voff_h2 = wave < 4 ? 8192u + voff_dma : 16u * (unsigned)lane;
+#define GSD_H16_ISSUE(KS)                                                                                      \
+    do {                                                                                                       \
+        const char* f_ = fh + min((KS), 7) * (4 * 3 * 64 * 16);                                                \
+        dma16_sa(f_, voff_dma, __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (16 * 1024) + wave * 1024)); \
+        dma16_sa(f_, voff_h2,                                                                                  \
+                 __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (16 * 1024) + (wave + 8) * 1024)); \
+    } while (0)
+    f32x4 ho[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
+    GSD_H16_ISSUE(0);
+    GSD_H16_ISSUE(1);
+    GSD_H16_ISSUE(2);
+    wait_vm_c<4>();
+    raw_barrier();
+    float* H7 = p.H[7];
+    unsigned short* B7 = p.bits[7];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        GSD_H16_ISSUE(ks + 3);
+        const Split8 b = split8(act[ks]);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (16 * 1024));
+        if constexpr (kStore) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                store_row_nt(act[ks][e], H7 + (size_t)(32 * ks) * ldp, voff_h, (16 * (e >> 2) + (e & 3)) * ldp);
+            if (bit_lane) store_word_nt(bits[ks], B7 + (size_t)(2 * ks) * ldp, voff_b);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            Split8 a;
+            a.hi = sa[(r * 3) * 64 + lane];
+            a.mid = sa[(r * 3 + 1) * 64 + lane];
+            a.lo = sa[(r * 3 + 2) * 64 + lane];
+            ho[r] = mfma16_x6(a, b, ho[r]);
+        }
+        wait_vm_u(4 + f16_stores(0, ks - 2, 0) * kStore + f16_stores(0, ks - 1, 0) * kStore +
+                  f16_stores(0, ks, 0) * kStore);
+        raw_barrier();
+    }
+#undef GSD_H16_ISSUE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's re-copies: nothing left in flight at exit
+    if (g < p.P) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float4 b4 = *reinterpret_cast<const float4*>(s_bias + 2048 + 16 * r + 4 * q);
+            const float bq[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int n = 16 * r + 4 * q + i;
+                if (n < 58) mlp_store_head(p.heads, g, n, ho[r][i] + bq[i]);
+            }
+        }
+    }
+}
+
 // ---- the backward's dX chain fused across the layers ----
 // g_{l-1} = (W_l^T g_l) masked by the forward's ReLU words of h_l, from the heads' gradient g8 down to g0, in one
 // kernel the way k_mlp_fwd_fused runs the forward: a wave keeps its 32 Gaussians' gradient in registers, layer l's
@@ -1043,6 +1349,258 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 #pragma unroll
         for (int q = 0; q < 16; ++q)
             p.dE[(size_t)(32 * r + 8 * (q >> 2) + 4 * h + (q & 3)) * ldp + g] = ho[r][q];
+}
+
+// ---- the dX chain at two waves per SIMD (k_mlp_bwd_chain16) ----
+// k_mlp_bwd_chain's structure on k_mlp_fwd_fused16's operand maps: eight waves of 16 Gaussians, v_mfma_f32_16x16x32,
+// the packed W^T k-steps (48 KB) through a three-slot ring two k-steps ahead.  Per step the next step's ReLU words
+// (the eight 16-bit words of the lane's half, 16 B) are loaded at its first k-step, ahead of the copies, so the
+// counted waits retire them a k-step later; the mask (k_mlp_fwd_fused16's word layout read back) is applied from
+// registers.  The two 64-row passes on W^T's enc(x) rows (layer 5's, times g5 before step 3, and layer 0's, times g0
+// at the end) run on a ring of their own over the drained main ring (four 16-KB slots, three ahead); the main ring
+// restarts after the first.  Every step's input goes to G[i] under its MFMAs, as in k_mlp_bwd_chain.
+
+// a 4-B LDS-DMA per lane (one 256-B row segment per wave): the ReLU words of the workgroup's 128 Gaussians
+__device__ __forceinline__ void dma4_sa(const void* sbase, unsigned voff, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds)
+                 : "memory");
+}
+// the sixteen ReLU-word rows of a step for the workgroup's Gaussians into s_w ([16][128] u16): wave w copies rows
+// 2 w, 2 w + 1 (two DMAs per wave, counted by the caller's waits)
+__device__ __forceinline__ void chain16_words(const unsigned short* bits, int ldp, int wave, unsigned voff_w2,
+                                              unsigned s_w) {
+    const int w = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        dma4_sa(bits + (size_t)(2 * w + j) * ldp, voff_w2, __builtin_amdgcn_readfirstlane(s_w + (2 * w + j) * 256));
+}
+
+// one step: KS k-steps of B = act (NAT: natural rows 32 ks + 8 q + j; else the accumulator order), the rows stored to
+// Gp under the MFMAs; s: the step's first k-step in the ring phase (slot s % 3); LAST: the ring is fed re-copies of
+// this step's own last k-step (no next step in this ring phase); MASKLD: the next step's ReLU words are loaded into
+// wn at k-step 0; PREV: stores of the k-step before (0 at a ring phase's start).
+template <int KS, bool NAT, bool LAST, bool MASKLD, int PREV>
+__device__ __forceinline__ void chain16_step(const char* fc, const char* fn, float* __restrict__ Gp, int ldp,
+                                             unsigned char* s_mem, int s, int wave, int lane, unsigned voff_dma,
+                                             unsigned voff_st, const unsigned short* bits_next, unsigned voff_w2,
+                                             unsigned s_wn, const float (&act)[8][8], f32x4 (&acc)[16]) {
+    constexpr int kStepB = kF16Step * 16;
+    const int s3 = s % 3;
+    const unsigned base = lds_addr(s_mem);
+    auto slot = [&](int k) -> unsigned {
+        int t = s3 + k % 3;
+        t = t >= 3 ? t - 3 : t;
+        return (unsigned)t * kF16Slot;
+    };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = f32x4{};
+    Split8 b = split8(act[0]);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int kk = ks + 2;
+        const char* f = kk < KS ? fc + kk * kStepB : (LAST ? fc + (KS - 1) * kStepB : fn + (kk - KS) * kStepB);
+        const unsigned dst = base + slot(kk);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + slot(ks));
+        if (MASKLD && ks == 0) chain16_words(bits_next, ldp, wave, voff_w2, s_wn);
+        Split8 bn = b;
+        Split8 a;
+        a.hi = sa[lane];
+        a.mid = sa[64 + lane];
+        a.lo = sa[128 + lane];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            Split8 an = a;
+            if (r + 1 < 16) {
+                an.hi = sa[((r + 1) * 3) * 64 + lane];
+                an.mid = sa[((r + 1) * 3 + 1) * 64 + lane];
+                an.lo = sa[((r + 1) * 3 + 2) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<0>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<1>(a, b, acc[r]);
+            if (r < 6) dma16_sa(f + 8192 * r, voff_dma, __builtin_amdgcn_readfirstlane(dst + (wave + 8 * r) * 1024));
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<2>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<3>(a, b, acc[r]);
+            if (r >= 6 && r < 14) {
+                const int e = r - 6;
+                store_row_nt(act[ks][e < 8 ? e : 0], Gp + (size_t)(32 * ks) * ldp, voff_st,
+                             (NAT ? e : 16 * (e >> 2) + (e & 3)) * ldp);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<4>(a, b, acc[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc[r] = mfma16_part<5>(a, b, acc[r]);
+            if (r >= 1 && r <= 4 && ks + 1 < KS) split_pair(act[ks + 1 < KS ? ks + 1 : 0], r - 1, bn);
+            __builtin_amdgcn_sched_barrier(0);
+            a = an;
+        }
+        b = bn;
+        // k-step ks + 1's copies (issued at k-step ks - 1, or before the phase) landed: all but the younger ops
+        wait_vm_u((ks == 0 ? PREV : 8) + (MASKLD && ks == 0 ? 2 : 0) + 6 + 8);
+        raw_barrier();
+    }
+}
+
+// threshold_backward by the forward's ReLU words (fused16_epilogue's layout) from s_w: word 2 k + (q & 1) of the
+// lane's Gaussian gl (0-127 in the workgroup)
+__device__ __forceinline__ void chain16_mask(const unsigned short* s_w, int gl, int q, const f32x4 (&acc)[16],
+                                             float (&act)[8][8]) {
+    int idx = (q & 1) * 128 + gl;
+    asm volatile("" : "+v"(idx));   // formed here, not hoisted to the kernel's start and held (or spilled) till now
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const unsigned wk = (unsigned)s_w[idx + 256 * k] >> (4 * (q >> 1));
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) act[k][4 * a + i] = (wk >> (8 * a + i)) & 1u ? acc[2 * k + a][i] : 0.f;
+    }
+}
+
+// a 64-row pass (four row blocks of 16, K = 256) of W^T's enc(x) rows times act, on a four-slot ring over the drained
+// main ring: ho += A act.  Gp: act's rows stored under it (the final step's g0), or null.
+template <bool STORE>
+__device__ __forceinline__ void chain16_enc_pass(const char* fe, unsigned char* s_mem, int wave, int lane,
+                                                 unsigned voff_dma, float* __restrict__ Gp, int ldp, unsigned voff_st,
+                                                 const float (&act)[8][8], f32x4 (&ho)[4]) {
+    const unsigned voff_2 = wave < 4 ? 8192u + voff_dma : 16u * (unsigned)lane;   // waves 4-7 re-copy chunk 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+#define GSD_E16_ISSUE(KS)                                                                                      \
+    do {                                                                                                       \
+        const char* f_ = fe + min((KS), 7) * (4 * 3 * 64 * 16);                                                \
+        dma16_sa(f_, voff_dma, __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (16 * 1024) + wave * 1024)); \
+        dma16_sa(f_, voff_2,                                                                                   \
+                 __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + ((KS) & 3) * (16 * 1024) + (wave + 8) * 1024)); \
+    } while (0)
+    GSD_E16_ISSUE(0);
+    GSD_E16_ISSUE(1);
+    GSD_E16_ISSUE(2);
+    wait_vm_c<4>();
+    raw_barrier();
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        GSD_E16_ISSUE(ks + 3);
+        const Split8 b = split8(act[ks]);
+        const bf16x8* sa = reinterpret_cast<const bf16x8*>(s_mem + (ks & 3) * (16 * 1024));
+        if constexpr (STORE) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                store_row_nt(act[ks][e], Gp + (size_t)(32 * ks) * ldp, voff_st, (16 * (e >> 2) + (e & 3)) * ldp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            Split8 a;
+            a.hi = sa[(r * 3) * 64 + lane];
+            a.mid = sa[(r * 3 + 1) * 64 + lane];
+            a.lo = sa[(r * 3 + 2) * 64 + lane];
+            ho[r] = mfma16_x6(a, b, ho[r]);
+        }
+        // k-step ks + 1 (issued at k-step ks - 2, or before the loop) landed
+        wait_vm_u(4 + (STORE ? (ks >= 2 ? 8 : 0) + (ks >= 1 ? 8 : 0) + 8 : 0));
+        raw_barrier();
+    }
+#undef GSD_E16_ISSUE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's re-copies: nothing in flight past the pass
+    raw_barrier();
+}
+
+__global__ __launch_bounds__(512) void k_mlp_bwd_chain16(MlpChainParams p) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_mem[3 * kF16Slot];
+    // the ReLU words of three steps ([16][128] u16 each): step i's are read at its end from buffer i % 3 while step
+    // i + 1's land in (i + 1) % 3 and step i + 2's are issued into (i + 2) % 3 by waves already past step i
+    __shared__ __attribute__((aligned(16))) unsigned short s_w[3][16 * 128];
+    const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, c = lane & 15, wave = tid >> 6;
+    const int gl = wave * 16 + c, g = blockIdx.x * 128 + gl;   // < ldp (the grid covers ldp / 128 workgroups)
+    const int ldp = p.ldp;
+    const unsigned voff_dma = 16u * (unsigned)tid;
+    const unsigned voff_n = (unsigned)(8 * q) * (unsigned)ldp + (unsigned)g;    // natural order: row 8 q
+    const unsigned voff_a = (unsigned)(4 * q) * (unsigned)ldp + (unsigned)g;    // accumulator order: row 4 q
+    const unsigned voff_w2 = 2u * (unsigned)(blockIdx.x * 128 + 2 * lane);     // words of Gaussians 2 lane, + 1
+    const unsigned sw0 = lds_addr(&s_w[0][0]);
+    auto swb = [&](int i) -> unsigned { return sw0 + (unsigned)(i % 3) * (16 * 128 * 2); };
+    float act[8][8];
+    f32x4 acc[16];
+    // g8, natural order: act[ks][j] = row 32 ks + 8 q + j of the heads' gradient (58 rows; zero past them and P)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = 32 * ks + 8 * q + j;
+            const int k = n < 3 ? 0 : (n < 6 ? 1 : (n < 10 ? 2 : 3));
+            const int c0 = k == 0 ? 0 : (k == 1 ? 3 : (k == 2 ? 6 : 10));
+            const float* src = p.heads.src[k];
+            act[ks][j] = (g < p.P && n < 58 && src) ? src[(size_t)g * p.heads.ld[k] + (n - c0)] : 0.f;
+        }
+#pragma unroll
+    for (int ks = 2; ks < 8; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) act[ks][j] = 0.f;
+    __builtin_amdgcn_s_waitcnt(0xf70);   // plain loads done before the first copy
+    chain16_words(p.bits[0], ldp, wave, voff_w2, swb(0));   // retired with the prologue's wait
+    auto prologue = [&](const char* f0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                dma16_sa(f0 + k * (kF16Step * 16) + 8192 * i, voff_dma,
+                         __builtin_amdgcn_readfirstlane(lds_addr(s_mem) + k * kF16Slot + (wave + 8 * i) * 1024));
+        wait_vm_c<6>();
+        raw_barrier();
+    };
+    auto F = [&](int i) { return reinterpret_cast<const char*>(p.frags[i]); };
+    // phase A: steps 0-2 (layers 8, 7, 6)
+    prologue(F(0));
+    chain16_step<2, true, false, true, 0>(F(0), F(1), p.G[0], ldp, s_mem, 0, wave, lane, voff_dma, voff_n, p.bits[1],
+                                          voff_w2, swb(1), act, acc);
+    chain16_mask(s_w[0], gl, q, acc, act);
+    chain16_step<8, false, false, true, 8>(F(1), F(2), p.G[1], ldp, s_mem, 2, wave, lane, voff_dma, voff_a, p.bits[2],
+                                           voff_w2, swb(2), act, acc);
+    chain16_mask(s_w[1], gl, q, acc, act);
+    chain16_step<8, false, true, true, 8>(F(2), F(2), p.G[2], ldp, s_mem, 10, wave, lane, voff_dma, voff_a, p.bits[3],
+                                          voff_w2, swb(3), act, acc);
+    chain16_mask(s_w[2], gl, q, acc, act);   // g5
+    {   // W5^T's enc(x) rows times g5 -> dE (added to at the end)
+        f32x4 he[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
+        chain16_enc_pass<false>(reinterpret_cast<const char*>(p.frags_e5), s_mem, wave, lane, voff_dma, nullptr, ldp,
+                                voff_a, act, he);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) store_row(he[r][i], p.dE, voff_a, (16 * r + i) * ldp);
+    }
+    // phase B: steps 3-7 (layers 5 .. 1)
+    prologue(F(3));
+    chain16_step<8, false, false, true, 0>(F(3), F(4), p.G[3], ldp, s_mem, 0, wave, lane, voff_dma, voff_a, p.bits[4],
+                                           voff_w2, swb(4), act, acc);
+    chain16_mask(s_w[0], gl, q, acc, act);
+#pragma unroll 1
+    for (int i = 4; i < 7; ++i) {
+        chain16_step<8, false, false, true, 8>(F(i), F(i + 1), p.G[i], ldp, s_mem, 8 * (i - 3), wave, lane, voff_dma,
+                                               voff_a, p.bits[i + 1], voff_w2, swb(i + 1), act, acc);
+        chain16_mask(reinterpret_cast<const unsigned short*>(s_w) + (i % 3) * (16 * 128), gl, q, acc, act);
+    }
+    chain16_step<8, false, true, false, 8>(F(7), F(7), p.G[7], ldp, s_mem, 32, wave, lane, voff_dma, voff_a, p.bits[7],
+                                           voff_w2, swb(8), act, acc);
+    chain16_mask(s_w[1], gl, q, acc, act);   // g0 (step 7: buffer 7 % 3)
+    // the final pass: W0^T's enc(x) rows times g0, added to the layer-5 part in dE; g0's rows stored under it
+    f32x4 ho[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ho[r][i] = load_row(p.dE, voff_a, (16 * r + i) * ldp);
+    chain16_enc_pass<true>(reinterpret_cast<const char*>(p.frags_e), s_mem, wave, lane, voff_dma, p.G[8], ldp, voff_a,
+                           act, ho);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) store_row(ho[r][i], p.dE, voff_a, (16 * r + i) * ldp);
 }
 
 // ---- dW = G X^T (split-K over Gaussian chunks) and db = row sums of G ----
@@ -1358,9 +1916,17 @@ void launch_mlp_fwd_fused(const MlpFusedParams& p, hipStream_t s, bool store) {
     if (store) hipLaunchKernelGGL(k_mlp_fwd_fused<true>, dim3(p.ldp / 128), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(k_mlp_fwd_fused<false>, dim3(p.ldp / 128), dim3(256), 0, s, p);
 }
+void launch_mlp_fwd_fused16(const MlpFusedParams& p, hipStream_t s, bool store) {
+    if (p.P <= 0) return;
+    if (store) hipLaunchKernelGGL(k_mlp_fwd_fused16<true>, dim3(p.ldp / 128), dim3(512), 0, s, p);
+    else hipLaunchKernelGGL(k_mlp_fwd_fused16<false>, dim3(p.ldp / 128), dim3(512), 0, s, p);
+}
 
 void launch_mlp_bwd_chain(const MlpChainParams& p, hipStream_t s) {
     if (p.P > 0) hipLaunchKernelGGL(k_mlp_bwd_chain, dim3(p.ldp / 128), dim3(256), 0, s, p);
+}
+void launch_mlp_bwd_chain16(const MlpChainParams& p, hipStream_t s) {
+    if (p.P > 0) hipLaunchKernelGGL(k_mlp_bwd_chain16, dim3(p.ldp / 128), dim3(512), 0, s, p);
 }
 
 void launch_mlp_gemm(const MlpGemmParams& p, int mode, hipStream_t s) {

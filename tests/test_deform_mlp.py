@@ -4,6 +4,7 @@ shapes, scene/gaussian_model.py:242-276).  The reference module itself cannot be
 needs plyfile / FrEIA / simple_knn), so parity is pinned by restatement; CPU."""
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from conftest import PKG  # noqa: F401
@@ -231,3 +232,191 @@ def test_se3net_padded_weights_compute_the_same_network_cpu():
     w = h @ ws[8].t() + bs[8]
     v = h @ ws[9].t() + bs[9]
     assert _rel(w, g["w"]) <= 1e-5 and _rel(v, g["v"]) <= 1e-5
+
+
+# ---- k_mlp_fwd_fused16 / k_mlp_bwd_chain16 operand maps (gsd_mlp_train.hip, round 6), emulated on the CPU ----
+# The lane maps of v_mfma_f32_16x16x32_bf16 (cdna_hip_programming.md §3): lane l holds A[l & 15][8 (l >> 4) + j],
+# B[8 (l >> 4) + j][l & 15], and C[4 (l >> 4) + i][l & 15].  The emulation restates k_mlp_pack's m16 fragment index,
+# the kernels' B operands (natural or the accumulator order), their epilogue / mask word layout, and multiplies in
+# float64 (the BF16x6 split is the same as the 32-wide kernels' and is not what is checked here).
+_LQ, _LC = np.arange(64) >> 4, np.arange(64) & 15
+
+
+def _pack_m16(A, perm_from):
+    """k_mlp_pack with m16: frag[ks, rb, lane, j] = A[16 rb + (lane & 15), kcol(ks, lane >> 4, j)]."""
+    M, K = A.shape
+    out = np.zeros((K // 32, M // 16, 64, 8))
+    for ks in range(K // 32):
+        for j in range(8):
+            k = 32 * ks + (16 * (j >> 2) + 4 * _LQ + (j & 3) if ks >= perm_from else 8 * _LQ + j)
+            for rb in range(M // 16):
+                out[ks, rb, :, j] = A[16 * rb + _LC, k]
+    return out
+
+
+def _mfma16(frag, breg):
+    """(64, 8) A fragment x (64, 8) B operand -> (64, 4) accumulator registers of one 16 x 16 x 32 product."""
+    A = np.zeros((16, 32))
+    B = np.zeros((32, 16))
+    for j in range(8):
+        A[_LC, 8 * _LQ + j] = frag[:, j]
+        B[8 * _LQ + j, _LC] = breg[:, j]
+    C = A @ B
+    return np.stack([C[4 * _LQ + i, _LC] for i in range(4)], -1)
+
+
+def _run16(frags, operands):
+    """A layer's k-steps: acc[rb] (64, 4) = sum over k-steps of frag[ks, rb] x operands[ks]."""
+    KS, RB = frags.shape[:2]
+    acc = np.zeros((RB, 64, 4))
+    for ks in range(KS):
+        for rb in range(RB):
+            acc[rb] += _mfma16(frags[ks, rb], operands[ks])
+    return acc
+
+
+def _epilogue16(acc, bias):
+    """fused16_epilogue: act[k][lane][4 a + i] = relu(acc[2 k + a] + bias[16 (2 k + a) + 4 q + i]) and the ReLU words
+    (word 2 k + (q & 1), lane halves combined as __shfl_xor(w, 32) does)."""
+    act = np.zeros((8, 64, 8))
+    bits = np.zeros((8, 64), dtype=np.int64)
+    for k in range(8):
+        w = np.zeros(64, dtype=np.int64)
+        for a in range(2):
+            for i in range(4):
+                y = np.maximum(acc[2 * k + a][:, i] + bias[16 * (2 * k + a) + 4 * _LQ + i], 0.0)
+                act[k][:, 4 * a + i] = y
+                w |= (y > 0).astype(np.int64) << (8 * a + i)
+        w <<= 4 * (_LQ >> 1)
+        bits[k] = w | w[np.arange(64) ^ 32]
+    return act, bits
+
+
+def _padded_layers(net):
+    """The kernels' A matrices in float64: layer 0 [enc(x) 63 | 0 | enc(t) 21 | 0 x 11], layer 5 [enc(x) 63 | 0 | h
+    256], the heads' 58 rows padded to 64; and the biases (heads padded)."""
+    Ws = [l.weight.detach().double().numpy() for l in net._time]
+    bs = [l.bias.detach().double().numpy() for l in net._time]
+    A = []
+    for i, w in enumerate(Ws):
+        if i == 0:
+            a = np.zeros((256, 96))
+            a[:, :63], a[:, 64:85] = w[:, :63], w[:, 63:]
+        elif i == 5:
+            a = np.zeros((256, 320))
+            a[:, :63], a[:, 64:] = w[:, :63], w[:, 63:]
+        else:
+            a = w
+        A.append(a)
+    heads = (net._time_out, net._time_out_scale, net._time_out_rot, net._time_out_shs)
+    wh = np.zeros((64, 256))
+    wh[:58] = torch.cat([m.weight for m in heads]).detach().double().numpy()
+    bh = np.zeros(64)
+    bh[:58] = torch.cat([m.bias for m in heads]).detach().double().numpy()
+    return A + [wh], bs + [bh]
+
+
+def test_fused16_and_chain16_maps_emulated():
+    """k_mlp_fwd_fused16's and k_mlp_bwd_chain16's operand maps, emulated lane by lane for one wave of 16 Gaussians:
+    the m16 packing (natural and accumulator-order k, the transposed W^T with layer 5's row offset), the B operands
+    chained from the accumulators with no lane movement, the ReLU words (checked against k_mlp_fwd_fused's layout:
+    word 2 rb + h, bit 4 q4 + i = row 32 rb + 8 q4 + 4 h + i) and the chain's mask read back from the words' rows.
+    The heads and the encoding's gradient equal float64 autograd of the network."""
+    from gsd_amd.deform_mlp import DirectTemporalNeRF, positional_encoding
+    torch.manual_seed(12)
+    net = DirectTemporalNeRF().double()
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(2.0)
+    x = torch.rand(16, 3, dtype=torch.float64) * 2 - 1
+    t = torch.full((16, 1), 0.45, dtype=torch.float64)
+    ex = positional_encoding(x).detach().requires_grad_(True)
+    et = positional_encoding(t)
+    # float64 reference: heads and d(sum(heads . wg)) / d enc(x)
+    h = torch.cat((ex, et), -1)
+    hs = []
+    for i, layer in enumerate(net._time):
+        h = torch.relu(layer(h))
+        hs.append(h)
+        if i in net.skips:
+            h = torch.cat((ex, h), -1)
+    heads = (net._time_out, net._time_out_scale, net._time_out_rot, net._time_out_shs)
+    ref = torch.cat([m(h) for m in heads], -1)
+    wg = torch.randn(16, 58, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
+    (ref * wg).sum().backward()
+    ref_dE = ex.grad.numpy()
+    A, b = _padded_layers(net)
+    E = np.zeros((64, 16))
+    E[:63] = ex.detach().numpy().T
+    ET = np.zeros((32, 16))
+    ET[:21] = et.numpy().T
+    # ---- forward (k_mlp_fwd_fused16) ----
+    xe = [E[32 * s + 8 * _LQ[:, None] + np.arange(8)[None, :], _LC[:, None]] for s in range(2)]
+    xt = ET[8 * _LQ[:, None] + np.arange(8)[None, :], _LC[:, None]]
+    acc = _run16(_pack_m16(A[0], 1 << 30), [xe[0], xe[1], xt])
+    words = {}
+    for l in range(1, 8):
+        act, bits = _epilogue16(acc, b[l - 1])
+        words[l] = bits   # h_l's ReLU words
+        ops = ([xe[0], xe[1]] if l == 5 else []) + [act[k] for k in range(8)]
+        act7 = act   # layer 7's B operand (h_7), for the negative check below
+        acc = _run16(_pack_m16(A[l], 2 if l == 5 else 0), ops)
+    act, bits = _epilogue16(acc, b[7])
+    words[8] = bits
+    # a wrong k order is caught: layer 7 packed in the natural order (its B operand is in the accumulator order)
+    bad, _ = _epilogue16(_run16(_pack_m16(A[7], 1 << 30), [act7[k] for k in range(8)]), b[7])
+    assert np.abs(bad - act).max() > 0.1 * np.abs(act).max()
+    ho = _run16(_pack_m16(A[8], 0), [act[k] for k in range(8)])
+    got = np.zeros((16, 64))
+    for r in range(4):
+        for i in range(4):
+            got[_LC, 16 * r + 4 * _LQ + i] = ho[r][:, i] + b[8][16 * r + 4 * _LQ + i]
+    ref = ref.detach().numpy()
+    np.testing.assert_allclose(got[:, :58], ref, rtol=0, atol=1e-9 * float(np.abs(ref).max()))
+    # the words in k_mlp_fwd_fused's layout, from the float64 hidden outputs
+    for l in range(1, 9):
+        hl = hs[l - 1].detach().numpy()   # (16, 256): h_l
+        for k in range(8):
+            for hh in range(2):
+                lanes = np.where((_LQ & 1) == hh)[0]
+                for cc in range(16):
+                    want = sum(int(hl[cc, 32 * k + 8 * (bit >> 2) + 4 * hh + (bit & 3)] > 0) << bit
+                               for bit in range(16))
+                    assert all(words[l][k][lanes[lanes & 15 == cc]] == want), (l, k, hh, cc)
+
+    # ---- backward chain (k_mlp_bwd_chain16) ----
+    def rows16(words_l):   # the [16][Gaussian] u16 rows chain16_words copies to LDS: row 2 k + h
+        rows = np.zeros((16, 16), dtype=np.int64)
+        for k in range(8):
+            for ln in range(64):
+                rows[2 * k + (_LQ[ln] & 1), _LC[ln]] = words_l[k][ln]
+        return rows
+
+    def mask(acc, rows):   # chain16_mask
+        out = np.zeros((8, 64, 8))
+        for k in range(8):
+            wk = rows[2 * k + (_LQ & 1), _LC] >> (4 * (_LQ >> 1))
+            for a in range(2):
+                for i in range(4):
+                    out[k][:, 4 * a + i] = np.where((wk >> (8 * a + i)) & 1, acc[2 * k + a][:, i], 0.0)
+        return out
+
+    g8 = np.zeros((64, 16))
+    g8[:58] = wg.numpy().T
+    gops = [g8[32 * s + 8 * _LQ[:, None] + np.arange(8)[None, :], _LC[:, None]] for s in range(2)]
+    acc = _run16(_pack_m16(A[8].T, 1 << 30), gops)   # W8^T (256 x 64), natural k
+    act = mask(acc, rows16(words[8]))                 # g7
+    dE = None
+    for L in range(7, 0, -1):
+        if L == 5:   # W5^T's enc(x) rows (0-63) times g5
+            he = _run16(_pack_m16(A[5].T[:64], 0), [act[k] for k in range(8)])
+            dE = he
+        AT = A[L].T[64:] if L == 5 else A[L].T   # layer 5: the h rows (m_off 64)
+        acc = _run16(_pack_m16(AT, 0), [act[k] for k in range(8)])
+        act = mask(acc, rows16(words[L]))        # g_{L-1}
+    dE = dE + _run16(_pack_m16(A[0].T[:64], 0), [act[k] for k in range(8)])
+    got_dE = np.zeros((16, 64))
+    for r in range(4):
+        for i in range(4):
+            got_dE[_LC, 16 * r + 4 * _LQ + i] = dE[r][:, i]
+    np.testing.assert_allclose(got_dE[:, :63], ref_dE, rtol=0, atol=1e-9 * float(np.abs(ref_dE).max()))
