@@ -793,6 +793,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 // so row blocks 2 s and 2 s + 1 of a layer's output are the next layer's k-step s with no lane movement.  The hidden
 // outputs and ReLU words go to HBM in the layouts k_mlp_fwd_fused writes (the backward reads them unchanged).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// the layer loops of the 16-wide kernels: one copy of a layer's code in the product; GSD_MLP_UNROLL_LAYERS (a check
+// build only, tests/test_codegen.py) unrolls them so that the text order of the code is its issue order
+#ifdef GSD_MLP_UNROLL_LAYERS
+#define GSD_LAYER_LOOP _Pragma("unroll")
+#else
+#define GSD_LAYER_LOOP _Pragma("unroll 1")
+#endif
 constexpr int kF16Step = 16 * 3 * 64;   // bf16x8 per hidden k-step (48 KB)
 constexpr int kF16Slot = 48 * 1024;
 
@@ -928,7 +935,7 @@ __device__ __forceinline__ void fused16_layer(const MlpFusedParams& p, unsigned 
             a = an;
         }
         b = bn;
-        wait_vm_u(f16_stores(KSE, ks - 1, PREV) + 6 + f16_stores(KSE, ks, PREV));
+        wait_vm_u((ST ? f16_stores(KSE, ks - 1, PREV) + f16_stores(KSE, ks, PREV) : 0) + 6);
         raw_barrier();
     }
 }
@@ -999,7 +1006,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_fused16(MlpFusedParams p) {
     fused16_epilogue(s_bias, q, acc, act, bits);
     fused16_layer<0, 8, 0, kStore>(p, s_mem, 3, 1, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt, act, bits, acc);
     fused16_epilogue(s_bias + 256, q, acc, act, bits);
-#pragma unroll 1
+GSD_LAYER_LOOP
     for (int l = 2; l <= 4; ++l) {
         fused16_layer<0, 8, PV, kStore>(p, s_mem, 3 + 8 * (l - 1), l, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt,
                                         act, bits, acc);
@@ -1007,7 +1014,7 @@ __global__ __launch_bounds__(512) void k_mlp_fwd_fused16(MlpFusedParams p) {
     }
     fused16_layer<2, 8, PV, kStore>(p, s_mem, 35, 5, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt, act, bits, acc);
     fused16_epilogue(s_bias + 256 * 5, q, acc, act, bits);
-#pragma unroll 1
+GSD_LAYER_LOOP
     for (int l = 6; l <= 7; ++l) {
         fused16_layer<0, 8, PV, kStore>(p, s_mem, 45 + 8 * (l - 6), l, wave, lane, voff_dma, voff_h, voff_b, bit_lane, xe, xt,
                                         act, bits, acc);
@@ -1580,7 +1587,7 @@ __global__ __launch_bounds__(512) void k_mlp_bwd_chain16(MlpChainParams p) {
     chain16_step<8, false, false, true, 0>(F(3), F(4), p.G[3], ldp, s_mem, 0, wave, lane, voff_dma, voff_a, p.bits[4],
                                            voff_w2, swb(4), act, acc);
     chain16_mask(s_w[0], gl, q, acc, act);
-#pragma unroll 1
+GSD_LAYER_LOOP
     for (int i = 4; i < 7; ++i) {
         chain16_step<8, false, false, true, 8>(F(i), F(i + 1), p.G[i], ldp, s_mem, 8 * (i - 3), wave, lane, voff_dma,
                                                voff_a, p.bits[i + 1], voff_w2, swb(i + 1), act, acc);
